@@ -1,0 +1,121 @@
+"""ctypes binding of libavr_hip.so (include/avr.h).
+
+The library is built in-tree (`make -C adaptive-volume-rendering_amd`, or
+__graft_entry__.build()) and loaded from this directory. There is no fallback:
+if the library or a HIP device is missing, every op raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libavr_hip.so")
+AVR_MAX_BLOCKS = 8
+ABI_VERSION = 1
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+c_void_p = ctypes.c_void_p
+i64 = ctypes.c_int64
+u64 = ctypes.c_uint64
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+
+
+class FieldDims(ctypes.Structure):
+    _fields_ = [("d_in", c_int), ("d_latent", c_int), ("d_hidden", c_int), ("n_blocks", c_int),
+                ("n_lin_z", c_int), ("num_freqs", c_int), ("freq_factor", c_float)]
+
+
+class ResnetFCWeights(ctypes.Structure):
+    _fields_ = [("lin_in_w", c_void_p), ("lin_in_b", c_void_p), ("lin_out_w", c_void_p), ("lin_out_b", c_void_p),
+                ("fc0_w", c_void_p * AVR_MAX_BLOCKS), ("fc0_b", c_void_p * AVR_MAX_BLOCKS),
+                ("fc1_w", c_void_p * AVR_MAX_BLOCKS), ("fc1_b", c_void_p * AVR_MAX_BLOCKS),
+                ("lin_z_w", c_void_p * AVR_MAX_BLOCKS), ("lin_z_b", c_void_p * AVR_MAX_BLOCKS)]
+
+
+class ViewDesc(ctypes.Structure):
+    _fields_ = [("poses", c_float * 12), ("focal", c_float * 2), ("c", c_float * 2), ("image_shape", c_float * 2),
+                ("latent_scaling", c_float * 2), ("latent_h", c_int), ("latent_w", c_int)]
+
+
+# name -> argtypes (all return int status)
+_SIGS = {
+    "avr_world_rays": [c_void_p, c_void_p, c_void_p, i64, i64, i64, i64, c_void_p, c_void_p, c_void_p],
+    "avr_depth_from_world": [c_void_p, c_void_p, c_void_p, c_void_p, i64, i64, i64, i64, c_void_p, c_void_p,
+                             c_void_p],
+    "avr_sample_coarse": [c_float, c_float, i64, c_int, c_void_p, u64, u64, c_void_p, c_void_p],
+    "avr_sample_fine": [c_void_p, c_void_p, c_float, c_float, i64, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                        c_void_p, u64, u64, c_void_p, c_void_p, c_void_p, c_void_p],
+    "avr_composite_fwd": [c_void_p, c_void_p, i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    "avr_composite_bwd": [c_void_p, c_void_p, i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p],
+    "avr_field_packed_floats": [ctypes.POINTER(FieldDims), ctypes.POINTER(i64)],
+    "avr_field_pack": [ctypes.POINTER(FieldDims), ctypes.POINTER(ResnetFCWeights), c_void_p, c_void_p],
+    "avr_field_latent_table": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "avr_field_fwd_rays": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p],
+    "avr_field_fwd_points": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
+                             c_void_p, i64, c_void_p, c_void_p],
+}
+EXPORTED = ("avr_version", "avr_last_error_string", "avr_device_count") + tuple(_SIGS)
+
+_lib = None
+
+
+class AVRError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load (once) and return the ctypes handle. Raises if the .so is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise AVRError(f"libavr_hip.so not built at {path}: run `make -C adaptive-volume-rendering_amd` "
+                       "(or __graft_entry__.build()); there is no non-HIP fallback")
+    torch.cuda.is_available()  # make torch's HIP runtime the one the library binds to
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    lib.avr_version.restype = c_int
+    lib.avr_last_error_string.restype = ctypes.c_char_p
+    lib.avr_device_count.restype = c_int
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = c_int
+    if lib.avr_version() != ABI_VERSION:
+        raise AVRError(f"libavr_hip.so ABI {lib.avr_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().avr_last_error_string().decode(errors="replace")
+        raise AVRError(f"{what} failed (code {rc}): {msg}")
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args), name)
+
+
+def stream_of(t):
+    """hipStream_t of torch's current stream on t's device."""
+    return c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def require_device(*tensors):
+    """Every tensor must be a contiguous fp32 (or int32) tensor on a HIP device."""
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise AVRError("avr kernels need tensors on a ROCm/HIP device (got device %s); there is no CPU path"
+                           % t.device)
+        if not t.is_contiguous():
+            raise AVRError("avr kernels need contiguous tensors")

@@ -1,0 +1,364 @@
+"""The PixelNeRF radiance field the renderer drives (models.py:41-87, 407-606,
+609-863 of the reference), with the same module tree and state_dict keys so
+reference checkpoints load (`strict=False`: the per-scene ResNet34 encoder is
+out of scope and replaced by a latent holder).
+
+`NewPixelNeRFNet.forward(xyz, coarse, viewdirs)` keeps the reference protocol:
+(SB, B, 3) points -> (SB, B, 4) = (sigmoid rgb, relu sigma). Under no_grad on
+a HIP device it runs the fused fp32-MFMA kernel (avr.field); with autograd it
+runs the module's PyTorch graph so train.py can back-propagate through it.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .conf import Conf
+
+
+def repeat_interleave(x, repeats, dim=0):
+    """utils.py:62-69: repeat each entry `repeats` times along dim 0."""
+    out = x.unsqueeze(1).expand(-1, repeats, *x.shape[1:])
+    return out.reshape(-1, *x.shape[1:])
+
+
+def combine_interleaved(t, inner_dims=(1,), agg_type="average"):
+    """utils.py:71-81: mean/max over the NS interleaved source views."""
+    if len(inner_dims) == 1 and inner_dims[0] == 1:
+        return t
+    t = t.reshape(-1, *inner_dims, *t.shape[1:])
+    if agg_type == "average":
+        return torch.mean(t, dim=1)
+    if agg_type == "max":
+        return torch.max(t, dim=1)[0]
+    raise NotImplementedError("Unsupported combine type " + agg_type)
+
+
+class PositionalEncoding(nn.Module):
+    """models.py:41-87: [x, sin(f_k x), sin(f_k x + pi/2), ...], f_k = freq_factor * 2^k."""
+
+    def __init__(self, num_freqs=6, d_in=3, freq_factor=np.pi, include_input=True):
+        super().__init__()
+        self.num_freqs, self.d_in, self.include_input = num_freqs, d_in, include_input
+        self.freq_factor = float(freq_factor)
+        self.freqs = freq_factor * 2.0 ** torch.arange(0, num_freqs)
+        self.d_out = num_freqs * 2 * d_in + (d_in if include_input else 0)
+        self.register_buffer("_freqs", torch.repeat_interleave(self.freqs, 2).view(1, -1, 1))
+        ph = torch.zeros(2 * num_freqs)
+        ph[1::2] = np.pi * 0.5
+        self.register_buffer("_phases", ph.view(1, -1, 1))
+
+    def forward(self, x):
+        emb = torch.addcmul(self._phases, x.unsqueeze(1).repeat(1, self.num_freqs * 2, 1), self._freqs)
+        emb = torch.sin(emb).view(x.shape[0], -1)
+        return torch.cat((x, emb), dim=-1) if self.include_input else emb
+
+    @classmethod
+    def from_conf(cls, conf, d_in=3):
+        return cls(conf.get_int("num_freqs", 6), d_in, conf.get_float("freq_factor", np.pi),
+                   conf.get_bool("include_input", True))
+
+
+class ResnetBlockFC(nn.Module):
+    """models.py:407-470 (fc_1 zero-initialised as in the reference)."""
+
+    def __init__(self, size_in, size_out=None, size_h=None, bn=False, beta=0.0):
+        super().__init__()
+        size_out = size_in if size_out is None else size_out
+        size_h = min(size_in, size_out) if size_h is None else size_h
+        self.bn, self.size_in, self.size_h, self.size_out = bn, size_in, size_h, size_out
+        self.bn_0 = nn.BatchNorm1d(size_in)
+        self.fc_0 = nn.Linear(size_in, size_h)
+        self.bn_1 = nn.BatchNorm1d(size_h)
+        self.fc_1 = nn.Linear(size_h, size_out)
+        nn.init.constant_(self.fc_0.bias, 0.0)
+        nn.init.kaiming_normal_(self.fc_0.weight, a=0, mode="fan_in")
+        nn.init.constant_(self.fc_1.bias, 0.0)
+        nn.init.zeros_(self.fc_1.weight)
+        self.activation = nn.Softplus(beta=beta) if beta > 0 else nn.ReLU()
+        self.shortcut = None if size_in == size_out else nn.Linear(size_in, size_out, bias=False)
+
+    def forward(self, x):
+        if self.bn:
+            net = self.fc_0(self.activation(self.bn_0(x.reshape(-1, self.size_in)).reshape(x.shape)))
+            dx = self.fc_1(self.activation(self.bn_0(net.reshape(-1, self.size_h)).reshape(net.shape)))
+        else:
+            dx = self.fc_1(self.activation(self.fc_0(self.activation(x))))
+        xs = x if self.shortcut is None else self.shortcut(x)
+        return xs + dx
+
+
+class ResnetFC(nn.Module):
+    """models.py:473-606."""
+
+    def __init__(self, d_in, d_out=4, n_blocks=5, d_latent=0, d_hidden=128, bn=False, beta=0.0,
+                 combine_layer=1000, combine_type="average", use_spade=False):
+        super().__init__()
+        if d_in > 0:
+            self.lin_in = nn.Linear(d_in, d_hidden)
+            nn.init.constant_(self.lin_in.bias, 0.0)
+            nn.init.kaiming_normal_(self.lin_in.weight, a=0, mode="fan_in")
+        self.lin_out = nn.Linear(d_hidden, d_out)
+        nn.init.constant_(self.lin_out.bias, 0.0)
+        nn.init.kaiming_normal_(self.lin_out.weight, a=0, mode="fan_in")
+        self.n_blocks, self.d_latent, self.d_in, self.d_out, self.d_hidden = n_blocks, d_latent, d_in, d_out, d_hidden
+        self.combine_layer, self.combine_type, self.use_spade, self.beta, self.bn = (
+            combine_layer, combine_type, use_spade, beta, bn)
+        self.blocks = nn.ModuleList([ResnetBlockFC(d_hidden, bn=bn, beta=beta) for _ in range(n_blocks)])
+        if d_latent != 0:
+            n_lin_z = min(combine_layer, n_blocks)
+            self.lin_z = nn.ModuleList([nn.Linear(d_latent, d_hidden) for _ in range(n_lin_z)])
+            for lz in self.lin_z:
+                nn.init.constant_(lz.bias, 0.0)
+                nn.init.kaiming_normal_(lz.weight, a=0, mode="fan_in")
+            if use_spade:
+                self.scale_z = nn.ModuleList([nn.Linear(d_latent, d_hidden) for _ in range(n_lin_z)])
+                for sz in self.scale_z:
+                    nn.init.constant_(sz.bias, 0.0)
+                    nn.init.kaiming_normal_(sz.weight, a=0, mode="fan_in")
+        self.activation = nn.Softplus(beta=beta) if beta > 0 else nn.ReLU()
+
+    def forward(self, zx, combine_inner_dims=(1,), combine_index=None, dim_size=None):
+        assert zx.size(-1) == self.d_latent + self.d_in
+        if self.d_latent > 0:
+            z, x = zx[..., :self.d_latent], zx[..., self.d_latent:]
+        else:
+            z, x = None, zx
+        x = self.lin_in(x) if self.d_in > 0 else torch.zeros(self.d_hidden, device=zx.device)
+        for b in range(self.n_blocks):
+            if b == self.combine_layer:
+                x = combine_interleaved(x, combine_inner_dims, self.combine_type)
+            if self.d_latent > 0 and b < self.combine_layer:
+                tz = self.lin_z[b](z)
+                x = self.scale_z[b](z) * x + tz if self.use_spade else x + tz
+            x = self.blocks[b](x)
+        return self.lin_out(self.activation(x))
+
+    @classmethod
+    def from_conf(cls, conf, d_in, **kwargs):
+        return cls(d_in, n_blocks=conf.get_int("n_blocks", 5), d_hidden=conf.get_int("d_hidden", 128),
+                   beta=conf.get_float("beta", 0.0), combine_layer=conf.get_int("combine_layer", 1000),
+                   combine_type=conf.get_string("combine_type", "average"),
+                   use_spade=conf.get_bool("use_spade", False), **kwargs)
+
+
+class LatentEncoder(nn.Module):
+    """Holds the per-scene feature map that SpatialEncoder.forward
+    (models.py:276-329) would produce, and samples it like SpatialEncoder.index
+    (models.py:245-274). The ResNet34 itself is out of scope (per-scene CNN)."""
+
+    def __init__(self, latent_size=512, index_interp="bilinear", index_padding="border"):
+        super().__init__()
+        self.latent_size = latent_size
+        self.index_interp, self.index_padding = index_interp, index_padding
+        self.register_buffer("latent", torch.empty(1, 1, 1, 1), persistent=False)
+        self.register_buffer("latent_scaling", torch.empty(2, dtype=torch.float32), persistent=False)
+
+    def set_latent(self, latent):
+        self.latent = latent
+        ls = torch.tensor([latent.shape[-1], latent.shape[-2]], dtype=torch.float32, device=latent.device)
+        self.latent_scaling = ls / (ls - 1) * 2.0
+        return self.latent
+
+    def index(self, uv, cam_z=None, image_size=(), z_bounds=None):
+        if uv.shape[0] == 1 and self.latent.shape[0] > 1:
+            uv = uv.expand(self.latent.shape[0], -1, -1)
+        if len(image_size) > 0:
+            if len(image_size) == 1:
+                image_size = (image_size, image_size)
+            uv = uv * (self.latent_scaling / image_size) - 1.0
+        samples = F.grid_sample(self.latent, uv.unsqueeze(2), align_corners=True, mode=self.index_interp,
+                                padding_mode=self.index_padding)
+        return samples[:, :, :, 0]
+
+
+def make_mlp(conf, d_in, d_latent=0, allow_empty=False, bn=False, **kwargs):
+    """models.py:18-28 (the resnet type; 'mlp' ImplicitNet is not part of this path)."""
+    mlp_type = conf.get_string("type", "mlp")
+    if mlp_type == "resnet":
+        return ResnetFC.from_conf(conf, d_in, d_latent=d_latent, bn=bn, **kwargs)
+    if mlp_type == "empty" and allow_empty:
+        return None
+    raise NotImplementedError(f"Unsupported MLP type {mlp_type!r} (only 'resnet' is on the hot path)")
+
+
+class NewPixelNeRFNet(nn.Module):
+    """models.py:609-863 with the encoder replaced by LatentEncoder."""
+
+    def __init__(self, conf, stop_encoder_grad=False, bn=False):
+        super().__init__()
+        conf = conf if hasattr(conf, "get_bool") else Conf(conf)
+        enc = conf["encoder"] if "encoder" in conf else Conf({})
+        num_layers = enc.get_int("num_layers", 4)
+        self.encoder = LatentEncoder([0, 64, 128, 256, 512, 1024][num_layers],
+                                     enc.get_string("index_interp", "bilinear"),
+                                     enc.get_string("index_padding", "border"))
+        self.use_encoder = conf.get_bool("use_encoder", True)
+        self.use_xyz = conf.get_bool("use_xyz", False)
+        assert self.use_encoder or self.use_xyz
+        self.normalize_z = conf.get_bool("normalize_z", True)
+        self.stop_encoder_grad = stop_encoder_grad
+        self.use_code = conf.get_bool("use_code", False)
+        self.use_code_viewdirs = conf.get_bool("use_code_viewdirs", True)
+        self.use_viewdirs = conf.get_bool("use_viewdirs", False)
+        self.use_global_encoder = conf.get_bool("use_global_encoder", False)
+        if self.use_global_encoder:
+            raise NotImplementedError("global image encoder is out of scope")
+        d_latent = self.encoder.latent_size if self.use_encoder else 0
+        d_in = 3 if self.use_xyz else 1
+        if self.use_viewdirs and self.use_code_viewdirs:
+            d_in += 3
+        if self.use_code and d_in > 0:
+            self.code = PositionalEncoding.from_conf(conf["code"], d_in=d_in)
+            d_in = self.code.d_out
+        if self.use_viewdirs and not self.use_code_viewdirs:
+            d_in += 3
+        self.latent_size = self.encoder.latent_size
+        self.mlp_coarse = make_mlp(conf["mlp_coarse"], d_in, d_latent, d_out=4, bn=bn)
+        self.mlp_fine = make_mlp(conf["mlp_fine"], d_in, d_latent, d_out=4, allow_empty=True, bn=bn)
+        self.register_buffer("poses", torch.empty(1, 3, 4), persistent=False)
+        self.register_buffer("image_shape", torch.empty(2), persistent=False)
+        self.register_buffer("focal", torch.empty(1, 2), persistent=False)
+        self.register_buffer("c", torch.empty(1, 2), persistent=False)
+        self.d_in, self.d_out, self.d_latent = d_in, 4, d_latent
+        self.num_objs, self.num_views_per_obj = 0, 1
+        self.use_fused = True  # HIP field under no_grad (avr.field)
+        self._fused = None
+
+    def encode_latent(self, latent, poses, focal, c=None, image_shape=None):
+        """The pose / focal / principal-point bookkeeping of encode()
+        (models.py:692-734) for a precomputed latent (NS, L, H, W)."""
+        self.num_objs = latent.size(0)
+        self.num_views_per_obj = 1
+        self.encoder.set_latent(latent)
+        rot = poses[:, :3, :3].transpose(1, 2)
+        trans = -torch.bmm(rot, poses[:, :3, 3:])
+        self.poses = torch.cat((rot, trans), dim=-1)
+        if image_shape is None:
+            image_shape = (latent.shape[-1] * 2, latent.shape[-2] * 2)  # ResNet conv1 stride 2
+        self.image_shape = torch.tensor([float(image_shape[0]), float(image_shape[1])], device=latent.device)
+        focal = torch.as_tensor(focal, dtype=torch.float32, device=latent.device)
+        if focal.dim() == 0:
+            focal = focal[None, None].repeat((1, 2))
+        elif focal.dim() == 1:
+            focal = focal.unsqueeze(-1).repeat((1, 2))
+        else:
+            focal = focal.clone()
+        self.focal = focal.float()
+        self.focal[..., 1] *= -1.0
+        if c is None:
+            c = (self.image_shape * 0.5).unsqueeze(0)
+        else:
+            c = torch.as_tensor(c, dtype=torch.float32, device=latent.device)
+            if c.dim() == 0:
+                c = c[None, None].repeat((1, 2))
+            elif c.dim() == 1:
+                c = c.unsqueeze(-1).repeat((1, 2))
+        self.c = c
+
+    def encode(self, images, poses, focal, z_bounds=None, c=None):
+        raise NotImplementedError("the per-scene ResNet34 encoder is out of scope: compute the latent map "
+                                  "elsewhere and call encode_latent(latent, poses, focal, c)")
+
+    # ------------------------------------------------------------------ forward
+    def fused(self):
+        from .field import FusedField
+        if self._fused is None:
+            self._fused = FusedField(self)
+        return self._fused
+
+    def can_fuse(self, xyz):
+        from .field import fused_eligible
+        return (self.use_fused and xyz.is_cuda and not (torch.is_grad_enabled() and self._needs_grad())
+                and fused_eligible(self))
+
+    def _needs_grad(self):
+        return any(p.requires_grad for p in self.parameters()) or self.encoder.latent.requires_grad
+
+    def forward(self, xyz, coarse=True, viewdirs=None, far=False, return_features=False):
+        if not return_features and self.can_fuse(xyz):
+            return self.fused().forward_points(xyz, viewdirs, coarse)
+        return self.forward_torch(xyz, coarse, viewdirs, far, return_features)
+
+    def forward_torch(self, xyz, coarse=True, viewdirs=None, far=False, return_features=False):
+        """models.py:739-863 as PyTorch ops (the autograd path)."""
+        SB, B, _ = xyz.shape
+        NS = self.num_views_per_obj
+        xyz = repeat_interleave(xyz, NS)
+        xyz_rot = torch.matmul(self.poses[:, None, :3, :3], xyz.unsqueeze(-1))[..., 0]
+        xyz = xyz_rot + self.poses[:, None, :3, 3]
+        if self.d_in > 0:
+            if self.use_xyz:
+                z_feature = (xyz_rot if self.normalize_z else xyz).reshape(-1, 3)
+            else:
+                z_feature = -(xyz_rot if self.normalize_z else xyz)[..., 2].reshape(-1, 1)
+            if self.use_code and not self.use_code_viewdirs:
+                z_feature = self.code(z_feature)
+            if self.use_viewdirs:
+                vd = repeat_interleave(viewdirs.reshape(SB, B, 3, 1), NS)
+                vd = torch.matmul(self.poses[:, None, :3, :3], vd).reshape(-1, 3)
+                z_feature = torch.cat((z_feature, vd), dim=1)
+            if self.use_code and self.use_code_viewdirs:
+                z_feature = self.code(z_feature)
+            mlp_input = z_feature
+        if self.use_encoder:
+            uv = -xyz[:, :, :2] / xyz[:, :, 2:]
+            uv = uv * repeat_interleave(self.focal.unsqueeze(1), NS if self.focal.shape[0] > 1 else 1)
+            uv = uv + repeat_interleave(self.c.unsqueeze(1), NS if self.c.shape[0] > 1 else 1)
+            latent = self.encoder.index(uv, None, self.image_shape)
+            if self.stop_encoder_grad:
+                latent = latent.detach()
+            latent = latent.transpose(1, 2).reshape(-1, self.latent_size)
+            mlp_input = latent if self.d_in == 0 else torch.cat((latent, z_feature), dim=-1)
+        if return_features:
+            return latent
+        mlp = self.mlp_coarse if (coarse or self.mlp_fine is None) else self.mlp_fine
+        out = mlp(mlp_input, combine_inner_dims=(self.num_views_per_obj, B)).reshape(-1, B, self.d_out)
+        out = torch.cat([torch.sigmoid(out[..., :3]), torch.relu(out[..., 3:4])], dim=-1)
+        return out.reshape(SB, B, -1)
+
+    def load_weights(self, model_path, opt_init=False, strict=True, device=None):
+        import os
+        import warnings
+        if os.path.exists(model_path):
+            self.load_state_dict(torch.load(model_path, map_location=device, weights_only=True), strict=strict)
+        elif not opt_init:
+            warnings.warn(f"WARNING: {model_path} does not exist, not loaded!! Model will be re-initialized.")
+        return self
+
+    def save_weights(self, model_path, opt_init=False):
+        torch.save(self.state_dict(), model_path)
+        return self
+
+
+def make_new_model(conf, *args, **kwargs):
+    """models.py:9-16."""
+    model_type = conf.get_string("type", "pixelnerf") if hasattr(conf, "get_string") else "pixelnerf"
+    if model_type != "pixelnerf":
+        raise NotImplementedError("Unsupported model type", model_type)
+    return NewPixelNeRFNet(conf, *args, **kwargs)
+
+
+class RadFieldAndRenderer(nn.Module):
+    """models.py:913-960."""
+
+    def __init__(self, rf, renderer):
+        super().__init__()
+        self.rf = rf
+        self.renderer = renderer
+
+    def forward(self, model_input):
+        return self.renderer(model_input["cam2world"], model_input["intrinsics"], model_input["x_pix"], self.rf)
+
+    def load_weights(self, model_path, opt_init=False, strict=True, device=None):
+        import os
+        import warnings
+        if os.path.exists(model_path):
+            self.load_state_dict(torch.load(model_path, map_location=device, weights_only=True), strict=strict)
+        elif not opt_init:
+            warnings.warn(f"WARNING: {model_path} does not exist, not loaded!! Model will be re-initialized.")
+        return self
+
+    def save_weights(self, model_path, opt_init=False):
+        torch.save(self.state_dict(), model_path)
+        return self

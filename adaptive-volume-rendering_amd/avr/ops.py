@@ -1,0 +1,168 @@
+"""Torch-tensor wrappers over the C ABI (one function per kernel entry point).
+
+All tensors are device tensors owned by PyTorch; every launch is enqueued on
+torch's current HIP stream. No function here has a host/CPU implementation.
+"""
+import torch
+
+from . import _lib
+from ._lib import call, ptr, require_device, stream_of
+
+F32 = torch.float32
+
+
+def _f32c(t):
+    return t if (t.dtype == F32 and t.is_contiguous()) else t.to(F32).contiguous()
+
+
+def world_rays(x_pix, intrinsics, cam2world):
+    """get_world_rays (utils.py:315-336). x_pix (SB,R,2), intrinsics (SB,3,3),
+    cam2world (SB,R,4,4) -- may be a stride-0 expand of one pose per batch."""
+    SB, R, _ = x_pix.shape
+    x_pix = _f32c(x_pix)
+    K = _f32c(intrinsics.reshape(SB, 3, 3))
+    c2w = cam2world.to(F32)
+    if c2w.dim() == 3:
+        c2w = c2w.unsqueeze(1)
+    if c2w.stride(-1) != 1 or c2w.stride(-2) != 4:
+        c2w = c2w.contiguous()
+    sb_stride = c2w.stride(0) if c2w.shape[0] > 1 else 0
+    ray_stride = c2w.stride(1) if c2w.shape[1] > 1 else 0
+    require_device(x_pix, K)
+    ro = torch.empty(SB, R, 3, device=x_pix.device, dtype=F32)
+    rd = torch.empty_like(ro)
+    call("avr_world_rays", ptr(x_pix), ptr(K), ptr(c2w), sb_stride, ray_stride, SB, R, ptr(ro), ptr(rd),
+         stream_of(x_pix))
+    return ro, rd, (c2w, sb_stride, ray_stride)
+
+
+def depth_from_world_fwd(ro, rd, dist, c2w_info, want_grad=False):
+    c2w, sb_stride, ray_stride = c2w_info
+    SB, R, _ = ro.shape
+    dist = _f32c(dist.detach().reshape(SB, R))
+    depth = torch.empty(SB, R, device=ro.device, dtype=F32)
+    dd = torch.empty(SB, R, device=ro.device, dtype=F32) if want_grad else None
+    call("avr_depth_from_world", ptr(ro), ptr(rd), ptr(dist), ptr(c2w), sb_stride, ray_stride, SB, R, ptr(depth),
+         ptr(dd), stream_of(ro))
+    return depth, dd
+
+
+class _Depth(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dist, ro, rd, c2w_info):
+        depth, dd = depth_from_world_fwd(ro, rd, dist, c2w_info, want_grad=True)
+        ctx.save_for_backward(dd)
+        ctx.dist_shape = dist.shape
+        return depth
+
+    @staticmethod
+    def backward(ctx, g):
+        (dd,) = ctx.saved_tensors
+        return (g * dd).reshape(ctx.dist_shape), None, None, None
+
+
+def depth_from_world(ro, rd, dist, c2w_info):
+    """depth_from_world(ro + rd*dist, c2w) (renderers.py:274-275, utils.py:358-361);
+    differentiable w.r.t. dist."""
+    if torch.is_grad_enabled() and dist.requires_grad:
+        return _Depth.apply(dist, ro, rd, c2w_info)
+    return depth_from_world_fwd(ro, rd, dist, c2w_info)[0]
+
+
+def sample_coarse(near, far, n_rays, n_samples, device, noise=None, seed=0, offset=0):
+    """sample_coarse (renderers.py:4-24) -> z (n_rays, n_samples). `noise` is the
+    rand_like draw (n_rays, n_samples) or None for in-kernel Philox."""
+    z = torch.empty(n_rays, n_samples, device=device, dtype=F32)
+    if noise is not None:
+        noise = _f32c(noise.reshape(n_rays, n_samples))
+        require_device(noise)
+    call("avr_sample_coarse", float(near), float(far), n_rays, n_samples, ptr(noise), seed, offset, ptr(z),
+         stream_of(z))
+    return z
+
+
+def sample_fine(weights, z_coarse, near, far, n_importance, n_depth, depth_std, u=None, u2=None, noise_depth=None,
+                seed=0, offset=0, want_idx=False, want_fine=False):
+    """sample_fine + sample_depth + clamp + sort (renderers.py:27-66, :252-258).
+    weights, z_coarse (R, Nc) -> z_sorted (R, Nc+Nf+Nd) [, idx (R,Nf) int32, z_fine (R,Nf)]."""
+    R, Nc = z_coarse.shape
+    weights = _f32c(weights.reshape(R, Nc))
+    z_coarse = _f32c(z_coarse)
+    dev = z_coarse.device
+    if u is not None:
+        u = _f32c(u.reshape(R, n_importance))
+        u2 = _f32c(u2.reshape(R, n_importance))
+        noise_depth = _f32c(noise_depth.reshape(R, n_depth)) if n_depth > 0 else None
+    require_device(weights, z_coarse, u, u2, noise_depth)
+    z_sorted = torch.empty(R, Nc + n_importance + n_depth, device=dev, dtype=F32)
+    idx = torch.empty(R, n_importance, device=dev, dtype=torch.int32) if want_idx else None
+    z_fine = torch.empty(R, n_importance, device=dev, dtype=F32) if want_fine else None
+    call("avr_sample_fine", ptr(weights), ptr(z_coarse), float(near), float(far), R, Nc, n_importance, n_depth,
+         float(depth_std), ptr(u), ptr(u2), ptr(noise_depth), seed, offset, ptr(z_sorted), ptr(idx), ptr(z_fine),
+         stream_of(z_coarse))
+    return z_sorted, idx, z_fine
+
+
+def composite_fwd(z, field, white_back=True, infinity=1.8, want_weights=True):
+    """volume_integral (renderers.py:69-119). z (R,N), field (R,N,4) ->
+    rgb (R,3), dist (R,), weights (R,N)."""
+    R, N = z.shape
+    z = _f32c(z)
+    field = _f32c(field.reshape(R, N, 4))
+    require_device(z, field)
+    rgb = torch.empty(R, 3, device=z.device, dtype=F32)
+    dist = torch.empty(R, device=z.device, dtype=F32)
+    w = torch.empty(R, N, device=z.device, dtype=F32) if want_weights else None
+    call("avr_composite_fwd", ptr(z), ptr(field), R, N, int(bool(white_back)), float(infinity), ptr(rgb),
+         ptr(dist), ptr(w), stream_of(z))
+    return rgb, dist, w
+
+
+def composite_bwd(z, field, grad_rgb, grad_dist, grad_w, white_back=True, infinity=1.8):
+    R, N = z.shape
+    grad_rgb = _f32c(grad_rgb.reshape(R, 3))
+    grad_dist = None if grad_dist is None else _f32c(grad_dist.reshape(R))
+    grad_w = None if grad_w is None else _f32c(grad_w.reshape(R, N))
+    require_device(grad_rgb, grad_dist, grad_w)
+    gfield = torch.empty(R, N, 4, device=z.device, dtype=F32)
+    call("avr_composite_bwd", ptr(z), ptr(field), R, N, int(bool(white_back)), float(infinity), ptr(grad_rgb),
+         ptr(grad_dist), ptr(grad_w), ptr(gfield), stream_of(z))
+    return gfield
+
+
+class _Composite(torch.autograd.Function):
+    """Autograd node for volume_integral: gradients flow to (rgb, sigma) of the
+    field output; z carries none (as in VolumeRenderer)."""
+
+    @staticmethod
+    def forward(ctx, z, field, white_back, infinity):
+        z = _f32c(z.detach())
+        field = _f32c(field.detach())
+        rgb, dist, w = composite_fwd(z, field, white_back, infinity, want_weights=True)
+        ctx.save_for_backward(z, field)
+        ctx.white_back, ctx.infinity = white_back, infinity
+        return rgb, dist, w
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_dist, g_w):
+        z, field = ctx.saved_tensors
+        if g_rgb is None:
+            g_rgb = torch.zeros(z.shape[0], 3, device=z.device, dtype=F32)
+        gfield = composite_bwd(z, field, g_rgb, g_dist, g_w, ctx.white_back, ctx.infinity)
+        return None, gfield, None, None
+
+
+def composite(z, field, white_back=True, infinity=1.8):
+    """Differentiable volume_integral on (R,N) z and (R,N,4) field."""
+    if torch.is_grad_enabled() and field.requires_grad:
+        return _Composite.apply(z, field, white_back, infinity)
+    return composite_fwd(z, field, white_back, infinity)
+
+
+def points(ro, rd, z):
+    """pts = ro + rd * z, viewdirs = rd per sample (renderers.py:171, :174) as
+    (R*N, 3) tensors for a generic radiance field."""
+    R, N = z.shape
+    pts = torch.addcmul(ro.reshape(R, 1, 3), rd.reshape(R, 1, 3), z.reshape(R, N, 1))
+    vd = rd.reshape(R, 1, 3).expand(R, N, 3)
+    return pts.reshape(R * N, 3), vd.reshape(R * N, 3)

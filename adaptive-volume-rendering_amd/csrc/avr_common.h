@@ -1,0 +1,102 @@
+// Shared device/host helpers for libavr_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "avr.h"
+
+namespace avr {
+
+// ------------------------------------------------------------------ errors
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+int check_launch(const char* what);
+
+#define AVR_REQUIRE(cond, ...)                                   \
+  do {                                                           \
+    if (!(cond)) return ::avr::fail(AVR_E_INVALID, __VA_ARGS__); \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;
+
+// ------------------------------------------------------------------ fp32 ops
+// Explicit round-to-nearest primitives so hipcc never contracts an a*b+c that
+// the reference evaluates as two roundings (the build also uses -ffp-contract=off).
+__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
+__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
+
+// ------------------------------------------------------------------ Philox4x32-10
+// Counter-based RNG for in-kernel noise (no noise bytes read from HBM).
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// 4 uniforms in [0,1) (24-bit grid) for (ray, block of 4 samples, stream).
+__device__ __forceinline__ float4 philox_uniform4(uint64_t seed, uint64_t ray, uint32_t block4, uint32_t stream) {
+  const uint4 r = philox4x32(make_uint4((uint32_t)ray, (uint32_t)(ray >> 32), block4, stream),
+                             make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+  const float s = 5.9604644775390625e-08f;  // 2^-24
+  return make_float4((r.x >> 8) * s, (r.y >> 8) * s, (r.z >> 8) * s, (r.w >> 8) * s);
+}
+
+__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t ray, uint32_t idx, uint32_t stream) {
+  const float4 v = philox_uniform4(seed, ray, idx >> 2, stream);
+  switch (idx & 3) {
+    case 0: return v.x;
+    case 1: return v.y;
+    case 2: return v.z;
+    default: return v.w;
+  }
+}
+
+// Standard normal via Box-Muller on two Philox uniforms.
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t ray, uint32_t idx, uint32_t stream) {
+  const float4 v = philox_uniform4(seed, ray, idx, stream);
+  const float u1 = fmaxf(v.x, 1e-7f);
+  return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * v.y);
+}
+
+// ------------------------------------------------------------------ wave primitives
+__device__ __forceinline__ double shfl_up_d(double v, int d) {
+  return __shfl_up(v, d, kWave);
+}
+
+// Inclusive wave64 scan of doubles (sum).
+__device__ __forceinline__ double wave_incl_scan_add(double v, int lane) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const double o = __shfl_up(v, d, kWave);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+// Inclusive wave64 scan of doubles (product).
+__device__ __forceinline__ double wave_incl_scan_mul(double v, int lane) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const double o = __shfl_up(v, d, kWave);
+    if (lane >= d) v *= o;
+  }
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
+  return v;
+}
+
+}  // namespace avr

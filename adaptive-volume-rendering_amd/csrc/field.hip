@@ -1,0 +1,528 @@
+// Radiance field: NewPixelNeRFNet.forward (models.py:739-863) fused into one
+// kernel on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact f32 products).
+//
+// Transposed formulation: every layer computes Y^T = W . X^T with the hidden
+// features on the MFMA rows and 16 samples on the MFMA columns, so a layer's
+// 16x16 accumulator tile (lane l: sample l&15, features 4(l>>4)+0..3) is
+// already in the lane order the next layer's B operand wants:
+//   k-step (t, r) uses feature 16t + 4g + r from lane group g = l>>4.
+// Weights are repacked once (avr_field_pack) into that fragment order,
+// [t][ot][lane] float4 = W[16ot + (l&15)][16t + 4(l>>4) + 0..3], so each lane
+// streams 16 B per 4 MFMAs with fully coalesced 1 KiB wave loads.
+//
+// One wave = 16 samples; a lane keeps the residual stream h and the block
+// temporary t for its 16x(d_hidden) slice in registers (2 x d_hidden/4 VGPRs),
+// and a 1 KiB-per-tile LDS slab (per wave, no cross-wave traffic, no barriers)
+// turns an accumulator tile into the next layer's B operand with one
+// ds_write_b128 / ds_read_b128 per tile.
+//
+// lin_z is applied to the latent map per texel (avr_field_latent_table) and
+// bilinearly interpolated per sample; every bias (b_in + bz0, b1 + bz_{b+1},
+// ...) is pre-summed at pack time.
+#include <math.h>
+
+#include "avr_common.h"
+
+namespace avr {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kFieldWaves = 4;  // 256-thread workgroups, one wave per SIMD
+constexpr int kSPW = 16;        // samples per wave (MFMA column count)
+constexpr int kInTiles = 3;     // lin_in K = 42 features padded to 48
+
+// ----------------------------------------------------------------- layout
+struct Layout {
+  int NT;                 // d_hidden / 16
+  int KTl;                // d_latent / 16
+  int64_t w_in, w_out, fc0[AVR_MAX_BLOCKS], fc1[AVR_MAX_BLOCKS], lin_z[AVR_MAX_BLOCKS];
+  int64_t b_in, b_out, b_fc0[AVR_MAX_BLOCKS], b_fc1[AVR_MAX_BLOCKS];
+  int64_t total;          // floats
+};
+
+static int make_layout(const avr_field_dims* d, Layout* L) {
+  AVR_REQUIRE(d, "field: null dims");
+  AVR_REQUIRE(d->d_hidden == 64 || d->d_hidden == 128 || d->d_hidden == 256 || d->d_hidden == 512,
+              "field: d_hidden must be 64/128/256/512 (got %d)", d->d_hidden);
+  AVR_REQUIRE(d->d_latent > 0 && d->d_latent % 16 == 0 && d->d_latent <= 1024,
+              "field: d_latent must be a positive multiple of 16 <= 1024 (got %d)", d->d_latent);
+  AVR_REQUIRE(d->n_blocks >= 1 && d->n_blocks <= AVR_MAX_BLOCKS, "field: n_blocks must be in [1, %d]",
+              AVR_MAX_BLOCKS);
+  AVR_REQUIRE(d->n_lin_z >= 0 && d->n_lin_z <= d->n_blocks, "field: n_lin_z must be in [0, n_blocks]");
+  AVR_REQUIRE(d->num_freqs >= 0 && 3 + 6 * d->num_freqs + 3 == d->d_in && d->d_in <= 16 * kInTiles,
+              "field: d_in %d != 6*num_freqs+6 or > 48 (fused path supports PE(xyz)+raw viewdirs)", d->d_in);
+  const int NT = d->d_hidden / 16;
+  L->NT = NT;
+  L->KTl = d->d_latent / 16;
+  const int64_t tile = 64 * 4;  // floats per (t, ot) fragment block
+  int64_t o = 0;
+  L->w_in = o; o += (int64_t)kInTiles * NT * tile;
+  for (int b = 0; b < d->n_blocks; ++b) {
+    L->fc0[b] = o; o += (int64_t)NT * NT * tile;
+    L->fc1[b] = o; o += (int64_t)NT * NT * tile;
+  }
+  L->w_out = o; o += (int64_t)NT * tile;
+  for (int b = 0; b < d->n_lin_z; ++b) { L->lin_z[b] = o; o += (int64_t)L->KTl * NT * tile; }
+  L->b_in = o; o += d->d_hidden;
+  for (int b = 0; b < d->n_blocks; ++b) {
+    L->b_fc0[b] = o; o += d->d_hidden;
+    L->b_fc1[b] = o; o += d->d_hidden;
+  }
+  L->b_out = o; o += 16;
+  L->total = o;
+  return AVR_OK;
+}
+
+// ----------------------------------------------------------------- packing
+// dst[(t*NTo + ot)*64 + l][r] = W[16ot + (l&15)][16t + 4(l>>4) + r]  (zero padded)
+__global__ void pack_linear_kernel(const float* __restrict__ W, int out_dim, int in_dim, int NTo, int KTi,
+                                   float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)KTi * NTo * 256;
+  if (i >= n) return;
+  const int r = (int)(i & 3);
+  const int l = (int)((i >> 2) & 63);
+  const int64_t blk = i >> 8;
+  const int ot = (int)(blk % NTo), t = (int)(blk / NTo);
+  const int row = 16 * ot + (l & 15), col = 16 * t + 4 * (l >> 4) + r;
+  dst[i] = (row < out_dim && col < in_dim) ? W[(int64_t)row * in_dim + col] : 0.f;
+}
+
+// dst[i] = a[i] + b[i] (b may be null), zero beyond n.
+__global__ void pack_bias_kernel(const float* __restrict__ a, const float* __restrict__ b, int n, int n_pad,
+                                 float* __restrict__ dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pad) return;
+  dst[i] = (i < n) ? (b ? fadd(a[i], b[i]) : a[i]) : 0.f;
+}
+
+// ----------------------------------------------------------------- MFMA tiles
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// acc[ot] += sum_t sum_r A(ot,t,r) B(t,r); A from packed global [t][ot][lane]
+// through a P-deep register ring that runs ahead across t iterations, B from
+// the wave's LDS slab [t][lane].
+template <int NT, int P>
+__device__ __forceinline__ void gemm_tiles(floatx4 (&acc)[NT], const floatx4* __restrict__ W, int KT,
+                                           const floatx4* slab, int lane) {
+  static_assert(NT % P == 0 && P % 2 == 0, "ring must divide the tile count");
+  const floatx4* wl = W + lane;
+  floatx4 ring[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) ring[p] = wl[p * 64];
+  for (int t = 0; t < KT; ++t) {
+    const floatx4 bv = slab[t * 64 + lane];
+    const floatx4* cur = wl + (int64_t)t * NT * 64;
+    const floatx4* nxt = wl + (int64_t)(t + 1 < KT ? t + 1 : t) * NT * 64;
+#pragma unroll
+    for (int ot = 0; ot < NT; ot += 2) {
+      const floatx4 a0 = ring[ot % P];
+      const floatx4 a1 = ring[(ot + 1) % P];
+      ring[ot % P] = (ot + P < NT) ? cur[(ot + P) * 64] : nxt[(ot + P - NT) * 64];
+      ring[(ot + 1) % P] = (ot + 1 + P < NT) ? cur[(ot + 1 + P) * 64] : nxt[(ot + 1 + P - NT) * 64];
+      acc[ot] = mfma4(a0.x, bv.x, acc[ot]);
+      acc[ot + 1] = mfma4(a1.x, bv.x, acc[ot + 1]);
+      acc[ot] = mfma4(a0.y, bv.y, acc[ot]);
+      acc[ot + 1] = mfma4(a1.y, bv.y, acc[ot + 1]);
+      acc[ot] = mfma4(a0.z, bv.z, acc[ot]);
+      acc[ot + 1] = mfma4(a1.z, bv.z, acc[ot + 1]);
+      acc[ot] = mfma4(a0.w, bv.w, acc[ot]);
+      acc[ot + 1] = mfma4(a1.w, bv.w, acc[ot + 1]);
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void load_bias(floatx4 (&acc)[NT], const float* __restrict__ bias, int g) {
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = *reinterpret_cast<const floatx4*>(bias + 16 * ot + 4 * g);
+}
+
+template <int NT>
+__device__ __forceinline__ void add_bias(floatx4 (&acc)[NT], const float* __restrict__ bias, int g) {
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] += *reinterpret_cast<const floatx4*>(bias + 16 * ot + 4 * g);
+}
+
+struct Bilinear {
+  int off[4];    // texel * d_hidden (float offsets into one lin_z table)
+  float w[4];
+};
+
+// acc += sum_c w_c * Z[texel_c][features of this lane]
+template <int NT>
+__device__ __forceinline__ void add_interp(floatx4 (&acc)[NT], const float* __restrict__ Z, const Bilinear& bl,
+                                           int g) {
+  constexpr int CH = NT < 8 ? NT : 8;
+#pragma unroll
+  for (int o0 = 0; o0 < NT; o0 += CH) {
+    floatx4 v[CH][4];
+#pragma unroll
+    for (int k = 0; k < CH; ++k)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        v[k][c] = *reinterpret_cast<const floatx4*>(Z + bl.off[c] + 16 * (o0 + k) + 4 * g);
+#pragma unroll
+    for (int k = 0; k < CH; ++k)
+      acc[o0 + k] += ((bl.w[0] * v[k][0] + bl.w[1] * v[k][1]) + bl.w[2] * v[k][2]) + bl.w[3] * v[k][3];
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void store_relu(floatx4* slab, const floatx4 (&acc)[NT], int lane) {
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) {
+    floatx4 v = acc[ot];
+    v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    slab[ot * 64 + lane] = v;
+  }
+}
+
+struct View {
+  float R[9], t[3];
+  float focal[2], c[2], scale[2];
+  int H, W;
+};
+
+struct FieldArgs {
+  const float* packed;
+  const float* table;
+  int64_t table_stride;  // floats per lin_z table (HW * d_hidden)
+  Layout L;
+  View v;
+  int n_blocks, n_lin_z, num_freqs;
+  float freq_factor;
+  // sample source: rays (z != null) or explicit points
+  const float* ro; const float* rd; const float* z; int n_samples;
+  const float* xyz; const float* vd;
+  int64_t M;
+  float4* out;
+};
+
+__device__ __forceinline__ float dot3(const float* R, float a, float b, float c) {
+  return fadd(fadd(fmul(R[0], a), fmul(R[1], b)), fmul(R[2], c));
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return fdiv(1.0f, fadd(1.0f, expf(-x))); }
+
+template <int NT>
+__global__ void __launch_bounds__(256, 1) field_fwd_kernel(FieldArgs a) {
+  extern __shared__ floatx4 lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  floatx4* slab = lds + (size_t)wid * (NT > kInTiles ? NT : kInTiles) * 64;
+  const int64_t m = ((int64_t)blockIdx.x * kFieldWaves + wid) * kSPW + j;
+  const bool valid = m < a.M;
+  const int64_t mm = valid ? m : a.M - 1;
+
+  // ---- sample position and view direction
+  float x0, x1, x2, d0, d1, d2;
+  if (a.z) {
+    const int64_t r = mm / a.n_samples;
+    const float zz = a.z[mm];
+    d0 = a.rd[3 * r]; d1 = a.rd[3 * r + 1]; d2 = a.rd[3 * r + 2];
+    x0 = fadd(a.ro[3 * r], fmul(d0, zz));
+    x1 = fadd(a.ro[3 * r + 1], fmul(d1, zz));
+    x2 = fadd(a.ro[3 * r + 2], fmul(d2, zz));
+  } else {
+    x0 = a.xyz[3 * mm]; x1 = a.xyz[3 * mm + 1]; x2 = a.xyz[3 * mm + 2];
+    d0 = a.vd[3 * mm]; d1 = a.vd[3 * mm + 1]; d2 = a.vd[3 * mm + 2];
+  }
+  const View& v = a.v;
+  // xyz_rot = R xyz (models.py:755-757); camera-space point = xyz_rot + t (:758)
+  const float xr0 = dot3(v.R + 0, x0, x1, x2), xr1 = dot3(v.R + 3, x0, x1, x2), xr2 = dot3(v.R + 6, x0, x1, x2);
+  const float xc0 = fadd(xr0, v.t[0]), xc1 = fadd(xr1, v.t[1]), xc2 = fadd(xr2, v.t[2]);
+
+  // ---- z_feature (models.py:763-789): [xyz_rot, PE(xyz_rot), R viewdir], padded to 48.
+  // This lane writes features 16t + 4g + r of its sample to slab[t][lane].
+  {
+    const float vr0 = dot3(v.R + 0, d0, d1, d2), vr1 = dot3(v.R + 3, d0, d1, d2), vr2 = dot3(v.R + 6, d0, d1, d2);
+    const float xr[3] = {xr0, xr1, xr2};
+    const float vr[3] = {vr0, vr1, vr2};
+    const int npe = 6 * a.num_freqs;
+#pragma unroll
+    for (int t = 0; t < kInTiles; ++t) {
+      float f[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * t + 4 * g + r;
+        float val = 0.f;
+        if (k < 3) {
+          val = xr[k];
+        } else if (k < 3 + npe) {
+          // embed[jj][dd] = sin(phase_jj + x_dd * freq_jj), jj = 2*freq + {0: sin, 1: cos}
+          const int q = k - 3, jj = q / 3, dd = q - 3 * jj;
+          const float freq = fmul(a.freq_factor, exp2f((float)(jj >> 1)));
+          const float phase = (jj & 1) ? 1.5707963705062866f : 0.f;  // fp32(pi/2)
+          val = sinf(fadd(phase, fmul(xr[dd], freq)));
+        } else if (k < 6 + npe) {
+          val = vr[k - 3 - npe];
+        }
+        f[r] = val;
+      }
+      slab[t * 64 + lane] = floatx4{f[0], f[1], f[2], f[3]};
+    }
+  }
+
+  // ---- bilinear latent lookup (SpatialEncoder.index, models.py:260-273):
+  // uv = -xyz_c[:2]/xyz_c[2] * focal + c; grid = uv * (latent_scaling/image_shape) - 1;
+  // grid_sample(bilinear, border, align_corners=True).
+  Bilinear bl;
+  {
+    const float u = fadd(fmul(fdiv(-xc0, xc2), v.focal[0]), v.c[0]);
+    const float w = fadd(fmul(fdiv(-xc1, xc2), v.focal[1]), v.c[1]);
+    const float gx = fsub(fmul(u, v.scale[0]), 1.0f), gy = fsub(fmul(w, v.scale[1]), 1.0f);
+    float ix = fmul(fdiv(fadd(gx, 1.0f), 2.0f), (float)(v.W - 1));
+    float iy = fmul(fdiv(fadd(gy, 1.0f), 2.0f), (float)(v.H - 1));
+    ix = fminf(fmaxf(ix, 0.f), (float)(v.W - 1));
+    iy = fminf(fmaxf(iy, 0.f), (float)(v.H - 1));
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const float wx1 = fsub(ix, fx0), wy1 = fsub(iy, fy0);
+    const float wx0 = fsub(fadd(fx0, 1.0f), ix), wy0 = fsub(fadd(fy0, 1.0f), iy);
+    const int X0 = (int)fx0, Y0 = (int)fy0;
+    const int X1 = X0 + 1 < v.W ? X0 + 1 : v.W - 1, Y1 = Y0 + 1 < v.H ? Y0 + 1 : v.H - 1;
+    const int HID = NT * 16;
+    bl.off[0] = (Y0 * v.W + X0) * HID; bl.w[0] = fmul(wx0, wy0);
+    bl.off[1] = (Y0 * v.W + X1) * HID; bl.w[1] = fmul(wx1, wy0);
+    bl.off[2] = (Y1 * v.W + X0) * HID; bl.w[2] = fmul(wx0, wy1);
+    bl.off[3] = (Y1 * v.W + X1) * HID; bl.w[3] = fmul(wx1, wy1);
+  }
+
+  const floatx4* P4 = reinterpret_cast<const floatx4*>(a.packed);
+  floatx4 h[NT], tt[NT];
+  constexpr int P = NT >= 16 ? 16 : NT;
+
+  // ---- lin_in (+ lin_z[0] + both biases)
+  load_bias<NT>(h, a.packed + a.L.b_in, g);
+  if (a.n_lin_z > 0) add_interp<NT>(h, a.table, bl, g);
+  gemm_tiles<NT, P>(h, P4 + a.L.w_in / 4, kInTiles, slab, lane);
+
+  // ---- ResnetBlockFC x n_blocks
+  for (int b = 0; b < a.n_blocks; ++b) {
+    store_relu<NT>(slab, h, lane);
+    load_bias<NT>(tt, a.packed + a.L.b_fc0[b], g);
+    gemm_tiles<NT, P>(tt, P4 + a.L.fc0[b] / 4, NT, slab, lane);
+    store_relu<NT>(slab, tt, lane);
+    add_bias<NT>(h, a.packed + a.L.b_fc1[b], g);
+    if (b + 1 < a.n_lin_z) add_interp<NT>(h, a.table + (b + 1) * a.table_stride, bl, g);
+    gemm_tiles<NT, P>(h, P4 + a.L.fc1[b] / 4, NT, slab, lane);
+  }
+
+  // ---- lin_out(relu(h)) -> (sigmoid rgb, relu sigma)
+  store_relu<NT>(slab, h, lane);
+  floatx4 o0 = *reinterpret_cast<const floatx4*>(a.packed + a.L.b_out + 4 * g);
+  floatx4 o1 = {0.f, 0.f, 0.f, 0.f};
+  const floatx4* wo = P4 + a.L.w_out / 4 + lane;
+#pragma unroll 4
+  for (int t = 0; t < NT; t += 2) {
+    const floatx4 A0 = wo[t * 64], A1 = wo[(t + 1) * 64];
+    const floatx4 B0 = slab[t * 64 + lane], B1 = slab[(t + 1) * 64 + lane];
+    o0 = mfma4(A0.x, B0.x, o0); o1 = mfma4(A1.x, B1.x, o1);
+    o0 = mfma4(A0.y, B0.y, o0); o1 = mfma4(A1.y, B1.y, o1);
+    o0 = mfma4(A0.z, B0.z, o0); o1 = mfma4(A1.z, B1.z, o1);
+    o0 = mfma4(A0.w, B0.w, o0); o1 = mfma4(A1.w, B1.w, o1);
+  }
+  const floatx4 o = o0 + o1;
+  if (g == 0 && valid) a.out[m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
+}
+
+// table[b][texel][f] = sum_c Wz_b[f][c] latent[c][texel]  (16 texels per wave)
+template <int NT>
+__global__ void __launch_bounds__(256, 1) latent_table_kernel(const float* __restrict__ packed, Layout L,
+                                                              const float* __restrict__ latent, int HW,
+                                                              float* __restrict__ table) {
+  extern __shared__ floatx4 lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y;
+  floatx4* slab = lds + (size_t)wid * L.KTl * 64;
+  const int64_t texel = ((int64_t)blockIdx.x * kFieldWaves + wid) * kSPW + j;
+  const bool valid = texel < HW;
+  const int64_t tx = valid ? texel : HW - 1;
+  for (int t = 0; t < L.KTl; ++t) {
+    const int c0 = 16 * t + 4 * g;
+    slab[t * 64 + lane] = floatx4{latent[(int64_t)c0 * HW + tx], latent[(int64_t)(c0 + 1) * HW + tx],
+                                  latent[(int64_t)(c0 + 2) * HW + tx], latent[(int64_t)(c0 + 3) * HW + tx]};
+  }
+  floatx4 acc[NT];
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+  constexpr int P = NT >= 16 ? 16 : NT;
+  gemm_tiles<NT, P>(acc, reinterpret_cast<const floatx4*>(packed + L.lin_z[b]), L.KTl, slab, lane);
+  if (valid) {
+    float* dst = table + ((int64_t)b * HW + texel) * (NT * 16) + 4 * g;
+#pragma unroll
+    for (int ot = 0; ot < NT; ++ot) *reinterpret_cast<floatx4*>(dst + 16 * ot) = acc[ot];
+  }
+}
+
+// ----------------------------------------------------------------- host side
+static int pack_linear(const float* W, int out_dim, int in_dim, int NTo, int KTi, float* dst, hipStream_t s) {
+  AVR_REQUIRE(W, "avr_field_pack: null weight tensor");
+  const int64_t n = (int64_t)KTi * NTo * 256;
+  pack_linear_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(W, out_dim, in_dim, NTo, KTi, dst);
+  return check_launch("pack_linear_kernel");
+}
+
+static int pack_bias(const float* a, const float* b, int n, int n_pad, float* dst, hipStream_t s) {
+  AVR_REQUIRE(a, "avr_field_pack: null bias tensor");
+  pack_bias_kernel<<<(unsigned)((n_pad + 255) / 256), 256, 0, s>>>(a, b, n, n_pad, dst);
+  return check_launch("pack_bias_kernel");
+}
+
+template <int NT>
+static int launch_field(const FieldArgs& a, hipStream_t s) {
+  const size_t shm = (size_t)kFieldWaves * (NT > kInTiles ? NT : kInTiles) * 64 * sizeof(floatx4);
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_fwd_kernel<NT>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
+      return fail(AVR_E_HIP, "field_fwd_kernel: cannot set dynamic LDS to %zu", shm);
+    attr = true;
+  }
+  const int64_t per_block = kFieldWaves * kSPW;
+  const int64_t blocks = (a.M + per_block - 1) / per_block;
+  AVR_REQUIRE(blocks < (1ll << 31), "field: too many points");
+  field_fwd_kernel<NT><<<(unsigned)blocks, 64 * kFieldWaves, shm, s>>>(a);
+  return check_launch("field_fwd_kernel");
+}
+
+template <int NT>
+static int launch_table(const float* packed, const Layout& L, const float* latent, int HW, int n_lin_z,
+                        float* table, hipStream_t s) {
+  const size_t shm = (size_t)kFieldWaves * L.KTl * 64 * sizeof(floatx4);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&latent_table_kernel<NT>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
+    return fail(AVR_E_HIP, "latent_table_kernel: cannot set dynamic LDS to %zu", shm);
+  const int per_block = kFieldWaves * kSPW;
+  dim3 grid((HW + per_block - 1) / per_block, n_lin_z);
+  latent_table_kernel<NT><<<grid, 64 * kFieldWaves, shm, s>>>(packed, L, latent, HW, table);
+  return check_launch("latent_table_kernel");
+}
+
+static int field_common(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
+                        const float* table, FieldArgs* a) {
+  Layout L;
+  int rc = make_layout(dims, &L);
+  if (rc) return rc;
+  AVR_REQUIRE(view && packed, "field: null view/packed");
+  AVR_REQUIRE(dims->n_lin_z == 0 || table, "field: null latent table");
+  AVR_REQUIRE(view->latent_h > 0 && view->latent_w > 0, "field: bad latent size");
+  a->packed = packed;
+  a->table = table;
+  a->table_stride = (int64_t)view->latent_h * view->latent_w * dims->d_hidden;
+  a->L = L;
+  for (int i = 0; i < 3; ++i) {
+    for (int k = 0; k < 3; ++k) a->v.R[3 * i + k] = view->poses[4 * i + k];
+    a->v.t[i] = view->poses[4 * i + 3];
+  }
+  for (int i = 0; i < 2; ++i) {
+    a->v.focal[i] = view->focal[i];
+    a->v.c[i] = view->c[i];
+    a->v.scale[i] = view->latent_scaling[i] / view->image_shape[i];  // models.py:263 (fp32 div)
+  }
+  a->v.H = view->latent_h;
+  a->v.W = view->latent_w;
+  a->n_blocks = dims->n_blocks;
+  a->n_lin_z = dims->n_lin_z;
+  a->num_freqs = dims->num_freqs;
+  a->freq_factor = dims->freq_factor;
+  return AVR_OK;
+}
+
+static int dispatch_field(int d_hidden, const FieldArgs& a, hipStream_t s) {
+  switch (d_hidden) {
+    case 64: return launch_field<4>(a, s);
+    case 128: return launch_field<8>(a, s);
+    case 256: return launch_field<16>(a, s);
+    case 512: return launch_field<32>(a, s);
+  }
+  return fail(AVR_E_UNSUPPORTED, "field: d_hidden %d", d_hidden);
+}
+
+}  // namespace avr
+
+using namespace avr;
+
+extern "C" int avr_field_packed_floats(const avr_field_dims* dims, int64_t* n_floats) {
+  Layout L;
+  const int rc = make_layout(dims, &L);
+  if (rc) return rc;
+  AVR_REQUIRE(n_floats, "avr_field_packed_floats: null output");
+  *n_floats = L.total;
+  return AVR_OK;
+}
+
+extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed,
+                              void* stream) {
+  Layout L;
+  int rc = make_layout(dims, &L);
+  if (rc) return rc;
+  AVR_REQUIRE(w && packed, "avr_field_pack: null pointer");
+  hipStream_t s = as_stream(stream);
+  const int H = dims->d_hidden, NT = L.NT;
+  if ((rc = pack_linear(w->lin_in_w, H, dims->d_in, NT, kInTiles, packed + L.w_in, s))) return rc;
+  if ((rc = pack_linear(w->lin_out_w, 4, H, 1, NT, packed + L.w_out, s))) return rc;
+  for (int b = 0; b < dims->n_blocks; ++b) {
+    if ((rc = pack_linear(w->fc0_w[b], H, H, NT, NT, packed + L.fc0[b], s))) return rc;
+    if ((rc = pack_linear(w->fc1_w[b], H, H, NT, NT, packed + L.fc1[b], s))) return rc;
+    if ((rc = pack_bias(w->fc0_b[b], nullptr, H, H, packed + L.b_fc0[b], s))) return rc;
+    const float* bz = (b + 1 < dims->n_lin_z) ? w->lin_z_b[b + 1] : nullptr;
+    if ((rc = pack_bias(w->fc1_b[b], bz, H, H, packed + L.b_fc1[b], s))) return rc;
+  }
+  for (int b = 0; b < dims->n_lin_z; ++b)
+    if ((rc = pack_linear(w->lin_z_w[b], H, dims->d_latent, NT, L.KTl, packed + L.lin_z[b], s))) return rc;
+  if ((rc = pack_bias(w->lin_in_b, dims->n_lin_z > 0 ? w->lin_z_b[0] : nullptr, H, H, packed + L.b_in, s)))
+    return rc;
+  return pack_bias(w->lin_out_b, nullptr, 4, 16, packed + L.b_out, s);
+}
+
+extern "C" int avr_field_latent_table(const avr_field_dims* dims, const float* packed, const float* latent, int H,
+                                      int W, float* table, void* stream) {
+  Layout L;
+  int rc = make_layout(dims, &L);
+  if (rc) return rc;
+  AVR_REQUIRE(packed && latent && table, "avr_field_latent_table: null pointer");
+  AVR_REQUIRE(H > 0 && W > 0, "avr_field_latent_table: bad latent size");
+  if (dims->n_lin_z == 0) return AVR_OK;
+  hipStream_t s = as_stream(stream);
+  switch (dims->d_hidden) {
+    case 64: return launch_table<4>(packed, L, latent, H * W, dims->n_lin_z, table, s);
+    case 128: return launch_table<8>(packed, L, latent, H * W, dims->n_lin_z, table, s);
+    case 256: return launch_table<16>(packed, L, latent, H * W, dims->n_lin_z, table, s);
+    case 512: return launch_table<32>(packed, L, latent, H * W, dims->n_lin_z, table, s);
+  }
+  return fail(AVR_E_UNSUPPORTED, "field: d_hidden %d", dims->d_hidden);
+}
+
+extern "C" int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
+                                  const float* table, const float* ro, const float* rd, const float* z,
+                                  int64_t n_rays, int n_samples, float* out, void* stream) {
+  FieldArgs a{};
+  int rc = field_common(dims, view, packed, table, &a);
+  if (rc) return rc;
+  AVR_REQUIRE(ro && rd && z && out, "avr_field_fwd_rays: null pointer");
+  AVR_REQUIRE(n_rays >= 0 && n_samples > 0, "avr_field_fwd_rays: bad sizes");
+  a.ro = ro; a.rd = rd; a.z = z; a.n_samples = n_samples;
+  a.M = n_rays * n_samples;
+  a.out = reinterpret_cast<float4*>(out);
+  if (a.M == 0) return AVR_OK;
+  return dispatch_field(dims->d_hidden, a, as_stream(stream));
+}
+
+extern "C" int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
+                                    const float* table, const float* xyz, const float* viewdirs, int64_t n_points,
+                                    float* out, void* stream) {
+  FieldArgs a{};
+  int rc = field_common(dims, view, packed, table, &a);
+  if (rc) return rc;
+  AVR_REQUIRE(xyz && viewdirs && out, "avr_field_fwd_points: null pointer");
+  AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points: bad size");
+  a.xyz = xyz; a.vd = viewdirs; a.n_samples = 1;
+  a.M = n_points;
+  a.out = reinterpret_cast<float4*>(out);
+  if (a.M == 0) return AVR_OK;
+  return dispatch_field(dims->d_hidden, a, as_stream(stream));
+}

@@ -1,0 +1,278 @@
+#!/usr/bin/env python
+"""Benchmark: rays/s of the coarse/fine VolumeRenderer hot path on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): 65 536 rays per GPU
+x (128 coarse + 64 importance samples, n_fine_depth = 0), one scene, the
+conf/default.conf PixelNeRF field (PE(6) + ResnetFC 3 x 512 with lin_z on all
+blocks, d_latent 512) with random-init weights and a random 512x64x64 latent
+map (synthetic: no dataset or checkpoint is available offline).
+
+One step = VolumeRenderer.forward over the batch: ray generation, stratified
+sampling, coarse field, compositing, inverse-CDF sampling + merge, fine field,
+compositing, depth -- plus, on N > 1 GPUs, the RCCL gather of every rank's
+(rgb_coarse, rgb_fine, depth) to rank 0. The per-scene preparation (weight
+repack and lin_z latent table) is redone inside every step, not cached.
+
+python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 via torch.distributed.run.
+Prints one JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "adaptive-volume-rendering_amd"))
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (= fp32 vector), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def field_flops_per_sample(d_in=42, d_hidden=512, n_blocks=3, n_lin_z=3, d_out=4):
+    """Algorithmic FLOPs of the fused field per sample (this design: lin_z is
+    applied per texel, so per sample it is a 4-tap bilinear blend)."""
+    macs = d_in * d_hidden + n_blocks * 2 * d_hidden * d_hidden + d_hidden * d_out
+    return 2 * macs + n_lin_z * d_hidden * 8
+
+
+def reference_flops_per_sample(d_in=42, d_latent=512, d_hidden=512, n_blocks=3, n_lin_z=3, d_out=4):
+    """FLOPs the reference's unfactored ResnetFC spends per sample (4.766 M)."""
+    return 2 * (d_in * d_hidden + n_lin_z * d_latent * d_hidden + n_blocks * 2 * d_hidden * d_hidden
+                + d_hidden * d_out)
+
+
+def build_scene(device, seed=0):
+    from avr.conf import default_conf
+    from avr.models import NewPixelNeRFNet
+    torch.manual_seed(seed)
+    net = NewPixelNeRFNet(default_conf()["model"])
+    with torch.no_grad():
+        for mlp in (net.mlp_coarse, net.mlp_fine):
+            for blk in mlp.blocks:     # reference zero-inits fc_1 (identity blocks); use N(0, 0.02)
+                blk.fc_1.weight.normal_(0.0, 0.02)
+    net = net.to(device).eval()
+    for p in net.parameters():
+        p.requires_grad_(False)
+    g = torch.Generator(device="cpu").manual_seed(seed + 1)
+    latent = torch.randn(1, 512, 64, 64, generator=g).to(device)
+    net.encoder.set_latent(latent)
+    poses = torch.zeros(1, 3, 4)
+    poses[0, :3, :3] = torch.eye(3)
+    poses[0, 2, 3] = 1.3
+    net.poses = poses.to(device)
+    net.focal = torch.tensor([[131.25, -131.25]], device=device)
+    net.c = torch.tensor([[64.0, 64.0]], device=device)
+    net.image_shape = torch.tensor([128.0, 128.0], device=device)
+    return net
+
+
+def orbit_c2w(angle, radius=1.3, z_height=0.4):
+    """generate_video's orbit pose (utils.py:497-513)."""
+    rr = np.sqrt(radius * radius - z_height * z_height)
+    t = np.array([rr * np.sin(angle), rr * np.cos(angle), z_height])
+    zax = -t / np.linalg.norm(t)
+    xax = np.cross([0.0, 0.0, -1.0], zax)
+    xax /= np.linalg.norm(xax)
+    yax = np.cross(zax, xax)
+    c2w = np.eye(4)
+    c2w[:3, :3] = np.stack([xax, yax, zax], 1)
+    c2w[:3, 3] = t
+    return torch.from_numpy((c2w @ np.diag([1.0, -1.0, -1.0, 1.0])).astype(np.float32))
+
+
+class FieldTimer:
+    """HIP events around every field launch, recorded on the launch stream."""
+
+    def __init__(self):
+        self.events = []
+        self.samples = 0
+
+    def wrap(self, fused):
+        orig = fused.forward_rays
+
+        def timed(ro, rd, z, coarse, sb=0):
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            fused.packed(coarse)
+            fused.table(coarse, sb)
+            s.record()
+            out = orig(ro, rd, z, coarse, sb)
+            e.record()
+            self.events.append((s, e))
+            self.samples += z.numel()
+            return out
+
+        fused.forward_rays = timed
+
+    def reset(self):
+        self.events, self.samples = [], 0
+
+    def total_ms(self):
+        return sum(s.elapsed_time(e) for s, e in self.events)
+
+
+def cpu_baseline(rays_cap=4096, budget_s=12.0):
+    """The oracle (numpy restatement of the reference path, 'port') on this
+    host's cores, on a bounded sample of the same workload: 128-ray chunks of
+    the 128 + 64 configuration with the same field architecture."""
+    sys.path.insert(0, REPO)
+    from oracle import avr_oracle as O
+    from oracle import synth
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:  # noqa: BLE001
+        threads = 1
+    pc = synth.resnetfc_params(42, 512, 512, 3, 1000, 40)
+    pf = synth.resnetfc_params(42, 512, 512, 3, 1000, 57)
+    poses, focal, c, image_shape, latent_scaling = synth.source_view((64, 64))
+    latent = synth.hashed_normalish((1, 512, 64, 64), 45, 1.0)
+    field = O.PixelNeRFField(pc, pf, latent, poses, focal, c, image_shape, latent_scaling)
+    rng = np.random.default_rng(0)
+    chunk, done, t_total = 128, 0, 0.0
+    K = synth.default_intrinsics()[None]
+    c2w1 = synth.orbit_cam2world(0.7)
+    while done < rays_cap and t_total < budget_s:
+        x_pix = rng.random((1, chunk, 2), dtype=np.float32)
+        c2w = np.broadcast_to(c2w1, (1, chunk, 4, 4))
+        noise = [rng.random((1, chunk, n), dtype=np.float32) for n in (128, 64, 64)]
+        t0 = time.perf_counter()
+        O.render(c2w, K, x_pix, field, 0.8, 1.8, 128, 64, 0, 0.01, True, noise[0], noise[1], noise[2],
+                 np.zeros((1, chunk, 0), np.float32))
+        t_total += time.perf_counter() - t0
+        done += chunk
+    return {"value": round(done / t_total, 2), "unit": "rays/s", "cores": int(threads), "kind": "port",
+            "sample": f"{done} rays x (128 coarse + 64 fine), oracle/avr_oracle.render (numpy, fp32 BLAS "
+                      f"{threads} threads), {t_total:.1f} s, host {os.cpu_count()} logical CPUs"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rays", type=int, default=65536, help="rays per GPU per step")
+    ap.add_argument("--n-coarse", type=int, default=128)
+    ap.add_argument("--n-fine", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    import avr
+    from avr.renderers import VolumeRenderer
+    avr.load_library()
+
+    net = build_scene(device)
+    fused = net.fused()
+    timer = FieldTimer()
+    timer.wrap(fused)
+    R = args.rays
+    rend = VolumeRenderer(0.8, 1.8, args.n_coarse, args.n_fine, 0, 0.01, True)
+    rend.seed = 1234 + rank
+    g = torch.Generator(device="cpu").manual_seed(100 + rank)
+    x_pix = torch.rand(1, R, 2, generator=g).to(device)
+    c2w = orbit_c2w(0.7 + 0.5 * rank).to(device).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
+    K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]], device=device)
+    gathered = None
+    if world > 1:
+        gathered = torch.empty(world * R * 7, device=device)
+
+    def step():
+        fused._packed.clear()       # per-scene prep inside the step: repack weights, rebuild lin_z tables
+        with torch.no_grad():
+            rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
+            if world > 1:
+                import torch.distributed as dist
+                local = torch.cat([rgb_c.reshape(-1), rgb_f.reshape(-1), depth.reshape(-1)])
+                dist.all_gather_into_tensor(gathered, local)
+        return rgb_f
+
+    for _ in range(args.warmup):
+        step()
+    assert rend.last_path == "fused", "bench must run the fused HIP field"
+    torch.cuda.synchronize()
+    timer.reset()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    field_ms = timer.total_ms()
+    if world > 1:
+        t = torch.tensor([elapsed, field_ms], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, field_ms = float(t[0]), float(t[1])
+    assert bool(torch.isfinite(out).all())
+
+    rays_total = R * world * args.steps
+    value = rays_total / elapsed
+    samples_per_ray = args.n_coarse + args.n_coarse + args.n_fine
+    fps = field_flops_per_sample()
+    field_launches = len(timer.events)
+    achieved_tflops = timer.samples * fps / (field_ms * 1e-3) / 1e12
+    line = {
+        "metric": "rays/sec (128 coarse + 64 fine samples) + achieved HBM GB/s vs roofline",
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic rays (x_pix ~ U[0,1)^2, orbit pose), random-init default.conf field, random 512x64x64 "
+                "latent",
+        "config": {"workload": f"BASELINE config 3: {R} rays/GPU x ({args.n_coarse} coarse + {args.n_fine} fine, "
+                               "n_fine_depth 0), conf/default.conf PixelNeRF field (3x512 ResnetFC, d_latent 512)",
+                   "rays_per_gpu": R, "n_coarse": args.n_coarse, "n_fine": args.n_fine,
+                   "field_samples_per_ray": samples_per_ray, "parallelism": f"ray-shard x{world} + RCCL gather"},
+        "roofline": {
+            "kernel": "field_fwd_kernel<32> (fused PE + latent lookup + ResnetFC on v_mfma_f32_16x16x4_f32)",
+            "bound": "mfma",
+            "achieved": round(achieved_tflops, 2),
+            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": None,
+            "flops_per_sample": fps,
+            "reference_flops_per_sample": reference_flops_per_sample(),
+            "avg_launch_ms": round(field_ms / max(field_launches, 1), 3),
+            "field_share_of_step": round(field_ms / (elapsed * 1e3), 4),
+        },
+    }
+    pmc = os.path.join(REPO, "profiles", "field_pmc.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            line["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,164 @@
+/*
+ * avr.h — C ABI of libavr_hip.so, the MI355X (gfx950) kernels for the
+ * coarse/fine volume-rendering hot path of yankeesong/adaptive-volume-rendering.
+ *
+ * Every entry point:
+ *   - takes DEVICE pointers owned by the caller (fp32, contiguous, ray-major,
+ *     sample-minor, channel-innermost unless stated) and an explicit HIP stream
+ *     (hipStream_t passed as void*; NULL = legacy default stream);
+ *   - allocates nothing, is stateless and re-entrant, and only enqueues work;
+ *   - returns 0 (AVR_OK) or an error code; avr_last_error_string() describes
+ *     the last failure on the calling thread.
+ *
+ * The reference is pure Python/PyTorch, so there is no foreign binding to
+ * replace; each function below replaces one stage of the reference's Python
+ * call chain (file:line in /root/reference) and is bound from Python by
+ * ctypes (adaptive-volume-rendering_amd/avr/_lib.py).
+ */
+#ifndef AVR_H_
+#define AVR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVR_ABI_VERSION 1
+#define AVR_MAX_BLOCKS 8
+
+enum {
+  AVR_OK = 0,
+  AVR_E_INVALID = 1001,     /* bad argument (null pointer, size out of range) */
+  AVR_E_UNSUPPORTED = 1002, /* configuration the kernels do not implement     */
+  AVR_E_HIP = 1003          /* a HIP runtime call failed                       */
+};
+
+int avr_version(void);
+const char* avr_last_error_string(void);
+/* Number of HIP devices visible (0 when no GPU); never fails. */
+int avr_device_count(void);
+
+/* ---------------------------------------------------------------- geometry
+ * get_world_rays — utils.py:315-336 (unproject :246-267, normalisation
+ * :309-312, transform_rigid :297-307).
+ *   x_pix  (n_sb, n_rays, 2)      pixel coordinates
+ *   K      (n_sb, 3, 3)           intrinsics
+ *   c2w    element (sb, r) at c2w + sb*c2w_sb_stride + r*c2w_ray_stride
+ *          (strides in floats; ray stride 0 = one pose per batch, the
+ *          stride-0 `expand` the reference's callers pass)
+ *   ro, rd (n_sb, n_rays, 3)      outputs                                      */
+int avr_world_rays(const float* x_pix, const float* K, const float* c2w, int64_t c2w_sb_stride,
+                   int64_t c2w_ray_stride, int64_t n_sb, int64_t n_rays, float* ro, float* rd, void* stream);
+
+/* depth_from_world(ro + rd*dist, c2w) — renderers.py:274-275, utils.py:358-361
+ * (transform_world2cam :270-281, a general 4x4 inverse per ray).
+ *   dist (n_sb, n_rays) -> depth (n_sb, n_rays)
+ *   ddepth_ddist (n_sb, n_rays) or NULL: d depth / d dist, for autograd.        */
+int avr_depth_from_world(const float* ro, const float* rd, const float* dist, const float* c2w,
+                         int64_t c2w_sb_stride, int64_t c2w_ray_stride, int64_t n_sb, int64_t n_rays,
+                         float* depth, float* ddepth_ddist, void* stream);
+
+/* ---------------------------------------------------------------- sampling
+ * sample_coarse — renderers.py:4-24 (infinity == -1 branch).
+ *   z (n_rays, n_samples) = near + (far-near)*i/N + U*(far-near)/N
+ *   noise (n_rays, n_samples) U[0,1) draws, or NULL: counter-based Philox
+ *   keyed on (seed, offset + ray, sample).                                     */
+int avr_sample_coarse(float near_, float far_, int64_t n_rays, int n_samples, const float* noise,
+                      uint64_t seed, uint64_t offset, float* z, void* stream);
+
+/* sample_fine + sample_depth + clamp + sort(cat(...)) — renderers.py:27-54,
+ * :56-66, :252-258.
+ *   weights  (n_rays, n_coarse)  coarse weights (detached)
+ *   z_coarse (n_rays, n_coarse)
+ *   u, u2    (n_rays, n_importance) the rand / rand_like draws,
+ *   noise_depth (n_rays, n_depth)   the randn_like draw;
+ *            all three NULL together => in-kernel Philox (seed, offset).
+ *   z_sorted (n_rays, n_coarse + n_importance + n_depth) ascending
+ *   idx      (n_rays, n_importance) int32 inverse-CDF bin (may be NULL)
+ *   z_fine   (n_rays, n_importance) unsorted importance z (may be NULL)
+ * n_coarse <= 256, total samples <= 512.                                       */
+int avr_sample_fine(const float* weights, const float* z_coarse, float near_, float far_, int64_t n_rays,
+                    int n_coarse, int n_importance, int n_depth, float depth_std, const float* u, const float* u2,
+                    const float* noise_depth, uint64_t seed, uint64_t offset, float* z_sorted, int32_t* idx,
+                    float* z_fine, void* stream);
+
+/* --------------------------------------------------------------- composite
+ * volume_integral — renderers.py:69-119.
+ *   z (n_rays, N), field (n_rays, N, 4) = (r, g, b, sigma) per sample
+ *   rgb (n_rays, 3), dist (n_rays), weights (n_rays, N) or NULL.
+ * N <= 1024.                                                                   */
+int avr_composite_fwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
+                      float infinity, float* rgb, float* dist, float* weights, void* stream);
+
+/* Gradient of volume_integral w.r.t. (r, g, b, sigma) (autograd of
+ * renderers.py:78-112; z carries no gradient in VolumeRenderer).
+ *   grad_rgb (n_rays,3), grad_dist (n_rays) or NULL, grad_weights (n_rays,N)
+ *   or NULL -> grad_field (n_rays, N, 4).                                      */
+int avr_composite_bwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
+                      float infinity, const float* grad_rgb, const float* grad_dist, const float* grad_weights,
+                      float* grad_field, void* stream);
+
+/* ------------------------------------------------------------------- field
+ * NewPixelNeRFNet.forward — models.py:739-863 with PositionalEncoding :41-87,
+ * SpatialEncoder.index :245-274 (bilinear, border, align_corners=True),
+ * ResnetFC :541-592, ResnetBlockFC :454-470 — for the default.conf family:
+ * use_encoder, use_xyz, normalize_z, PE on xyz only (include_input), raw
+ * viewdirs, ReLU, no BN, NS = 1.
+ *
+ * The lin_z projections are applied to the latent map once per texel
+ * (avr_field_latent_table) and bilinearly interpolated per sample: the
+ * interpolation and lin_z are both linear, so this is the same function with
+ * one third fewer per-sample FLOPs.                                            */
+typedef struct {
+  int d_in;        /* MLP input width without latent: 3 + 6*num_freqs + 3 */
+  int d_latent;    /* latent channels (multiple of 16, <= 1024)           */
+  int d_hidden;    /* 64, 128, 256 or 512                                 */
+  int n_blocks;    /* ResnetBlockFC count (<= AVR_MAX_BLOCKS)             */
+  int n_lin_z;     /* min(combine_layer, n_blocks)                        */
+  int num_freqs;   /* positional-encoding frequencies                     */
+  float freq_factor;
+} avr_field_dims;
+
+/* One ResnetFC's nn.Linear tensors, PyTorch layout (out, in) row-major. */
+typedef struct {
+  const float* lin_in_w;  const float* lin_in_b;
+  const float* lin_out_w; const float* lin_out_b;
+  const float* fc0_w[AVR_MAX_BLOCKS]; const float* fc0_b[AVR_MAX_BLOCKS];
+  const float* fc1_w[AVR_MAX_BLOCKS]; const float* fc1_b[AVR_MAX_BLOCKS];
+  const float* lin_z_w[AVR_MAX_BLOCKS]; const float* lin_z_b[AVR_MAX_BLOCKS];
+} avr_resnetfc_weights;
+
+/* Source-view buffers set by NewPixelNeRFNet.encode (models.py:705-734) and
+ * SpatialEncoder.forward (models.py:326-328). Host struct, passed by pointer. */
+typedef struct {
+  float poses[12];        /* world->cam rows [R | t], 3x4 row-major */
+  float focal[2];         /* (fx, -fy) as stored by encode           */
+  float c[2];
+  float image_shape[2];   /* (W, H)                                  */
+  float latent_scaling[2];
+  int latent_h, latent_w;
+} avr_view_desc;
+
+/* Floats needed for one packed ResnetFC (fragment-ordered weights + biases). */
+int avr_field_packed_floats(const avr_field_dims* dims, int64_t* n_floats);
+/* Repack one ResnetFC into MFMA fragment order (device -> device). */
+int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed, void* stream);
+/* table (n_lin_z, H*W, d_hidden) = lin_z[b].weight @ latent[:, texel] (no bias;
+ * the bias is folded into the packed biases). latent (d_latent, H, W).        */
+int avr_field_latent_table(const avr_field_dims* dims, const float* packed, const float* latent, int H, int W,
+                           float* table, void* stream);
+/* Field at xyz = ro[r] + rd[r] * z[r, s], viewdir = rd[r]; out (n_rays*n_samples, 4)
+ * = (sigmoid rgb, relu sigma).                                                 */
+int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
+                       const float* table, const float* ro, const float* rd, const float* z, int64_t n_rays,
+                       int n_samples, float* out, void* stream);
+/* Field at explicit points: xyz, viewdirs (n_points, 3) -> out (n_points, 4). */
+int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
+                         const float* table, const float* xyz, const float* viewdirs, int64_t n_points,
+                         float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVR_H_ */

@@ -222,10 +222,16 @@ def g1_volume_integral(R):
             sig[0, 3, :] = 0.0
             sig[0, 3, N // 2] = 1e4                # opaque spike
             rad = synth.hashed_uniform((1, R, N, 3), seed + 3)
-            rgb, dmap, w = REF_R.volume_integral(torch.from_numpy(z), torch.from_numpy(sig), torch.from_numpy(rad),
-                                                 white_back=wb)
+            ts, tr = torch.from_numpy(sig).requires_grad_(True), torch.from_numpy(rad).requires_grad_(True)
+            rgb, dmap, w = REF_R.volume_integral(torch.from_numpy(z), ts, tr, white_back=wb)
+            g_rgb = synth.hashed_centered((1, R, 3), seed + 4, 2.0)
+            g_dep = synth.hashed_centered((1, R, 1), seed + 5, 2.0)
+            ((rgb * torch.from_numpy(g_rgb)).sum() + (dmap * torch.from_numpy(g_dep)).sum()).backward()
             out[f"{key}_z"], out[f"{key}_sigma"], out[f"{key}_rad"] = z, sig, rad
-            out[f"{key}_rgb"], out[f"{key}_depth"], out[f"{key}_weights"] = rgb.numpy(), dmap.numpy(), w.numpy()
+            out[f"{key}_rgb"], out[f"{key}_depth"] = rgb.detach().numpy(), dmap.detach().numpy()
+            out[f"{key}_weights"] = w.detach().numpy()
+            out[f"{key}_grad_rgb"], out[f"{key}_grad_depth"] = g_rgb, g_dep
+            out[f"{key}_dsigma"], out[f"{key}_drad"] = ts.grad.numpy(), tr.grad.numpy()
     save("g1_volume_integral.npz", **out)
 
 

@@ -1,0 +1,96 @@
+"""CPU-only checks: the C-ABI library loads and exports every symbol that
+include/avr.h declares, the Python surface mirrors the reference's, and the
+product refuses host tensors (no CPU fallback). No kernel is launched."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "avr.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(avr_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_the_abi():
+    syms = declared_symbols()
+    for s in ("avr_world_rays", "avr_sample_coarse", "avr_sample_fine", "avr_composite_fwd", "avr_composite_bwd",
+              "avr_field_fwd_rays", "avr_field_fwd_points", "avr_depth_from_world", "avr_version"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from avr import _lib
+    lib = _lib.load()
+    for s in declared_symbols():
+        assert hasattr(lib, s), f"libavr_hip.so does not export {s}"
+    assert set(_lib.EXPORTED) == set(declared_symbols())
+    assert lib.avr_version() == _lib.ABI_VERSION
+
+
+def test_device_count_without_gpu_does_not_fail():
+    from avr import _lib
+    assert _lib.load().avr_device_count() >= 0
+
+
+def test_invalid_arguments_return_codes():
+    """Argument validation runs before any HIP call, so it is testable on CPU."""
+    from avr import _lib
+    lib = _lib.load()
+    rc = lib.avr_composite_fwd(None, None, 4, 8, 1, ctypes.c_float(1.8), None, None, None, None)
+    assert rc == 1001 and b"null" in lib.avr_last_error_string()
+    dims = _lib.FieldDims(42, 512, 384, 3, 3, 6, 1.5)  # 384 hidden is unsupported
+    n = ctypes.c_int64()
+    assert lib.avr_field_packed_floats(ctypes.byref(dims), ctypes.byref(n)) == 1001
+    dims = _lib.FieldDims(42, 512, 512, 3, 3, 6, 1.5)
+    assert lib.avr_field_packed_floats(ctypes.byref(dims), ctypes.byref(n)) == 0
+    # 3 blocks x 2 x 512^2 + lin_in (3 tiles) + lin_out + 3 lin_z x 512^2 (+ biases)
+    assert n.value == 3 * 2 * 512 * 512 + 3 * 16 * 512 + 512 * 16 + 3 * 512 * 512 + 512 * 7 + 16
+
+
+def test_ops_refuse_host_tensors():
+    from avr import _lib, ops
+    with pytest.raises(_lib.AVRError):
+        ops.composite_fwd(torch.zeros(4, 8), torch.zeros(4, 8, 4))
+    with pytest.raises(_lib.AVRError):
+        ops.world_rays(torch.zeros(1, 4, 2), torch.eye(3)[None], torch.eye(4).expand(1, 4, 4, 4))
+
+
+def test_renderer_surface_matches_reference():
+    import inspect
+    from avr import renderers
+    from avr.conf import Conf, default_conf
+    sig = inspect.signature(renderers.VolumeRenderer.__init__)
+    assert list(sig.parameters)[1:] == ["near", "far", "n_coarse", "n_fine", "n_fine_depth", "depth_std",
+                                        "white_back"]
+    r = renderers.VolumeRenderer.from_conf(default_conf()["normal_renderer"])
+    assert (r.n_coarse, r.n_fine, r.n_fine_depth, r.white_back) == (64, 32, 16, True)
+    r = renderers.VolumeRenderer.from_conf(Conf({}))
+    assert (r.n_coarse, r.n_fine, r.n_fine_depth, r.depth_std) == (32, 16, 8, 0.01)  # renderers.py:279-289
+    assert len(list(r.parameters())) == 0 and len(r.state_dict()) == 0  # contributes no state_dict keys
+    for name in ("sample_coarse", "sample_fine", "sample_depth", "volume_integral"):
+        assert callable(getattr(renderers, name))
+
+
+def test_model_state_dict_keys_match_reference_layout():
+    from avr.conf import default_conf
+    from avr.models import NewPixelNeRFNet
+    net = NewPixelNeRFNet(default_conf()["model"])
+    keys = set(net.state_dict())
+    for k in ("mlp_coarse.lin_in.weight", "mlp_coarse.lin_z.2.bias", "mlp_fine.blocks.2.fc_1.weight",
+              "mlp_fine.blocks.0.bn_0.running_mean", "mlp_coarse.lin_out.bias", "code._freqs"):
+        assert k in keys, k
+    assert net.mlp_coarse.lin_in.weight.shape == (512, 42)
+    assert net.d_latent == 512
+    from avr.field import fused_eligible
+    net.encoder.set_latent(torch.zeros(1, 512, 4, 4))
+    assert fused_eligible(net)
+    mv = NewPixelNeRFNet(default_conf(multiview=True)["model"])
+    mv.encoder.set_latent(torch.zeros(1, 512, 4, 4))
+    assert fused_eligible(mv) and len(mv.mlp_coarse.lin_z) == 3 and mv.mlp_coarse.n_blocks == 5
