@@ -184,9 +184,9 @@ using namespace avr;
 
 extern "C" int avr_composite_fwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
                                  float infinity, float* rgb, float* dist, float* weights, void* stream) {
-  AVR_REQUIRE(z && field && rgb && dist, "avr_composite_fwd: null pointer");
   AVR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples <= 1024, "avr_composite_fwd: n_samples must be in [1,1024]");
   if (n_rays == 0) return AVR_OK;
+  AVR_REQUIRE(z && field && rgb && dist, "avr_composite_fwd: null pointer");
   const size_t shm = (size_t)kCompWaves * (n_samples + 64) * sizeof(float);
   const unsigned grid = (unsigned)((n_rays + kCompWaves - 1) / kCompWaves);
   composite_fwd_kernel<<<grid, 64 * kCompWaves, shm, as_stream(stream)>>>(
@@ -197,9 +197,9 @@ extern "C" int avr_composite_fwd(const float* z, const float* field, int64_t n_r
 extern "C" int avr_composite_bwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
                                  float infinity, const float* grad_rgb, const float* grad_dist,
                                  const float* grad_weights, float* grad_field, void* stream) {
-  AVR_REQUIRE(z && field && grad_rgb && grad_field, "avr_composite_bwd: null pointer");
   AVR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples <= 1024, "avr_composite_bwd: n_samples must be in [1,1024]");
   if (n_rays == 0) return AVR_OK;
+  AVR_REQUIRE(z && field && grad_rgb && grad_field, "avr_composite_bwd: null pointer");
   const size_t shm = (size_t)kCompWaves * n_samples * (sizeof(double) + sizeof(double));
   const unsigned grid = (unsigned)((n_rays + kCompWaves - 1) / kCompWaves);
   composite_bwd_kernel<<<grid, 64 * kCompWaves, shm, as_stream(stream)>>>(

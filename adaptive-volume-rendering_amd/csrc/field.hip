@@ -503,8 +503,8 @@ extern "C" int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_des
   FieldArgs a{};
   int rc = field_common(dims, view, packed, table, &a);
   if (rc) return rc;
-  AVR_REQUIRE(ro && rd && z && out, "avr_field_fwd_rays: null pointer");
   AVR_REQUIRE(n_rays >= 0 && n_samples > 0, "avr_field_fwd_rays: bad sizes");
+  AVR_REQUIRE(n_rays == 0 || (ro && rd && z && out), "avr_field_fwd_rays: null pointer");
   a.ro = ro; a.rd = rd; a.z = z; a.n_samples = n_samples;
   a.M = n_rays * n_samples;
   a.out = reinterpret_cast<float4*>(out);
@@ -518,8 +518,8 @@ extern "C" int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_d
   FieldArgs a{};
   int rc = field_common(dims, view, packed, table, &a);
   if (rc) return rc;
-  AVR_REQUIRE(xyz && viewdirs && out, "avr_field_fwd_points: null pointer");
   AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points: bad size");
+  AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && out), "avr_field_fwd_points: null pointer");
   a.xyz = xyz; a.vd = viewdirs; a.n_samples = 1;
   a.M = n_points;
   a.out = reinterpret_cast<float4*>(out);

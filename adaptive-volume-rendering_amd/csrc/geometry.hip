@@ -113,10 +113,10 @@ using namespace avr;
 extern "C" int avr_world_rays(const float* x_pix, const float* K, const float* c2w, int64_t c2w_sb_stride,
                               int64_t c2w_ray_stride, int64_t n_sb, int64_t n_rays, float* ro, float* rd,
                               void* stream) {
-  AVR_REQUIRE(x_pix && K && c2w && ro && rd, "avr_world_rays: null pointer");
   AVR_REQUIRE(n_sb >= 0 && n_rays >= 0, "avr_world_rays: negative size");
   const int64_t n = n_sb * n_rays;
   if (n == 0) return AVR_OK;
+  AVR_REQUIRE(x_pix && K && c2w && ro && rd, "avr_world_rays: null pointer");
   world_rays_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(
       x_pix, K, c2w, c2w_sb_stride, c2w_ray_stride, n_sb, n_rays, ro, rd);
   return check_launch("world_rays_kernel");
@@ -125,10 +125,10 @@ extern "C" int avr_world_rays(const float* x_pix, const float* K, const float* c
 extern "C" int avr_depth_from_world(const float* ro, const float* rd, const float* dist, const float* c2w,
                                     int64_t c2w_sb_stride, int64_t c2w_ray_stride, int64_t n_sb, int64_t n_rays,
                                     float* depth, float* ddepth_ddist, void* stream) {
-  AVR_REQUIRE(ro && rd && dist && c2w && depth, "avr_depth_from_world: null pointer");
   AVR_REQUIRE(n_sb >= 0 && n_rays >= 0, "avr_depth_from_world: negative size");
   const int64_t n = n_sb * n_rays;
   if (n == 0) return AVR_OK;
+  AVR_REQUIRE(ro && rd && dist && c2w && depth, "avr_depth_from_world: null pointer");
   depth_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(ro, rd, dist, c2w, c2w_sb_stride,
                                                                            c2w_ray_stride, n_sb, n_rays, depth,
                                                                            ddepth_ddist);

@@ -160,10 +160,10 @@ using namespace avr;
 
 extern "C" int avr_sample_coarse(float near_, float far_, int64_t n_rays, int n_samples, const float* noise,
                                  uint64_t seed, uint64_t offset, float* z, void* stream) {
-  AVR_REQUIRE(z, "avr_sample_coarse: null output");
   AVR_REQUIRE(n_rays >= 0 && n_samples > 0, "avr_sample_coarse: bad sizes");
   const int64_t n = n_rays * n_samples;
   if (n == 0) return AVR_OK;
+  AVR_REQUIRE(z, "avr_sample_coarse: null output");
   sample_coarse_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(near_, far_, n_rays, n_samples,
                                                                                  noise, seed, offset, z);
   return check_launch("sample_coarse_kernel");
@@ -173,8 +173,8 @@ extern "C" int avr_sample_fine(const float* weights, const float* z_coarse, floa
                                int n_coarse, int n_importance, int n_depth, float depth_std, const float* u,
                                const float* u2, const float* noise_depth, uint64_t seed, uint64_t offset,
                                float* z_sorted, int32_t* idx, float* z_fine, void* stream) {
-  AVR_REQUIRE(weights && z_coarse && z_sorted, "avr_sample_fine: null pointer");
   AVR_REQUIRE(n_rays >= 0, "avr_sample_fine: negative n_rays");
+  AVR_REQUIRE(n_rays == 0 || (weights && z_coarse && z_sorted), "avr_sample_fine: null pointer");
   AVR_REQUIRE(n_coarse > 0 && n_coarse <= kMaxCoarse, "avr_sample_fine: n_coarse must be in [1, %d]", kMaxCoarse);
   AVR_REQUIRE(n_importance >= 0 && n_depth >= 0, "avr_sample_fine: negative sample count");
   const int ntot = n_coarse + n_importance + n_depth;

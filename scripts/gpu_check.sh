@@ -8,8 +8,10 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
 echo "== host: $(nproc) cpus; $(python -c 'import torch;print(torch.__version__)')"
-timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
-rc=$?; tail -5 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || { echo "pytest gpu failed rc=$rc"; exit $rc; }
+timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+rc=$?; tail -15 $OUT/pytest_gpu.log
+# test failures (rc 1) still let smoke/bench run; a crash, abort or timeout stops here
+[ $rc -le 1 ] || { echo "pytest gpu crashed rc=$rc"; exit $rc; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 rc=$?; cat $OUT/smoke.log | tail -3; [ $rc -eq 0 ] || { echo "smoke failed rc=$rc"; exit $rc; }
 timeout -k 10 600 python bench.py --steps 5 --warmup 2 > $OUT/bench.log 2>&1
