@@ -24,7 +24,11 @@ c_float = ctypes.c_float
 
 class FieldDims(ctypes.Structure):
     _fields_ = [("d_in", c_int), ("d_latent", c_int), ("d_hidden", c_int), ("n_blocks", c_int),
-                ("n_lin_z", c_int), ("num_freqs", c_int), ("freq_factor", c_float)]
+                ("n_lin_z", c_int), ("num_freqs", c_int), ("freq_factor", c_float), ("precision", c_int)]
+
+
+FIELD_FP32 = 0
+FIELD_X3 = 1
 
 
 class ResnetFCWeights(ctypes.Structure):

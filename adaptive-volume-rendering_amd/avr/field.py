@@ -67,8 +67,17 @@ class _Packed:
         self.tables = {}
 
 
+PRECISIONS = {"fp32": _lib.FIELD_FP32, "x3": _lib.FIELD_X3}
+
+
 class FusedField:
-    def __init__(self, net):
+    """precision: "x3" (default) = split-fp16 MFMA (3 products per fp32 product,
+    fp32 accumulation, within fp32 noise of the fp32 path); "fp32" = fp32 MFMA."""
+
+    def __init__(self, net, precision="x3"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
+        self.precision = precision
         self.net = net
         self._packed = {}     # coarse(bool) -> (key, _Packed)
         self._view_cache = {}
@@ -81,7 +90,8 @@ class FusedField:
     def dims(self, mlp):
         code = self.net.code
         return FieldDims(self.net.d_in, self.net.d_latent, mlp.d_hidden, mlp.n_blocks,
-                         min(mlp.combine_layer, mlp.n_blocks), code.num_freqs, _freq_factor(code))
+                         min(mlp.combine_layer, mlp.n_blocks), code.num_freqs, _freq_factor(code),
+                         PRECISIONS[self.precision])
 
     def packed(self, coarse):
         mlp = self._mlp(coarse)
@@ -163,6 +173,7 @@ class FusedField:
         entry = self.packed(coarse)
         table = self.table(coarse, sb)
         out = torch.empty(R * N, 4, device=z.device, dtype=F32)
+        entry.dims.precision = PRECISIONS[self.precision]
         call("avr_field_fwd_rays", ctypes.byref(entry.dims), ctypes.byref(self.view(sb)), ptr(entry.packed),
              ptr(table), ptr(ro), ptr(rd), ptr(z), R, N, ptr(out), stream_of(z))
         return out
@@ -177,6 +188,7 @@ class FusedField:
             v = viewdirs.reshape(SB, B, 3)[sb].to(F32).contiguous()
             require_device(p, v)
             table = self.table(coarse, sb)
+            entry.dims.precision = PRECISIONS[self.precision]
             call("avr_field_fwd_points", ctypes.byref(entry.dims), ctypes.byref(self.view(sb)), ptr(entry.packed),
                  ptr(table), ptr(p), ptr(v), B, ptr(out[sb]), stream_of(p))
         return out

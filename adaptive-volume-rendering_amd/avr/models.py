@@ -222,7 +222,8 @@ class NewPixelNeRFNet(nn.Module):
         self.register_buffer("c", torch.empty(1, 2), persistent=False)
         self.d_in, self.d_out, self.d_latent = d_in, 4, d_latent
         self.num_objs, self.num_views_per_obj = 0, 1
-        self.use_fused = True  # HIP field under no_grad (avr.field)
+        self.use_fused = True           # HIP field under no_grad (avr.field)
+        self.field_precision = "x3"     # "x3" split-fp16 MFMA | "fp32" MFMA
         self._fused = None
 
     def encode_latent(self, latent, poses, focal, c=None, image_shape=None):
@@ -264,7 +265,8 @@ class NewPixelNeRFNet(nn.Module):
     def fused(self):
         from .field import FusedField
         if self._fused is None:
-            self._fused = FusedField(self)
+            self._fused = FusedField(self, self.field_precision)
+        self._fused.precision = self.field_precision
         return self._fused
 
     def can_fuse(self, xyz):

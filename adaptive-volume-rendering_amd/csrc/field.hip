@@ -19,27 +19,11 @@
 // lin_z is applied to the latent map per texel (avr_field_latent_table) and
 // bilinearly interpolated per sample; every bias (b_in + bz0, b1 + bz_{b+1},
 // ...) is pre-summed at pack time.
-#include <math.h>
-
-#include "avr_common.h"
+#include "field_common.h"
 
 namespace avr {
 
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-constexpr int kFieldWaves = 4;  // 256-thread workgroups, one wave per SIMD
-constexpr int kSPW = 16;        // samples per wave (MFMA column count)
-constexpr int kInTiles = 3;     // lin_in K = 42 features padded to 48
-
 // ----------------------------------------------------------------- layout
-struct Layout {
-  int NT;                 // d_hidden / 16
-  int KTl;                // d_latent / 16
-  int64_t w_in, w_out, fc0[AVR_MAX_BLOCKS], fc1[AVR_MAX_BLOCKS], lin_z[AVR_MAX_BLOCKS];
-  int64_t b_in, b_out, b_fc0[AVR_MAX_BLOCKS], b_fc1[AVR_MAX_BLOCKS];
-  int64_t total;          // floats
-};
-
 static int make_layout(const avr_field_dims* d, Layout* L) {
   AVR_REQUIRE(d, "field: null dims");
   AVR_REQUIRE(d->d_hidden == 64 || d->d_hidden == 128 || d->d_hidden == 256 || d->d_hidden == 512,
@@ -51,10 +35,11 @@ static int make_layout(const avr_field_dims* d, Layout* L) {
   AVR_REQUIRE(d->n_lin_z >= 0 && d->n_lin_z <= d->n_blocks, "field: n_lin_z must be in [0, n_blocks]");
   AVR_REQUIRE(d->num_freqs >= 0 && 3 + 6 * d->num_freqs + 3 == d->d_in && d->d_in <= 16 * kInTiles,
               "field: d_in %d != 6*num_freqs+6 or > 48 (fused path supports PE(xyz)+raw viewdirs)", d->d_in);
-  const int NT = d->d_hidden / 16;
+  const int NT = d->d_hidden / 16, KC = d->d_hidden / 32;
   L->NT = NT;
   L->KTl = d->d_latent / 16;
-  const int64_t tile = 64 * 4;  // floats per (t, ot) fragment block
+  const int64_t tile = 64 * 4;  // floats per (t, ot) fp32 fragment block
+  const int64_t tile16 = 64 * 8;  // floats per (c, ft) fp16 hi/lo fragment block (64 lanes x 32 B)
   int64_t o = 0;
   L->w_in = o; o += (int64_t)kInTiles * NT * tile;
   for (int b = 0; b < d->n_blocks; ++b) {
@@ -69,6 +54,14 @@ static int make_layout(const avr_field_dims* d, Layout* L) {
     L->b_fc1[b] = o; o += d->d_hidden;
   }
   L->b_out = o; o += 16;
+  o = (o + 63) & ~(int64_t)63;
+  L->x3_hdr = o; o += 64;
+  L->x3_in = o; o += (int64_t)kX3InChunks * NT * tile16;
+  for (int b = 0; b < d->n_blocks; ++b) {
+    L->x3_fc0[b] = o; o += (int64_t)KC * NT * tile16;
+    L->x3_fc1[b] = o; o += (int64_t)KC * NT * tile16;
+  }
+  L->x3_out = o; o += (int64_t)KC * tile16;
   L->total = o;
   return AVR_OK;
 }
@@ -96,11 +89,41 @@ __global__ void pack_bias_kernel(const float* __restrict__ a, const float* __res
   dst[i] = (i < n) ? (b ? fadd(a[i], b[i]) : a[i]) : 0.f;
 }
 
-// ----------------------------------------------------------------- MFMA tiles
-__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+// max|W| of one layer as float bits (atomicMax on non-negative floats = on their bits)
+__global__ void absmax_kernel(const float* __restrict__ W, int64_t n, unsigned* __restrict__ out) {
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(W[i]));
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
+// x3 fragments: dst[((c*FTt + ft)*64 + l)*16 + {e, 8+e}] = (hi, lo) of
+// W[16ft + (l&15)][32c + (e<4 ? 4g+e : 16+4g+e-4)] * s_w, g = l>>4, with
+// s_w = 2^(14 - ceil-exponent of max|W|) from the layer's header word.
+__global__ void pack_x3_kernel(const float* __restrict__ W, int out_dim, int in_dim, int KC, int FTt,
+                               const unsigned* __restrict__ maxbits, _Float16* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)KC * FTt * 64 * 8;
+  if (i >= n) return;
+  const int e = (int)(i & 7);
+  const int l = (int)((i >> 3) & 63);
+  const int64_t blk = i >> 9;
+  const int ft = (int)(blk % FTt), c = (int)(blk / FTt);
+  const int g = l >> 4;
+  const int row = 16 * ft + (l & 15);
+  const int col = 32 * c + (e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4));
+  const float sw = pow2_scale_for(__uint_as_float(*maxbits));
+  const float v = (row < out_dim && col < in_dim) ? W[(int64_t)row * in_dim + col] * sw : 0.f;
+  const _Float16 hi = (_Float16)v;
+  const _Float16 lo = (_Float16)(v - (float)hi);
+  const int64_t base = (((int64_t)c * FTt + ft) * 64 + l) * 16;
+  dst[base + e] = hi;
+  dst[base + 8 + e] = lo;
+}
+
+// ----------------------------------------------------------------- fp32 MFMA tiles
 // acc[ot] += sum_t sum_r A(ot,t,r) B(t,r); A from packed global [t][ot][lane]
 // through a P-deep register ring that runs ahead across t iterations, B from
 // the wave's LDS slab [t][lane].
@@ -146,11 +169,6 @@ __device__ __forceinline__ void add_bias(floatx4 (&acc)[NT], const float* __rest
   for (int ot = 0; ot < NT; ++ot) acc[ot] += *reinterpret_cast<const floatx4*>(bias + 16 * ot + 4 * g);
 }
 
-struct Bilinear {
-  int off[4];    // texel * d_hidden (float offsets into one lin_z table)
-  float w[4];
-};
-
 // acc += sum_c w_c * Z[texel_c][features of this lane]
 template <int NT>
 __device__ __forceinline__ void add_interp(floatx4 (&acc)[NT], const float* __restrict__ Z, const Bilinear& bl,
@@ -163,7 +181,7 @@ __device__ __forceinline__ void add_interp(floatx4 (&acc)[NT], const float* __re
     for (int k = 0; k < CH; ++k)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        v[k][c] = *reinterpret_cast<const floatx4*>(Z + bl.off[c] + 16 * (o0 + k) + 4 * g);
+        v[k][c] = *reinterpret_cast<const floatx4*>(Z + (int64_t)bl.tex[c] * (NT * 16) + 16 * (o0 + k) + 4 * g);
 #pragma unroll
     for (int k = 0; k < CH; ++k)
       acc[o0 + k] += ((bl.w[0] * v[k][0] + bl.w[1] * v[k][1]) + bl.w[2] * v[k][2]) + bl.w[3] * v[k][3];
@@ -180,33 +198,6 @@ __device__ __forceinline__ void store_relu(floatx4* slab, const floatx4 (&acc)[N
   }
 }
 
-struct View {
-  float R[9], t[3];
-  float focal[2], c[2], scale[2];
-  int H, W;
-};
-
-struct FieldArgs {
-  const float* packed;
-  const float* table;
-  int64_t table_stride;  // floats per lin_z table (HW * d_hidden)
-  Layout L;
-  View v;
-  int n_blocks, n_lin_z, num_freqs;
-  float freq_factor;
-  // sample source: rays (z != null) or explicit points
-  const float* ro; const float* rd; const float* z; int n_samples;
-  const float* xyz; const float* vd;
-  int64_t M;
-  float4* out;
-};
-
-__device__ __forceinline__ float dot3(const float* R, float a, float b, float c) {
-  return fadd(fadd(fmul(R[0], a), fmul(R[1], b)), fmul(R[2], c));
-}
-
-__device__ __forceinline__ float sigmoidf_(float x) { return fdiv(1.0f, fadd(1.0f, expf(-x))); }
-
 template <int NT>
 __global__ void __launch_bounds__(256, 1) field_fwd_kernel(FieldArgs a) {
   extern __shared__ floatx4 lds[];
@@ -217,78 +208,16 @@ __global__ void __launch_bounds__(256, 1) field_fwd_kernel(FieldArgs a) {
   const bool valid = m < a.M;
   const int64_t mm = valid ? m : a.M - 1;
 
-  // ---- sample position and view direction
-  float x0, x1, x2, d0, d1, d2;
-  if (a.z) {
-    const int64_t r = mm / a.n_samples;
-    const float zz = a.z[mm];
-    d0 = a.rd[3 * r]; d1 = a.rd[3 * r + 1]; d2 = a.rd[3 * r + 2];
-    x0 = fadd(a.ro[3 * r], fmul(d0, zz));
-    x1 = fadd(a.ro[3 * r + 1], fmul(d1, zz));
-    x2 = fadd(a.ro[3 * r + 2], fmul(d2, zz));
-  } else {
-    x0 = a.xyz[3 * mm]; x1 = a.xyz[3 * mm + 1]; x2 = a.xyz[3 * mm + 2];
-    d0 = a.vd[3 * mm]; d1 = a.vd[3 * mm + 1]; d2 = a.vd[3 * mm + 2];
-  }
-  const View& v = a.v;
-  // xyz_rot = R xyz (models.py:755-757); camera-space point = xyz_rot + t (:758)
-  const float xr0 = dot3(v.R + 0, x0, x1, x2), xr1 = dot3(v.R + 3, x0, x1, x2), xr2 = dot3(v.R + 6, x0, x1, x2);
-  const float xc0 = fadd(xr0, v.t[0]), xc1 = fadd(xr1, v.t[1]), xc2 = fadd(xr2, v.t[2]);
-
-  // ---- z_feature (models.py:763-789): [xyz_rot, PE(xyz_rot), R viewdir], padded to 48.
-  // This lane writes features 16t + 4g + r of its sample to slab[t][lane].
-  {
-    const float vr0 = dot3(v.R + 0, d0, d1, d2), vr1 = dot3(v.R + 3, d0, d1, d2), vr2 = dot3(v.R + 6, d0, d1, d2);
-    const float xr[3] = {xr0, xr1, xr2};
-    const float vr[3] = {vr0, vr1, vr2};
-    const int npe = 6 * a.num_freqs;
+  // ---- sample geometry, z_feature (features 16t + 4g + r of this lane's sample -> slab[t][lane])
+  const SampleGeom sg = sample_geom(a, mm);
 #pragma unroll
-    for (int t = 0; t < kInTiles; ++t) {
-      float f[4];
+  for (int t = 0; t < kInTiles; ++t) {
+    float f[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int k = 16 * t + 4 * g + r;
-        float val = 0.f;
-        if (k < 3) {
-          val = xr[k];
-        } else if (k < 3 + npe) {
-          // embed[jj][dd] = sin(phase_jj + x_dd * freq_jj), jj = 2*freq + {0: sin, 1: cos}
-          const int q = k - 3, jj = q / 3, dd = q - 3 * jj;
-          const float freq = fmul(a.freq_factor, exp2f((float)(jj >> 1)));
-          const float phase = (jj & 1) ? 1.5707963705062866f : 0.f;  // fp32(pi/2)
-          val = sinf(fadd(phase, fmul(xr[dd], freq)));
-        } else if (k < 6 + npe) {
-          val = vr[k - 3 - npe];
-        }
-        f[r] = val;
-      }
-      slab[t * 64 + lane] = floatx4{f[0], f[1], f[2], f[3]};
-    }
+    for (int r = 0; r < 4; ++r) f[r] = z_feature(sg, 16 * t + 4 * g + r, a.num_freqs, a.freq_factor);
+    slab[t * 64 + lane] = floatx4{f[0], f[1], f[2], f[3]};
   }
-
-  // ---- bilinear latent lookup (SpatialEncoder.index, models.py:260-273):
-  // uv = -xyz_c[:2]/xyz_c[2] * focal + c; grid = uv * (latent_scaling/image_shape) - 1;
-  // grid_sample(bilinear, border, align_corners=True).
-  Bilinear bl;
-  {
-    const float u = fadd(fmul(fdiv(-xc0, xc2), v.focal[0]), v.c[0]);
-    const float w = fadd(fmul(fdiv(-xc1, xc2), v.focal[1]), v.c[1]);
-    const float gx = fsub(fmul(u, v.scale[0]), 1.0f), gy = fsub(fmul(w, v.scale[1]), 1.0f);
-    float ix = fmul(fdiv(fadd(gx, 1.0f), 2.0f), (float)(v.W - 1));
-    float iy = fmul(fdiv(fadd(gy, 1.0f), 2.0f), (float)(v.H - 1));
-    ix = fminf(fmaxf(ix, 0.f), (float)(v.W - 1));
-    iy = fminf(fmaxf(iy, 0.f), (float)(v.H - 1));
-    const float fx0 = floorf(ix), fy0 = floorf(iy);
-    const float wx1 = fsub(ix, fx0), wy1 = fsub(iy, fy0);
-    const float wx0 = fsub(fadd(fx0, 1.0f), ix), wy0 = fsub(fadd(fy0, 1.0f), iy);
-    const int X0 = (int)fx0, Y0 = (int)fy0;
-    const int X1 = X0 + 1 < v.W ? X0 + 1 : v.W - 1, Y1 = Y0 + 1 < v.H ? Y0 + 1 : v.H - 1;
-    const int HID = NT * 16;
-    bl.off[0] = (Y0 * v.W + X0) * HID; bl.w[0] = fmul(wx0, wy0);
-    bl.off[1] = (Y0 * v.W + X1) * HID; bl.w[1] = fmul(wx1, wy0);
-    bl.off[2] = (Y1 * v.W + X0) * HID; bl.w[2] = fmul(wx0, wy1);
-    bl.off[3] = (Y1 * v.W + X1) * HID; bl.w[3] = fmul(wx1, wy1);
-  }
+  const Bilinear& bl = sg.bl;
 
   const floatx4* P4 = reinterpret_cast<const floatx4*>(a.packed);
   floatx4 h[NT], tt[NT];
@@ -366,6 +295,19 @@ static int pack_linear(const float* W, int out_dim, int in_dim, int NTo, int KTi
   return check_launch("pack_linear_kernel");
 }
 
+static int pack_x3(const float* W, int out_dim, int in_dim, int KC, int FTt, unsigned* maxbits, float* dst,
+                   hipStream_t s) {
+  AVR_REQUIRE(W, "avr_field_pack: null weight tensor");
+  const int64_t nw = (int64_t)out_dim * in_dim;
+  absmax_kernel<<<(unsigned)((nw + 255) / 256 < 256 ? (nw + 255) / 256 : 256), 256, 0, s>>>(W, nw, maxbits);
+  int rc = check_launch("absmax_kernel");
+  if (rc) return rc;
+  const int64_t n = (int64_t)KC * FTt * 64 * 8;
+  pack_x3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(W, out_dim, in_dim, KC, FTt, maxbits,
+                                                            reinterpret_cast<_Float16*>(dst));
+  return check_launch("pack_x3_kernel");
+}
+
 static int pack_bias(const float* a, const float* b, int n, int n_pad, float* dst, hipStream_t s) {
   AVR_REQUIRE(a, "avr_field_pack: null bias tensor");
   pack_bias_kernel<<<(unsigned)((n_pad + 255) / 256), 256, 0, s>>>(a, b, n, n_pad, dst);
@@ -432,7 +374,10 @@ static int field_common(const avr_field_dims* dims, const avr_view_desc* view, c
   return AVR_OK;
 }
 
-static int dispatch_field(int d_hidden, const FieldArgs& a, hipStream_t s) {
+static int dispatch_field(const avr_field_dims* dims, const FieldArgs& a, hipStream_t s) {
+  const int d_hidden = dims->d_hidden;
+  if (dims->precision == AVR_FIELD_X3) return dispatch_field_x3(d_hidden, a, s);
+  AVR_REQUIRE(dims->precision == AVR_FIELD_FP32, "field: unknown precision %d", dims->precision);
   switch (d_hidden) {
     case 64: return launch_field<4>(a, s);
     case 128: return launch_field<8>(a, s);
@@ -476,7 +421,18 @@ extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_wei
     if ((rc = pack_linear(w->lin_z_w[b], H, dims->d_latent, NT, L.KTl, packed + L.lin_z[b], s))) return rc;
   if ((rc = pack_bias(w->lin_in_b, dims->n_lin_z > 0 ? w->lin_z_b[0] : nullptr, H, H, packed + L.b_in, s)))
     return rc;
-  return pack_bias(w->lin_out_b, nullptr, 4, 16, packed + L.b_out, s);
+  if ((rc = pack_bias(w->lin_out_b, nullptr, 4, 16, packed + L.b_out, s))) return rc;
+  // split-fp16 fragments (header word per layer: 0 lin_in, 1 lin_out, 2+2b fc0[b], 3+2b fc1[b])
+  unsigned* hdr = reinterpret_cast<unsigned*>(packed + L.x3_hdr);
+  if (hipMemsetAsync(hdr, 0, 64 * sizeof(float), s) != hipSuccess) return fail(AVR_E_HIP, "avr_field_pack: memset");
+  const int KC = H / 32;
+  if ((rc = pack_x3(w->lin_in_w, H, dims->d_in, kX3InChunks, NT, hdr + 0, packed + L.x3_in, s))) return rc;
+  if ((rc = pack_x3(w->lin_out_w, 4, H, KC, 1, hdr + 1, packed + L.x3_out, s))) return rc;
+  for (int b = 0; b < dims->n_blocks; ++b) {
+    if ((rc = pack_x3(w->fc0_w[b], H, H, KC, NT, hdr + 2 + 2 * b, packed + L.x3_fc0[b], s))) return rc;
+    if ((rc = pack_x3(w->fc1_w[b], H, H, KC, NT, hdr + 3 + 2 * b, packed + L.x3_fc1[b], s))) return rc;
+  }
+  return AVR_OK;
 }
 
 extern "C" int avr_field_latent_table(const avr_field_dims* dims, const float* packed, const float* latent, int H,
@@ -509,7 +465,7 @@ extern "C" int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_des
   a.M = n_rays * n_samples;
   a.out = reinterpret_cast<float4*>(out);
   if (a.M == 0) return AVR_OK;
-  return dispatch_field(dims->d_hidden, a, as_stream(stream));
+  return dispatch_field(dims, a, as_stream(stream));
 }
 
 extern "C" int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
@@ -524,5 +480,5 @@ extern "C" int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_d
   a.M = n_points;
   a.out = reinterpret_cast<float4*>(out);
   if (a.M == 0) return AVR_OK;
-  return dispatch_field(dims->d_hidden, a, as_stream(stream));
+  return dispatch_field(dims, a, as_stream(stream));
 }

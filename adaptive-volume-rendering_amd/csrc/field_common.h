@@ -1,0 +1,149 @@
+// Shared pieces of the radiance-field kernels (field.hip: fp32 MFMA path and
+// packing; field_x3.hip: split-fp16 MFMA path).
+#pragma once
+#include <math.h>
+
+#include "avr_common.h"
+
+namespace avr {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+constexpr int kFieldWaves = 4;   // 256-thread workgroups, one wave per SIMD
+constexpr int kSPW = 16;         // fp32 path: samples per wave (MFMA column count)
+constexpr int kInTiles = 3;      // fp32 path: lin_in K = 42 features padded to 48
+constexpr int kX3Samples = 64;   // x3 path: samples per workgroup (4 MFMA column groups)
+constexpr int kX3InChunks = 2;   // x3 path: lin_in K padded to 64 = 2 chunks of 32
+constexpr int kX3MaxLayers = 2 + 2 * AVR_MAX_BLOCKS;
+
+// Packed blob (floats). fp32 part: [t][ot][lane] float4 fragments for
+// v_mfma_f32_16x16x4_f32 (also used by the latent-table kernel for lin_z).
+// x3 part: [c][ft][lane][16 x fp16] = (hi[8], lo[8]) fragments for
+// v_mfma_f32_16x16x32_f16, scaled by 2^e per layer (header holds max|W| bits).
+struct Layout {
+  int NT;                 // d_hidden / 16
+  int KTl;                // d_latent / 16
+  int64_t w_in, w_out, fc0[AVR_MAX_BLOCKS], fc1[AVR_MAX_BLOCKS], lin_z[AVR_MAX_BLOCKS];
+  int64_t b_in, b_out, b_fc0[AVR_MAX_BLOCKS], b_fc1[AVR_MAX_BLOCKS];
+  int64_t x3_hdr, x3_in, x3_out, x3_fc0[AVR_MAX_BLOCKS], x3_fc1[AVR_MAX_BLOCKS];
+  int64_t total;          // floats
+};
+
+struct View {
+  float R[9], t[3];
+  float focal[2], c[2], scale[2];
+  int H, W;
+};
+
+struct FieldArgs {
+  const float* packed;
+  const float* table;
+  int64_t table_stride;  // floats per lin_z table (HW * d_hidden)
+  Layout L;
+  View v;
+  int n_blocks, n_lin_z, num_freqs;
+  float freq_factor;
+  // sample source: rays (z != null) or explicit points
+  const float* ro; const float* rd; const float* z; int n_samples;
+  const float* xyz; const float* vd;
+  int64_t M;
+  float4* out;
+};
+
+struct Bilinear {
+  int tex[4];   // texel index of the 4 corners
+  float w[4];
+};
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ floatx4 mfma32h(half8 a, half8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float dot3(const float* R, float a, float b, float c) {
+  return fadd(fadd(fmul(R[0], a), fmul(R[1], b)), fmul(R[2], c));
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return fdiv(1.0f, fadd(1.0f, expf(-x))); }
+
+// Per-sample geometry of NewPixelNeRFNet.forward (models.py:753-808):
+// xyz_rot = R xyz, camera point = xyz_rot + t, R viewdir, and the bilinear
+// corners of SpatialEncoder.index (models.py:260-273: uv*scale - 1, then
+// grid_sample bilinear / border / align_corners=True).
+struct SampleGeom {
+  float xr[3], vr[3];
+  Bilinear bl;
+};
+
+__device__ __forceinline__ SampleGeom sample_geom(const FieldArgs& a, int64_t mm) {
+  float x0, x1, x2, d0, d1, d2;
+  if (a.z) {
+    const int64_t r = mm / a.n_samples;
+    const float zz = a.z[mm];
+    d0 = a.rd[3 * r]; d1 = a.rd[3 * r + 1]; d2 = a.rd[3 * r + 2];
+    x0 = fadd(a.ro[3 * r], fmul(d0, zz));      // ros + rds * z (renderers.py:171, :260)
+    x1 = fadd(a.ro[3 * r + 1], fmul(d1, zz));
+    x2 = fadd(a.ro[3 * r + 2], fmul(d2, zz));
+  } else {
+    x0 = a.xyz[3 * mm]; x1 = a.xyz[3 * mm + 1]; x2 = a.xyz[3 * mm + 2];
+    d0 = a.vd[3 * mm]; d1 = a.vd[3 * mm + 1]; d2 = a.vd[3 * mm + 2];
+  }
+  const View& v = a.v;
+  SampleGeom s;
+  s.xr[0] = dot3(v.R + 0, x0, x1, x2); s.xr[1] = dot3(v.R + 3, x0, x1, x2); s.xr[2] = dot3(v.R + 6, x0, x1, x2);
+  s.vr[0] = dot3(v.R + 0, d0, d1, d2); s.vr[1] = dot3(v.R + 3, d0, d1, d2); s.vr[2] = dot3(v.R + 6, d0, d1, d2);
+  const float xc0 = fadd(s.xr[0], v.t[0]), xc1 = fadd(s.xr[1], v.t[1]), xc2 = fadd(s.xr[2], v.t[2]);
+  const float u = fadd(fmul(fdiv(-xc0, xc2), v.focal[0]), v.c[0]);
+  const float w = fadd(fmul(fdiv(-xc1, xc2), v.focal[1]), v.c[1]);
+  const float gx = fsub(fmul(u, v.scale[0]), 1.0f), gy = fsub(fmul(w, v.scale[1]), 1.0f);
+  float ix = fmul(fdiv(fadd(gx, 1.0f), 2.0f), (float)(v.W - 1));
+  float iy = fmul(fdiv(fadd(gy, 1.0f), 2.0f), (float)(v.H - 1));
+  ix = fminf(fmaxf(ix, 0.f), (float)(v.W - 1));
+  iy = fminf(fmaxf(iy, 0.f), (float)(v.H - 1));
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const float wx1 = fsub(ix, fx0), wy1 = fsub(iy, fy0);
+  const float wx0 = fsub(fadd(fx0, 1.0f), ix), wy0 = fsub(fadd(fy0, 1.0f), iy);
+  const int X0 = (int)fx0, Y0 = (int)fy0;
+  const int X1 = X0 + 1 < v.W ? X0 + 1 : v.W - 1, Y1 = Y0 + 1 < v.H ? Y0 + 1 : v.H - 1;
+  s.bl.tex[0] = Y0 * v.W + X0; s.bl.w[0] = fmul(wx0, wy0);
+  s.bl.tex[1] = Y0 * v.W + X1; s.bl.w[1] = fmul(wx1, wy0);
+  s.bl.tex[2] = Y1 * v.W + X0; s.bl.w[2] = fmul(wx0, wy1);
+  s.bl.tex[3] = Y1 * v.W + X1; s.bl.w[3] = fmul(wx1, wy1);
+  return s;
+}
+
+// Feature k of z_feature (models.py:763-789): [xyz_rot (3), PE (6*num_freqs),
+// R viewdir (3)], zero beyond. PE entry q = 3*jj + dd is
+// sin(phase_jj + x_dd * freq_jj) with jj = 2*freq_index + {0: sin, 1: pi/2}.
+__device__ __forceinline__ float z_feature(const SampleGeom& s, int k, int num_freqs, float freq_factor) {
+  // selects instead of runtime-indexed arrays keep everything in registers (no scratch)
+  const int npe = 6 * num_freqs;
+  const auto pick = [](const float* v, int i) { return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]); };
+  if (k < 3) return pick(s.xr, k);
+  if (k < 3 + npe) {
+    const int q = k - 3, jj = q / 3, dd = q - 3 * jj;
+    const float freq = fmul(freq_factor, exp2f((float)(jj >> 1)));
+    const float phase = (jj & 1) ? 1.5707963705062866f : 0.f;  // fp32(pi/2)
+    return sinf(fadd(phase, fmul(pick(s.xr, dd), freq)));
+  }
+  if (k < 6 + npe) return pick(s.vr, k - 3 - npe);
+  return 0.f;
+}
+
+// Power-of-two scale that maps max|x| to [2^13, 2^14] (fp16 split operands).
+// The exponent is clamped to [-60, 60] so scale products stay finite.
+__device__ __forceinline__ float pow2_scale_for(float maxabs) {
+  if (!(maxabs > 0.f) || !isfinite(maxabs)) return 1.0f;
+  int e;
+  frexpf(maxabs, &e);   // maxabs = m * 2^e, m in [0.5, 1)
+  const int k = 14 - e;
+  return ldexpf(1.0f, k < -60 ? -60 : (k > 60 ? 60 : k));
+}
+
+int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s);
+
+}  // namespace avr

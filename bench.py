@@ -29,6 +29,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "adaptive-volume-rendering_amd"))
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (= fp32 vector), MI355X_MICROARCH.md
+FP16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 MFMA
 HBM_PEAK_GBS = 8000.0
 
 
@@ -158,6 +159,8 @@ def main():
     ap.add_argument("--rays", type=int, default=65536, help="rays per GPU per step")
     ap.add_argument("--n-coarse", type=int, default=128)
     ap.add_argument("--n-fine", type=int, default=64)
+    ap.add_argument("--precision", choices=["x3", "fp32"], default="x3",
+                    help="field MFMA path: split-fp16 (3 products, fp32 accumulate) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -176,6 +179,7 @@ def main():
     avr.load_library()
 
     net = build_scene(device)
+    net.field_precision = args.precision
     fused = net.fused()
     timer = FieldTimer()
     timer.wrap(fused)
@@ -230,6 +234,13 @@ def main():
     fps = field_flops_per_sample()
     field_launches = len(timer.events)
     achieved_tflops = timer.samples * fps / (field_ms * 1e-3) / 1e12
+    if args.precision == "x3":
+        # each fp32-equivalent MAC is 3 fp16 MFMA MACs: the attainable fp32-equivalent peak is fp16 / 3
+        peak, kname = FP16_MFMA_PEAK_TFLOPS / 3.0, ("field_x3_kernel<8> (fused PE + latent lookup + ResnetFC on "
+                                                    "split-fp16 v_mfma_f32_16x16x32_f16 x3, fp32 accumulate)")
+    else:
+        peak, kname = FP32_MFMA_PEAK_TFLOPS, ("field_fwd_kernel<32> (fused PE + latent lookup + ResnetFC on "
+                                              "v_mfma_f32_16x16x4_f32)")
     line = {
         "metric": "rays/sec (128 coarse + 64 fine samples) + achieved HBM GB/s vs roofline",
         "value": round(value, 1),
@@ -241,7 +252,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32" if args.precision == "fp32" else "fp32 (field products as 3 fp16 MFMA terms)",
         "data": "synthetic rays (x_pix ~ U[0,1)^2, orbit pose), random-init default.conf field, random 512x64x64 "
                 "latent",
         "config": {"workload": f"BASELINE config 3: {R} rays/GPU x ({args.n_coarse} coarse + {args.n_fine} fine, "
@@ -249,12 +260,13 @@ def main():
                    "rays_per_gpu": R, "n_coarse": args.n_coarse, "n_fine": args.n_fine,
                    "field_samples_per_ray": samples_per_ray, "parallelism": f"ray-shard x{world} + RCCL gather"},
         "roofline": {
-            "kernel": "field_fwd_kernel<32> (fused PE + latent lookup + ResnetFC on v_mfma_f32_16x16x4_f32)",
+            "kernel": kname,
             "bound": "mfma",
             "achieved": round(achieved_tflops, 2),
-            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "peak": round(peak, 1),
             "unit": "TFLOP/s",
-            "frac": round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+            "frac": round(achieved_tflops / peak, 4),
+            "precision": args.precision,
             "traffic": None,
             "flops_per_sample": fps,
             "reference_flops_per_sample": reference_flops_per_sample(),

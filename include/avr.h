@@ -118,7 +118,12 @@ typedef struct {
   int n_lin_z;     /* min(combine_layer, n_blocks)                        */
   int num_freqs;   /* positional-encoding frequencies                     */
   float freq_factor;
+  int precision;   /* AVR_FIELD_FP32: v_mfma_f32_16x16x4_f32;
+                      AVR_FIELD_X3: split-fp16 v_mfma_f32_16x16x32_f16 (3 products, fp32 accumulate) */
 } avr_field_dims;
+
+#define AVR_FIELD_FP32 0
+#define AVR_FIELD_X3 1
 
 /* One ResnetFC's nn.Linear tensors, PyTorch layout (out, in) row-major. */
 typedef struct {

@@ -17,7 +17,7 @@ def model_conf(d_hidden, n_blocks, combine_layer, d_latent):
                  "encoder": {"backbone": "resnet34", "pretrained": False, "num_layers": num_layers}})
 
 
-def build_net(g, device):
+def build_net(g, device, precision="x3"):
     """avr.models.NewPixelNeRFNet carrying the fixture's weights and source view."""
     from avr.models import NewPixelNeRFNet
     pc, pf, latent = synth.field_from_meta(g)
@@ -36,6 +36,7 @@ def build_net(g, device):
     net.c = torch.from_numpy(g["c"]).to(device)
     net.image_shape = torch.from_numpy(g["image_shape"]).to(device)
     net.num_views_per_obj = 1
+    net.field_precision = precision
     for p in net.parameters():
         p.requires_grad_(False)
     return net

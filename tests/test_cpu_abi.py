@@ -50,8 +50,11 @@ def test_invalid_arguments_return_codes():
     assert lib.avr_field_packed_floats(ctypes.byref(dims), ctypes.byref(n)) == 1001
     dims = _lib.FieldDims(42, 512, 512, 3, 3, 6, 1.5)
     assert lib.avr_field_packed_floats(ctypes.byref(dims), ctypes.byref(n)) == 0
-    # 3 blocks x 2 x 512^2 + lin_in (3 tiles) + lin_out + 3 lin_z x 512^2 (+ biases)
-    assert n.value == 3 * 2 * 512 * 512 + 3 * 16 * 512 + 512 * 16 + 3 * 512 * 512 + 512 * 7 + 16
+    # fp32 fragments: 3 blocks x 2 x 512^2 + lin_in (3 tiles) + lin_out + 3 lin_z x 512^2 (+ biases)
+    fp32 = 3 * 2 * 512 * 512 + 3 * 16 * 512 + 512 * 16 + 3 * 512 * 512 + 512 * 7 + 16
+    # split-fp16 fragments (hi+lo = 4 B per weight): header, lin_in (K 64), 6 x 512^2, lin_out (16 rows)
+    x3 = 64 + 64 * 512 + 6 * 512 * 512 + 16 * 512
+    assert n.value == ((fp32 + 63) // 64) * 64 + x3
 
 
 def test_ops_refuse_host_tensors():

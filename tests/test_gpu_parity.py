@@ -163,10 +163,14 @@ def test_world_rays_and_depth_golden(golden):
 
 
 # ----------------------------------------------------------------- field
+PRECISIONS = ["fp32", "x3"]
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("tag", ["small", "small_mv", "full"])
-def test_field_points_golden(golden, tag):
+def test_field_points_golden(golden, tag, precision):
     g = golden(f"g4_field_{tag}.npz")
-    net = build_net(g, DEV)
+    net = build_net(g, DEV, precision)
     with torch.no_grad():
         assert net.can_fuse(T(g["xyz"]))
         oc = net(T(g["xyz"]), coarse=True, viewdirs=T(g["viewdirs"]))
@@ -175,12 +179,14 @@ def test_field_points_golden(golden, tag):
     np.testing.assert_allclose(to_np(of), g["out_fine"], atol=5e-5, rtol=1e-4)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("tag", ["small", "small_mv", "full"])
-def test_field_fused_matches_torch_path(golden, tag):
+def test_field_fused_matches_torch_path(golden, tag, precision):
     """The fused kernel and the module's PyTorch graph (same device, same
-    weights) agree: the lin_z-per-texel factorisation changes rounding only."""
+    weights) agree: the lin_z-per-texel factorisation and (x3) the split-fp16
+    products change rounding only."""
     g = golden(f"g4_field_{tag}.npz")
-    net = build_net(g, DEV)
+    net = build_net(g, DEV, precision)
     xyz = torch.rand(1, 5000, 3, device=DEV) - 0.5
     vd = torch.nn.functional.normalize(torch.randn(1, 5000, 3, device=DEV), dim=-1)
     with torch.no_grad():
@@ -189,9 +195,10 @@ def test_field_fused_matches_torch_path(golden, tag):
     np.testing.assert_allclose(to_np(a), to_np(b), atol=5e-5, rtol=1e-4)
 
 
-def test_field_rays_mode_matches_points_mode(golden):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_field_rays_mode_matches_points_mode(golden, precision):
     g = golden("g4_field_full.npz")
-    net = build_net(g, DEV)
+    net = build_net(g, DEV, precision)
     R, N = 300, 17
     ro = torch.tensor([[0.3, -1.1, 0.5]], device=DEV).expand(R, 3).contiguous()
     rd = torch.nn.functional.normalize(-ro + 0.2 * torch.randn(R, 3, device=DEV), dim=-1)
@@ -204,14 +211,15 @@ def test_field_rays_mode_matches_points_mode(golden):
 
 
 # ----------------------------------------------------------------- end to end
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("tag", ["c64f32d16", "c128f64d0"])
-def test_volume_renderer_golden(golden, tag):
+def test_volume_renderer_golden(golden, tag, precision):
     """Full VolumeRenderer.forward with the reference's captured noise; staged
     expectations: coarse rgb tight, fine rgb / depth <= 1e-4 on >= 99.9% of rays
     (a fine-bin flip from a ULP-level weight change is the only allowed outlier)."""
     from avr.renderers import VolumeRenderer
     g = golden(f"g5_forward_{tag}.npz")
-    net = build_net(g, DEV)
+    net = build_net(g, DEV, precision)
     R = g["x_pix"].shape[1]
     rend = VolumeRenderer(float(g["near"]), float(g["far"]), int(g["Nc"]), int(g["Nf"]), int(g["Nd"]),
                           float(g["depth_std"]), True)
@@ -226,7 +234,8 @@ def test_volume_renderer_golden(golden, tag):
     assert ok.mean() >= 0.999 or (~ok).sum() <= 1, (~ok).sum()
 
 
-def test_volume_renderer_c3_shape_properties(golden):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_volume_renderer_c3_shape_properties(golden, precision):
     """BASELINE config 3 size (65536 rays, 128 + 64, Nd = 0) with Philox noise:
     finite outputs, rgb in [0, 1] (white background), depth within the
     near/far shell, and the first 128 rays equal the oracle fed the same
@@ -234,7 +243,7 @@ def test_volume_renderer_c3_shape_properties(golden):
     from avr import ops
     from avr.renderers import VolumeRenderer
     g = golden("g4_field_full.npz")
-    net = build_net(g, DEV)
+    net = build_net(g, DEV, precision)
     R = 65536
     rend = VolumeRenderer(0.8, 1.8, 128, 64, 0, 0.01, True)
     rend.seed = 1234
@@ -322,3 +331,21 @@ def test_errors_are_loud():
         ops.composite_fwd(torch.zeros(4, 8), torch.zeros(4, 8, 4))  # host tensors: no CPU path
     with pytest.raises(_lib.AVRError):
         ops.sample_fine(torch.zeros(2, 300, device=DEV), torch.zeros(2, 300, device=DEV), 0.8, 1.8, 8, 0, 0.0)
+
+
+def test_field_x3_tracks_fp32_at_scale(golden):
+    """Split-fp16 field vs fp32 field on 200k random samples of the 512-wide net:
+    the difference stays at fp32-accumulation level."""
+    g = golden("g4_field_full.npz")
+    net = build_net(g, DEV, "fp32")
+    R, N = 2000, 100
+    ro = torch.tensor([[0.4, -1.0, 0.6]], device=DEV).expand(R, 3).contiguous()
+    rd = torch.nn.functional.normalize(-ro + 0.3 * torch.randn(R, 3, device=DEV), dim=-1)
+    z = torch.sort(0.8 + torch.rand(R, N, device=DEV), -1)[0]
+    with torch.no_grad():
+        a = net.fused().forward_rays(ro, rd, z, coarse=True)
+        net.field_precision = "x3"
+        b = net.fused().forward_rays(ro, rd, z, coarse=True)
+    d = (a - b).abs()
+    assert float(d[:, :3].max()) < 2e-5, float(d[:, :3].max())
+    assert float((d[:, 3] / a[:, 3].abs().clamp_min(1.0)).max()) < 1e-4
