@@ -391,6 +391,11 @@ static int dispatch_field(const avr_field_dims* dims, const FieldArgs& a, hipStr
 
 using namespace avr;
 
+#ifdef AVR_STAMPS
+static unsigned long long* g_stamps = nullptr;
+extern "C" void avr_debug_set_stamps(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
+#endif
+
 extern "C" int avr_field_packed_floats(const avr_field_dims* dims, int64_t* n_floats) {
   Layout L;
   const int rc = make_layout(dims, &L);
@@ -462,6 +467,9 @@ extern "C" int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_des
   AVR_REQUIRE(n_rays >= 0 && n_samples > 0, "avr_field_fwd_rays: bad sizes");
   AVR_REQUIRE(n_rays == 0 || (ro && rd && z && out), "avr_field_fwd_rays: null pointer");
   a.ro = ro; a.rd = rd; a.z = z; a.n_samples = n_samples;
+#ifdef AVR_STAMPS
+  a.stamps = g_stamps;
+#endif
   a.M = n_rays * n_samples;
   a.out = reinterpret_cast<float4*>(out);
   if (a.M == 0) return AVR_OK;

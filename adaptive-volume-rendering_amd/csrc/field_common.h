@@ -49,7 +49,21 @@ struct FieldArgs {
   const float* xyz; const float* vd;
   int64_t M;
   float4* out;
+  unsigned long long* stamps;  // diagnostic builds (-DAVR_STAMPS) only: per-block phase clocks
 };
+
+#ifdef AVR_STAMPS
+#define AVR_STAMP(k)                                                                          \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    unsigned long long _t;                                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");              \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 32 + (k)] = _t;         \
+  } while (0)
+#else
+#define AVR_STAMP(k) do { } while (0)
+#endif
 
 struct Bilinear {
   int tex[4];   // texel index of the 4 corners

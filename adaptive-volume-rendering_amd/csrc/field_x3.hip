@@ -278,6 +278,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
   const uint4* P16 = reinterpret_cast<const uint4*>(a.packed);  // 16-B units
   const int zoff = 16 * FT * wid + 4 * g;         // this lane's feature offset inside a table row
 
+  AVR_STAMP(0);
   // ---- prologue: wave w prepares samples 16w + j (lanes g share the geometry);
   // lane g computes z_feature 16g .. 16g+15 of that sample (K = 64 padded input)
   floatx4 f[4];
@@ -299,6 +300,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
       }
     mx = wave_max(mx);
   }
+  AVR_STAMP(1);
   float s_x;
   {
     if (lane == 0) red[wid] = mx;
@@ -317,6 +319,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
     __syncthreads();
   }
 
+  AVR_STAMP(2);
   floatx4 h[FT][4], t[FT][4], v[FT][4];
 
   // ---- lin_in: h = (b_in + bz0 + interp(Z0)) * S + W_in . X ; h stays scaled by S_h
@@ -329,21 +332,26 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
       for (int sg = 0; sg < 4; ++sg) h[ft][sg] = b * S_h;
     }
     if (a.n_lin_z > 0) add_interp<FT>(h, a.table + zoff, bil_tex, bil_w, S_h, j);
+    AVR_STAMP(3);
     gemm_x3<FT>(h, P16 + L.x3_in / 4 + 2 * 64 * FT * wid, kX3InChunks, 64 * NTT, X16, lane);
+    AVR_STAMP(4);
   }
 
   for (int b = 0; b < a.n_blocks; ++b) {
     // fc_0 input relu(h)
     mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
     s_x = publish<FT>(X16, v, mx, red, wid, lane, g, j);
+    AVR_STAMP(5 + 5 * (b & 3));
     // fc_0 (from zero)
     const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
     const float* Zw = (b + 1 < a.n_lin_z) ? a.table + (b + 1) * a.table_stride + zoff : nullptr;
     gemm_x3_fc0<FT>(t, h, P16 + L.x3_fc0[b] / 4 + 2 * 64 * FT * wid, 64 * NTT, X16, lane, nullptr, bil_tex, bil_w,
                     S_h);
+    AVR_STAMP(6 + 5 * (b & 3));
     // fc_1 input relu(t + b0)
     mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
     s_x = publish<FT>(X16, v, mx, red, wid, lane, g, j);
+    AVR_STAMP(7 + 5 * (b & 3));
     // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1 + bz[b+1])
     const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
     const float r = S1 / S_h;
@@ -355,7 +363,9 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
     }
     if (Zw) add_interp<FT>(h, Zw, bil_tex, bil_w, S1, j);
     S_h = S1;
+    AVR_STAMP(8 + 5 * (b & 3));
     gemm_x3<FT>(h, P16 + L.x3_fc1[b] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
+    AVR_STAMP(9 + 5 * (b & 3));
   }
 
   // ---- lin_out(relu(h)): wave w computes the 16-row output tile for samples 16w + j.
@@ -367,6 +377,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
   }
   mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
   s_x = publish<FT>(X16, v, mx, red, wid, lane, g, j);
+  AVR_STAMP(25);
   const float S = layer_scale(a.packed, L, 1) * s_x;
   floatx4 o = *reinterpret_cast<const floatx4*>(a.packed + L.b_out + 4 * g) * S;
   {
@@ -381,6 +392,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
     }
   }
   o *= 1.0f / S;
+  AVR_STAMP(26);
   const int64_t m = base + 16 * wid + j;
   if (g == 0 && m < a.M) a.out[m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
 }

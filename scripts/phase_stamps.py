@@ -1,0 +1,54 @@
+"""Diagnostic: per-phase clock breakdown of field_x3_kernel (wave 0 of every
+workgroup) from the -DAVR_STAMPS build. Not part of the product or the bench."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "adaptive-volume-rendering_amd"))
+sys.path.insert(0, REPO)
+import avr._lib as L  # noqa: E402
+
+L.LIB_PATH = os.path.join(REPO, "adaptive-volume-rendering_amd", "build", "libavr_hip_stamps.so")
+lib = L.load(L.LIB_PATH)
+lib.avr_debug_set_stamps.argtypes = [ctypes.c_void_p]
+import bench  # noqa: E402
+
+dev = torch.device("cuda:0")
+net = bench.build_scene(dev)
+net.field_precision = os.environ.get("PREC", "x3")
+f = net.fused()
+R, N = 65536, 192
+ro = torch.tensor([[0.3, -1.1, 0.5]], device=dev).expand(R, 3).contiguous()
+rd = torch.nn.functional.normalize(-ro + 0.3 * torch.randn(R, 3, device=dev), dim=-1)
+z = torch.sort(0.8 + torch.rand(R, N, device=dev), -1)[0]
+blocks = (R * N + 63) // 64
+stamps = torch.zeros(blocks * 32, dtype=torch.int64, device=dev)
+with torch.no_grad():
+    f.forward_rays(ro, rd, z, False)
+    torch.cuda.synchronize()
+    lib.avr_debug_set_stamps(ctypes.c_void_p(stamps.data_ptr()))
+    t0 = torch.cuda.Event(enable_timing=True); t1 = torch.cuda.Event(enable_timing=True)
+    t0.record(); f.forward_rays(ro, rd, z, False); t1.record()
+    torch.cuda.synchronize()
+    lib.avr_debug_set_stamps(None)
+st = stamps.view(blocks, 32).cpu().numpy().astype(np.int64)
+names = {0: "start", 1: "prologue(geom+PE)", 2: "publish X0", 3: "lin_in init+gather", 4: "lin_in gemm"}
+for b in range(4):
+    names.update({5 + 5 * b: f"b{b} prep+publish h", 6 + 5 * b: f"b{b} fc0 gemm", 7 + 5 * b: f"b{b} prep+publish t",
+                  8 + 5 * b: f"b{b} fc1 init+gather", 9 + 5 * b: f"b{b} fc1 gemm"})
+names.update({25: "lin_out prep+publish", 26: "lin_out gemm"})
+used = [k for k in sorted(names) if (st[:, k] != 0).mean() > 0.99]
+print(f"kernel {t0.elapsed_time(t1):.2f} ms for {R * N} samples, {blocks} blocks")
+tot = np.median(st[:, used[-1]] - st[:, 0])
+prev = used[0]
+for k in used[1:]:
+    d = np.median(st[:, k] - st[:, prev])
+    print(f"{names[k]:28s} {d:10.0f} cyc  {100 * d / tot:5.1f} %")
+    prev = k
+print(f"{'total (median per block)':28s} {tot:10.0f} cyc")
+span = (st[:, used[-1]].max() - st[:, 0].min())
+print("blocks per CU (approx)", blocks / 256, "span cycles", span)
