@@ -15,6 +15,7 @@ constexpr int kSPW = 16;         // fp32 path: samples per wave (MFMA column cou
 constexpr int kInTiles = 3;      // fp32 path: lin_in K = 42 features padded to 48
 constexpr int kX3Samples = 64;   // x3 path: samples per workgroup (4 MFMA column groups)
 constexpr int kX3InChunks = 2;   // x3 path: lin_in K padded to 64 = 2 chunks of 32
+constexpr int kPeSlots = 11;     // x3 prologue: PE entries per lane (6 * num_freqs <= 42)
 constexpr int kX3MaxLayers = 2 + 2 * AVR_MAX_BLOCKS;
 
 // Packed blob (floats). fp32 part: [t][ot][lane] float4 fragments for
@@ -146,6 +147,27 @@ __device__ __forceinline__ float z_feature(const SampleGeom& s, int k, int num_f
   }
   if (k < 6 + npe) return pick(s.vr, k - 3 - npe);
   return 0.f;
+}
+
+// sin(a) for the positional encoding, ~1.5 ulp (numpy's float32 sin: ~1.45):
+// Cody-Waite reduction by pi/2 (3-term split, fma) + Cephes minimax
+// polynomials on [-pi/4, pi/4]. About 20 VALU ops instead of the library
+// sinf's generic path; |a| > 8192 falls back to sinf.
+__device__ __forceinline__ float pe_sin(float a) {
+  if (fabsf(a) > 8192.f) return sinf(a);
+  const float j = __builtin_rintf(a * 0.6366197466850281f);
+  float r = __builtin_fmaf(-j, 1.5707963705062866f, a);
+  r = __builtin_fmaf(-j, -4.371138828673793e-08f, r);
+  r = __builtin_fmaf(-j, -1.7151245100058819e-15f, r);
+  const float z = r * r;
+  const float ps = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+  const float S = __builtin_fmaf(r * z, ps, r);
+  const float pc = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                                  4.166664568298827e-2f);
+  const float C = __builtin_fmaf(z * z, pc, __builtin_fmaf(-0.5f, z, 1.0f));
+  const int q = (int)j & 3;
+  const float v = (q & 1) ? C : S;
+  return (q & 2) ? -v : v;
 }
 
 // Power-of-two scale that maps max|x| to [2^13, 2^14] (fp16 split operands).

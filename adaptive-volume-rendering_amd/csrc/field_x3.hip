@@ -57,16 +57,19 @@ __device__ __forceinline__ BPair read_b(const uint4* X16, int c, int sg, int g, 
   return b;
 }
 
-__device__ __forceinline__ void split4(const floatx4& x, uint2& hi, uint2& lo) {
-  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-  half4 h, l;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    h[e] = (_Float16)x[e];
-    l[e] = (_Float16)(x[e] - (float)h[e]);
-  }
-  hi = __builtin_bit_cast(uint2, h);
-  lo = __builtin_bit_cast(uint2, l);
+// hi = fp16(x*s), lo = fp16(x*s - hi): one packed convert per pair for hi and
+// one v_fma_mix{lo,hi}_f16 per value for lo (x*s is exact: s is a power of two)
+__device__ __forceinline__ void split4(const floatx4& x, float s, uint2& hi, uint2& lo) {
+  const floatx4 y = x * s;
+  unsigned h0, h1, l0, l1;
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h0) : "v"(y.x), "v"(y.y));
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h1) : "v"(y.z), "v"(y.w));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l0) : "v"(x.x), "v"(s), "v"(h0));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l0) : "v"(x.y), "v"(s), "v"(h0));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l1) : "v"(x.z), "v"(s), "v"(h1));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l1) : "v"(x.w), "v"(s), "v"(h1));
+  hi = make_uint2(h0, h1);
+  lo = make_uint2(l0, l1);
 }
 
 // One K-chunk on resident A fragments: per sample group, the three products
@@ -91,10 +94,11 @@ __device__ __forceinline__ void chunk_mfma(floatx4 (&acc)[FT][4], const FragX3 (
   }
 }
 
-// acc += W . X over KC chunks (KC even, runtime). W points at this wave's
-// first fragment of chunk 0; consecutive chunks are `cstride` fragments
-// (32 B each) apart. A is double-buffered one chunk ahead in registers.
-template <int FT>
+// acc (+)= W . X over KC chunks (KC even, runtime; ZERO: acc starts from 0).
+// W points at this wave's first fragment of chunk 0; consecutive chunks are
+// `cstride` fragments (32 B each) apart. A is double-buffered one chunk ahead
+// in registers.
+template <int FT, bool ZERO>
 __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], const uint4* __restrict__ W, int KC, int cstride,
                                         const uint4* X16, int lane) {
   const int g = lane >> 4, j = lane & 15;
@@ -109,7 +113,10 @@ __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], const uint4* __re
     for (int ft = 0; ft < FT; ++ft) A1[ft] = load_frag(w1 + 2 * 64 * ft);
     __builtin_amdgcn_sched_barrier(0);
     const int c2 = c + 2 < KC ? c + 2 : c + 1;
-    chunk_mfma<FT, false>(acc, A0, X16, c, c + 1, B, g, j);
+    if (ZERO && c == 0)
+      chunk_mfma<FT, true>(acc, A0, X16, c, c + 1, B, g, j);
+    else
+      chunk_mfma<FT, false>(acc, A0, X16, c, c + 1, B, g, j);
     const uint4* w2 = wl + (int64_t)2 * c2 * cstride;
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft) A0[ft] = load_frag(w2 + 2 * 64 * ft);
@@ -118,80 +125,131 @@ __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], const uint4* __re
   }
 }
 
-// Bilinear lin_z gather for one (feature tile, sample group) pair: 4 corner
-// rows of this lane's 4 features.
-struct Gath {
-  floatx4 v[4];
+// ---- lin_z interpolation through LDS.
+// The 64 samples x 4 bilinear corners of a workgroup touch few distinct
+// texels (samples run along one ray: ~40-60 of 256 at the bench geometry).
+// They are deduplicated once per workgroup (LDS hash table, slots numbered in
+// first-occurrence order), the distinct rows of each lin_z table are copied
+// into LDS by LDS-DMA (global_load_lds_dwordx4, no VGPRs), and every lane
+// blends its 4 features x 4 corners from LDS with ds_read_b128. Rows are
+// padded by 16 B so consecutive slots start in different bank quads. More
+// distinct texels than the stage holds are handled in passes.
+
+// Per-workgroup bookkeeping at the top of the LDS allocation.
+struct ZTail {
+  int tex[256];          // [sample][corner] texel index
+  float w[256];          // [sample][corner] bilinear weight
+  int slot[256];         // [sample][corner] distinct-texel slot
+  unsigned ht_key[512];  // hash table: texel
+  unsigned ht_min[512];  //             first entry holding it
+  int first_slot[256];   // [entry] slot, for first occurrences
+  int uniq[256];         // [slot] texel
+  float red[16];
+  int wtot[4];
 };
+constexpr unsigned kEmpty = 0xffffffffu;
 
-__device__ __forceinline__ Gath issue_gather(const float* __restrict__ Zw, const int* bil_tex, int s) {
-  const int4 tex = *reinterpret_cast<const int4*>(bil_tex + 4 * s);
-  Gath G;
-  G.v[0] = *reinterpret_cast<const floatx4*>(Zw + tex.x);
-  G.v[1] = *reinterpret_cast<const floatx4*>(Zw + tex.y);
-  G.v[2] = *reinterpret_cast<const floatx4*>(Zw + tex.z);
-  G.v[3] = *reinterpret_cast<const floatx4*>(Zw + tex.w);
-  return G;
+// Entry e = threadIdx.x (sample e>>2, corner e&3); tail->tex complete and
+// ht_key/ht_min initialised before the first barrier inside. Returns the
+// number of distinct texels; tail->slot is complete after the last barrier.
+__device__ __forceinline__ int dedup_texels(ZTail* tail, int lane, int wid) {
+  const int e = threadIdx.x;
+  __syncthreads();
+  const unsigned tex = (unsigned)tail->tex[e];
+  unsigned b = (tex * 2654435761u) >> 23;  // 9-bit bucket
+  for (;;) {
+    const unsigned old = atomicCAS(&tail->ht_key[b], kEmpty, tex);
+    if (old == kEmpty || old == tex) break;
+    b = (b + 1) & 511;
+  }
+  atomicMin(&tail->ht_min[b], (unsigned)e);
+  __syncthreads();
+  const int first = (int)tail->ht_min[b];
+  const bool is_first = first == e;
+  const unsigned long long m = __ballot(is_first);
+  const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+  if (lane == 0) tail->wtot[wid] = __popcll(m);
+  __syncthreads();
+  int off = 0;
+#pragma unroll
+  for (int w = 0; w < kFieldWaves; ++w) off += w < wid ? tail->wtot[w] : 0;
+  const int D = tail->wtot[0] + tail->wtot[1] + tail->wtot[2] + tail->wtot[3];
+  if (is_first) {
+    tail->uniq[off + pos] = (int)tex;
+    tail->first_slot[e] = off + pos;
+  }
+  __syncthreads();
+  tail->slot[e] = tail->first_slot[first];
+  return D;
 }
 
-__device__ __forceinline__ floatx4 blend(const Gath& G, const float* bil_w, int s, float scale) {
-  const float4 w = *reinterpret_cast<const float4*>(bil_w + 4 * s);
-  return (((G.v[0] * w.x + G.v[1] * w.y) + G.v[2] * w.z) + G.v[3] * w.w) * scale;
-}
-
-// t = W . X over KC = 2 FT chunks (compile-time, fully unrolled) starting from
-// zero, while the lin_z gather of the next block streams into the residual h:
-// chunk c issues the corner loads of pairs 2c, 2c+1 (feature tile c/2, sample
-// groups 2(c&1), 2(c&1)+1) before its 96 MFMAs and blends them into h after.
-// `Zw` = this lane's feature base of the next lin_z table (null: no gather);
-// `zs` = h's accumulator scale.
+// Copy table rows uniq[lo .. lo+n) (row = HID floats) to stage rows 0 .. n
+// (stride RS bytes) by LDS-DMA; wave w takes pieces w, w+4, ... of 1 KiB.
+// The row indices are read from LDS up front (lane i holds the row of the
+// wave's i-th piece): an LDS read between two LDS-DMA issues would make the
+// compiler wait for the earlier DMA to land.
 template <int FT>
-__device__ __forceinline__ void gemm_x3_fc0(floatx4 (&acc)[FT][4], floatx4 (&h)[FT][4], const uint4* __restrict__ W,
-                                            int cstride, const uint4* X16, int lane, const float* __restrict__ Zw,
-                                            const int* bil_tex, const float* bil_w, float zs) {
-  constexpr int KC = 2 * FT;
-  const int g = lane >> 4, j = lane & 15;
-  const uint4* wl = W + 2 * lane;
-  FragX3 A[2][FT];
-#pragma unroll
-  for (int ft = 0; ft < FT; ++ft) A[0][ft] = load_frag(wl + 2 * 64 * ft);
-  BPair B = read_b(X16, 0, 0, g, j);
-#pragma unroll
-  for (int c = 0; c < KC; ++c) {
-    const int cur = c & 1, nxt = cur ^ 1;
-    const int cn = c + 1 < KC ? c + 1 : c;
-    const int ftp = c >> 1, sg0 = 2 * (c & 1);
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft) A[nxt][ft] = load_frag(wl + (int64_t)2 * cn * cstride + 2 * 64 * ft);
-    Gath G0, G1;
-    if (Zw) {
-      G0 = issue_gather(Zw + 16 * ftp, bil_tex, 16 * sg0 + j);
-      G1 = issue_gather(Zw + 16 * ftp, bil_tex, 16 * (sg0 + 1) + j);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (c == 0)
-      chunk_mfma<FT, true>(acc, A[cur], X16, c, cn, B, g, j);
-    else
-      chunk_mfma<FT, false>(acc, A[cur], X16, c, cn, B, g, j);
-    if (Zw) {
-      h[ftp][sg0] += blend(G0, bil_w, 16 * sg0 + j, zs);
-      h[ftp][sg0 + 1] += blend(G1, bil_w, 16 * (sg0 + 1) + j, zs);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+__device__ __forceinline__ void stage_rows(char* stage, const float* __restrict__ table, const ZTail* tail, int lo,
+                                           int n, int RS, int lane, int wid) {
+  constexpr int HID = 64 * FT;
+  constexpr int ROWB = 4 * HID;                                  // bytes per row
+  constexpr int PPR = ROWB >= 1024 ? ROWB / 1024 : 1;            // pieces per row
+  constexpr int LANES = ROWB >= 1024 ? 64 : ROWB / 16;           // active lanes per piece
+  const int npc = n * PPR;
+  const int mine = (npc - wid + kFieldWaves - 1) / kFieldWaves;  // pieces of this wave (<= 64 * PPR)
+  int rowv = 0;
+  {
+    const int pc = wid + kFieldWaves * lane;
+    if (lane < mine) rowv = tail->uniq[lo + pc / PPR];
+  }
+  for (int i = 0; i < mine; ++i) {
+    const int pc = wid + kFieldWaves * i;
+    const int r = pc / PPR, q = pc - r * PPR;
+    const int row = __builtin_amdgcn_readlane(rowv, i);
+    const char* src = reinterpret_cast<const char*>(table + (int64_t)row * HID) + 1024 * q + 16 * lane;
+    auto* dst = (__attribute__((address_space(3))) void*)(stage + r * RS + 1024 * q);
+    if (lane < LANES) __builtin_amdgcn_global_load_lds((const void*)src, dst, 16, 0, 0);
   }
 }
 
-// h += scale * interp(Z) for all of this wave's tiles (blocking, one sample group per batch)
-template <int FT>
-__device__ __forceinline__ void add_interp(floatx4 (&h)[FT][4], const float* __restrict__ Zw, const int* bil_tex,
-                                           const float* bil_w, float scale, int j) {
+typedef __attribute__((address_space(3))) char lds_char;
+
+// h += S * sum_c w_c * row(slot_c) over the corners whose slot is in [lo, lo+n).
+// PREP: also v = relu(h * f) and the running max for the next publish (the
+// fc_0 input of the block), from the same register read of h.
+template <int FT, bool PREP>
+__device__ __forceinline__ void blend_stage(floatx4 (&h)[FT][4], floatx4 (&v)[FT][4], float& mx, const char* stage_g,
+                                            const ZTail* tail, int lo, int n, int RS, float S, float f, int wid, int g,
+                                            int j) {
+  const lds_char* stage = (const lds_char*)stage_g;
+  const unsigned fo = 64u * FT * wid + 16u * g;   // this lane's feature offset in a row
 #pragma unroll
   for (int sg = 0; sg < 4; ++sg) {
-    Gath G[FT];
+    const int s = 16 * sg + j;
+    const int4 sl = *reinterpret_cast<const int4*>(tail->slot + 4 * s);
+    const float4 w = *reinterpret_cast<const float4*>(tail->w + 4 * s);
+    const int sc0 = sl.x - lo, sc1 = sl.y - lo, sc2 = sl.z - lo, sc3 = sl.w - lo;
+    const bool i0 = (unsigned)sc0 < (unsigned)n, i1 = (unsigned)sc1 < (unsigned)n;
+    const bool i2 = (unsigned)sc2 < (unsigned)n, i3 = (unsigned)sc3 < (unsigned)n;
+    const unsigned o0 = (i0 ? sc0 : 0) * RS + fo, o1 = (i1 ? sc1 : 0) * RS + fo;
+    const unsigned o2 = (i2 ? sc2 : 0) * RS + fo, o3 = (i3 ? sc3 : 0) * RS + fo;
+    const float w0 = i0 ? w.x * S : 0.f, w1 = i1 ? w.y * S : 0.f, w2 = i2 ? w.z * S : 0.f, w3 = i3 ? w.w * S : 0.f;
 #pragma unroll
-    for (int ft = 0; ft < FT; ++ft) G[ft] = issue_gather(Zw + 16 * ft, bil_tex, 16 * sg + j);
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft) h[ft][sg] += blend(G[ft], bil_w, 16 * sg + j, scale);
+    for (int ft = 0; ft < FT; ++ft) {
+      const floatx4 v0 = *reinterpret_cast<const __attribute__((address_space(3))) floatx4*>(stage + o0 + 64 * ft);
+      const floatx4 v1 = *reinterpret_cast<const __attribute__((address_space(3))) floatx4*>(stage + o1 + 64 * ft);
+      const floatx4 v2 = *reinterpret_cast<const __attribute__((address_space(3))) floatx4*>(stage + o2 + 64 * ft);
+      const floatx4 v3 = *reinterpret_cast<const __attribute__((address_space(3))) floatx4*>(stage + o3 + 64 * ft);
+      const floatx4 hn = h[ft][sg] + (((v0 * w0 + v1 * w1) + v2 * w2) + v3 * w3);
+      h[ft][sg] = hn;
+      if (PREP) {
+        floatx4 x = hn * f;
+        x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
+        v[ft][sg] = x;
+        mx = fmaxf(fmaxf(mx, x.x), fmaxf(fmaxf(x.y, x.z), x.w));
+      }
+      if (ft & 1) __builtin_amdgcn_sched_barrier(0);  // bound the LDS reads in flight (register pressure)
+    }
   }
 }
 
@@ -231,7 +289,7 @@ __device__ __forceinline__ void store_split(uint4* X16, const floatx4 (&v)[FT][4
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) {
       uint2 hi, lo;
-      split4(v[ft][sg] * s_x, hi, lo);
+      split4(v[ft][sg], s_x, hi, lo);
       const int s = 16 * sg + j;
       *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 0, g, s) * 16 + (ftg & 1) * 8) = hi;
       *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 1, g, s) * 16 + (ftg & 1) * 8) = lo;
@@ -260,44 +318,81 @@ __device__ __forceinline__ float publish(uint4* X16, const floatx4 (&v)[FT][4], 
   return s_x;
 }
 
+// LDS plan: X (KCX chunks x 8 KiB) from byte 0; the lin_z stage aliases X
+// (rows of RS bytes from byte 0); ZTail at the top of the allocation.
+template <int FT>
+struct LdsPlan {
+  static constexpr int KC = 2 * FT;
+  static constexpr int KCX = KC > kX3InChunks ? KC : kX3InChunks;
+  static constexpr int XB = KCX * 8192;
+  static constexpr int RS = 256 * FT + 16;
+  static constexpr int TAIL = (int)((sizeof(ZTail) + 15) / 16 * 16);
+  static constexpr int WANT = (XB > 96 * RS ? XB : 96 * RS) + TAIL;
+  static constexpr int BYTES = WANT < 160 * 1024 ? WANT : 160 * 1024;
+  static constexpr int CAP = (BYTES - TAIL) / RS;
+  static_assert(XB + TAIL <= BYTES, "X and tail must fit");
+  static_assert(CAP * (256 * FT >= 1024 ? FT / 4 : 1) <= 4 * 64, "stage_rows: one lane per piece");
+};
+
 template <int FT>
 __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
-  constexpr int KC = 2 * FT;                       // K chunks of a hidden layer (HID / 32)
-  constexpr int KCX = KC > kX3InChunks ? KC : kX3InChunks;
+  using P = LdsPlan<FT>;
+  constexpr int KC = P::KC;
   constexpr int NTT = 4 * FT;                      // feature tiles of a hidden layer
-  constexpr int HID = 64 * FT;
   extern __shared__ float lds[];
   uint4* X16 = reinterpret_cast<uint4*>(lds);      // KCX * 512 slots of 16 B
-  int* bil_tex = reinterpret_cast<int*>(lds + KCX * 2048);   // [64][4] element offsets into a table
-  float* bil_w = reinterpret_cast<float*>(bil_tex + 256);    // [64][4]
-  float* red = bil_w + 256;
+  char* stage = reinterpret_cast<char*>(lds);
+  ZTail* tail = reinterpret_cast<ZTail*>(reinterpret_cast<char*>(lds) + (P::BYTES - P::TAIL));
+  float* red = tail->red;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, j = lane & 15;
   const int64_t base = (int64_t)blockIdx.x * kX3Samples;
   const Layout& L = a.L;
   const uint4* P16 = reinterpret_cast<const uint4*>(a.packed);  // 16-B units
-  const int zoff = 16 * FT * wid + 4 * g;         // this lane's feature offset inside a table row
 
   AVR_STAMP(0);
-  // ---- prologue: wave w prepares samples 16w + j (lanes g share the geometry);
-  // lane g computes z_feature 16g .. 16g+15 of that sample (K = 64 padded input)
-  floatx4 f[4];
-  float mx = 0.f;
+  // ---- prologue: wave w prepares samples 16w + j (lanes g share the geometry).
+  // The 6 * num_freqs sines of a sample are spread over its 4 lanes (lane g:
+  // PE entries g, g + 4, ...; lanes 0-2 also own xyz_rot[g] / R viewdir[g]),
+  // then each value is written as fp16 hi/lo into its B-fragment slot; the
+  // padding features d_in .. 63 stay zero.
+  {
+    uint4* xz = X16 + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 2 * kX3InChunks; ++i) xz[256 * i] = make_uint4(0u, 0u, 0u, 0u);
+    tail->ht_key[threadIdx.x] = kEmpty; tail->ht_key[threadIdx.x + 256] = kEmpty;
+    tail->ht_min[threadIdx.x] = kEmpty; tail->ht_min[threadIdx.x + 256] = kEmpty;
+  }
+  const int npe = 6 * a.num_freqs;
+  float xr[3], vr[3];
   {
     const int s = 16 * wid + j;
     const int64_t m = base + s;
     const SampleGeom geo = sample_geom(a, m < a.M ? m : a.M - 1);
     if (g == 0) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) { bil_tex[4 * s + c] = geo.bl.tex[c] * HID; bil_w[4 * s + c] = geo.bl.w[c]; }
+      *reinterpret_cast<int4*>(tail->tex + 4 * s) = make_int4(geo.bl.tex[0], geo.bl.tex[1], geo.bl.tex[2], geo.bl.tex[3]);
+      *reinterpret_cast<float4*>(tail->w + 4 * s) = make_float4(geo.bl.w[0], geo.bl.w[1], geo.bl.w[2], geo.bl.w[3]);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int d = 0; d < 3; ++d) { xr[d] = geo.xr[d]; vr[d] = geo.vr[d]; }
+  }
+  AVR_STAMP(27);
+  const int D = a.n_lin_z > 0 ? dedup_texels(tail, lane, wid) : 0;
+  AVR_STAMP(28);
+  float pe[kPeSlots], xo = 0.f, vo = 0.f;
+  float mx = 0.f;
+  {
+    const auto pick = [](const float* v, int i) { return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]); };
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        f[q][e] = z_feature(geo, 16 * g + 4 * q + e, a.num_freqs, a.freq_factor);
-        mx = fmaxf(mx, fabsf(f[q][e]));
-      }
+    for (int i = 0; i < kPeSlots; ++i) {
+      const int q = g + 4 * i, jj = q / 3, dd = q - 3 * jj;
+      const float freq = fmul(a.freq_factor, (float)(1 << (jj >> 1)));
+      const float phase = (jj & 1) ? 1.5707963705062866f : 0.f;  // fp32(pi/2)
+      pe[i] = q < npe ? pe_sin(fadd(phase, fmul(pick(xr, dd), freq))) : 0.f;
+      mx = fmaxf(mx, fabsf(pe[i]));
+    }
+    if (g < 3) { xo = pick(xr, g); vo = pick(vr, g); }
+    mx = fmaxf(mx, fmaxf(fabsf(xo), fabsf(vo)));
     mx = wave_max(mx);
   }
   AVR_STAMP(1);
@@ -306,53 +401,75 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
     if (lane == 0) red[wid] = mx;
     __syncthreads();
     s_x = pow2_scale_for(red_max(red));
-    // feature 16g + 4q + e: chunk g>>1, tile parity g&1, lane group q
-    char* xb = reinterpret_cast<char*>(X16);
     const int s = 16 * wid + j;
+    char* xb = reinterpret_cast<char*>(X16);
+    // feature k -> chunk k>>5, lane group (k>>2)&3, element 4*((k>>4)&1) + (k&3)
+    const auto put = [&](int k, float val) {
+      const int c = k >> 5, gg = (k >> 2) & 3, e = 4 * ((k >> 4) & 1) + (k & 3);
+      const float y = val * s_x;
+      const _Float16 hi = (_Float16)y;
+      *reinterpret_cast<_Float16*>(xb + xidx(c, 0, gg, s) * 16 + 2 * e) = hi;
+      *reinterpret_cast<_Float16*>(xb + xidx(c, 1, gg, s) * 16 + 2 * e) = (_Float16)(y - (float)hi);
+    };
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint2 hi, lo;
-      split4(f[q] * s_x, hi, lo);
-      *reinterpret_cast<uint2*>(xb + xidx(g >> 1, 0, q, s) * 16 + (g & 1) * 8) = hi;
-      *reinterpret_cast<uint2*>(xb + xidx(g >> 1, 1, q, s) * 16 + (g & 1) * 8) = lo;
-    }
+    for (int i = 0; i < kPeSlots; ++i)
+      if (g + 4 * i < npe) put(3 + g + 4 * i, pe[i]);
+    if (g < 3) { put(g, xo); put(3 + npe + g, vo); }
     __syncthreads();
   }
 
   AVR_STAMP(2);
   floatx4 h[FT][4], t[FT][4], v[FT][4];
 
-  // ---- lin_in: h = (b_in + bz0 + interp(Z0)) * S + W_in . X ; h stays scaled by S_h
+  // ---- lin_in: h = (b_in + W_in . X) * S_h ; h stays scaled by S_h
   float S_h = layer_scale(a.packed, L, 0) * s_x;
-  {
 #pragma unroll
-    for (int ft = 0; ft < FT; ++ft) {
-      const floatx4 b = *reinterpret_cast<const floatx4*>(a.packed + L.b_in + 16 * (FT * wid + ft) + 4 * g);
+  for (int ft = 0; ft < FT; ++ft) {
+    const floatx4 b = *reinterpret_cast<const floatx4*>(a.packed + L.b_in + 16 * (FT * wid + ft) + 4 * g);
 #pragma unroll
-      for (int sg = 0; sg < 4; ++sg) h[ft][sg] = b * S_h;
-    }
-    if (a.n_lin_z > 0) add_interp<FT>(h, a.table + zoff, bil_tex, bil_w, S_h, j);
-    AVR_STAMP(3);
-    gemm_x3<FT>(h, P16 + L.x3_in / 4 + 2 * 64 * FT * wid, kX3InChunks, 64 * NTT, X16, lane);
-    AVR_STAMP(4);
+    for (int sg = 0; sg < 4; ++sg) h[ft][sg] = b * S_h;
   }
+  AVR_STAMP(3);
+  gemm_x3<FT, false>(h, P16 + L.x3_in / 4 + 2 * 64 * FT * wid, kX3InChunks, 64 * NTT, X16, lane);
+  AVR_STAMP(4);
 
   for (int b = 0; b < a.n_blocks; ++b) {
-    // fc_0 input relu(h)
-    mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
-    s_x = publish<FT>(X16, v, mx, red, wid, lane, g, j);
+    // + lin_z[b](interp latent) (models.py ResnetFC: x = x + lin_z[b](z) before block b)
+    // (fused with the fc_0 input prep: v = relu(h), mx)
+    if (b < a.n_lin_z) __syncthreads();  // every wave is done reading X (the stage aliases it)
+    const float* table = a.table + b * a.table_stride;
+    if (b < a.n_lin_z && D <= P::CAP) {
+      stage_rows<FT>(stage, table, tail, 0, D, P::RS, lane, wid);
+      AVR_STAMP(29);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      AVR_STAMP(30);
+      mx = 0.f;
+      blend_stage<FT, true>(h, v, mx, stage, tail, 0, D, P::RS, S_h, 1.0f / S_h, wid, g, j);
+      mx = wave_max(mx);
+    } else {
+      for (int lo = 0; b < a.n_lin_z && lo < D; lo += P::CAP) {   // more distinct texels than the stage holds
+        const int n = D - lo < P::CAP ? D - lo : P::CAP;
+        if (lo > 0) __syncthreads();
+        stage_rows<FT>(stage, table, tail, lo, n, P::RS, lane, wid);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        blend_stage<FT, false>(h, v, mx, stage, tail, lo, n, P::RS, S_h, 1.0f / S_h, wid, g, j);
+      }
+      mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
+    }
     AVR_STAMP(5 + 5 * (b & 3));
+    s_x = publish<FT>(X16, v, mx, red, wid, lane, g, j);
+    AVR_STAMP(6 + 5 * (b & 3));
     // fc_0 (from zero)
     const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
-    const float* Zw = (b + 1 < a.n_lin_z) ? a.table + (b + 1) * a.table_stride + zoff : nullptr;
-    gemm_x3_fc0<FT>(t, h, P16 + L.x3_fc0[b] / 4 + 2 * 64 * FT * wid, 64 * NTT, X16, lane, nullptr, bil_tex, bil_w,
-                    S_h);
-    AVR_STAMP(6 + 5 * (b & 3));
+    gemm_x3<FT, true>(t, P16 + L.x3_fc0[b] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
+    AVR_STAMP(7 + 5 * (b & 3));
     // fc_1 input relu(t + b0)
     mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
     s_x = publish<FT>(X16, v, mx, red, wid, lane, g, j);
-    AVR_STAMP(7 + 5 * (b & 3));
-    // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1 + bz[b+1])
+    AVR_STAMP(8 + 5 * (b & 3));
+    // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
     const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
     const float r = S1 / S_h;
 #pragma unroll
@@ -361,10 +478,8 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
 #pragma unroll
       for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb * S1;
     }
-    if (Zw) add_interp<FT>(h, Zw, bil_tex, bil_w, S1, j);
     S_h = S1;
-    AVR_STAMP(8 + 5 * (b & 3));
-    gemm_x3<FT>(h, P16 + L.x3_fc1[b] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
+    gemm_x3<FT, false>(h, P16 + L.x3_fc1[b] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
     AVR_STAMP(9 + 5 * (b & 3));
   }
 
@@ -399,9 +514,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
 
 template <int FT>
 static int launch_x3(const FieldArgs& a, hipStream_t s) {
-  constexpr int KC = 2 * FT;
-  constexpr int KCX = KC > kX3InChunks ? KC : kX3InChunks;
-  const size_t shm = (size_t)KCX * 2048 * sizeof(float) + 512 * sizeof(float) + 64;  // X + bilinear + red
+  const size_t shm = LdsPlan<FT>::BYTES;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT>),

@@ -36,12 +36,14 @@ with torch.no_grad():
     torch.cuda.synchronize()
     lib.avr_debug_set_stamps(None)
 st = stamps.view(blocks, 32).cpu().numpy().astype(np.int64)
-names = {0: "start", 1: "prologue(geom+PE)", 2: "publish X0", 3: "lin_in init+gather", 4: "lin_in gemm"}
+names = {0: "start", 27: "sample_geom", 28: "dedup texels", 1: "PE sines", 2: "publish X0", 3: "lin_in init",
+         4: "lin_in gemm"}
 for b in range(4):
-    names.update({5 + 5 * b: f"b{b} prep+publish h", 6 + 5 * b: f"b{b} fc0 gemm", 7 + 5 * b: f"b{b} prep+publish t",
-                  8 + 5 * b: f"b{b} fc1 init+gather", 9 + 5 * b: f"b{b} fc1 gemm"})
-names.update({25: "lin_out prep+publish", 26: "lin_out gemm"})
-used = [k for k in sorted(names) if (st[:, k] != 0).mean() > 0.99]
+    names.update({5 + 5 * b: f"b{b} lin_z interp", 6 + 5 * b: f"b{b} prep+publish h", 7 + 5 * b: f"b{b} fc0 gemm",
+                  8 + 5 * b: f"b{b} prep+publish t", 9 + 5 * b: f"b{b} fc1 init+gemm"})
+names.update({25: "lin_out prep+publish", 26: "lin_out gemm", 29: "b2 stage issue", 30: "b2 stage wait"})
+used = [k for k in names if (st[:, k] != 0).mean() > 0.99]
+used.sort(key=lambda k: np.median(st[:, k] - st[:, 0]))
 print(f"kernel {t0.elapsed_time(t1):.2f} ms for {R * N} samples, {blocks} blocks")
 tot = np.median(st[:, used[-1]] - st[:, 0])
 prev = used[0]
