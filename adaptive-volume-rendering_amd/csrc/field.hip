@@ -394,6 +394,8 @@ using namespace avr;
 #ifdef AVR_STAMPS
 static unsigned long long* g_stamps = nullptr;
 extern "C" void avr_debug_set_stamps(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
+static int g_debug = 0;
+extern "C" void avr_debug_set_flags(int f) { g_debug = f; }
 #endif
 
 extern "C" int avr_field_packed_floats(const avr_field_dims* dims, int64_t* n_floats) {
@@ -469,6 +471,7 @@ extern "C" int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_des
   a.ro = ro; a.rd = rd; a.z = z; a.n_samples = n_samples;
 #ifdef AVR_STAMPS
   a.stamps = g_stamps;
+  a.debug = g_debug;
 #endif
   a.M = n_rays * n_samples;
   a.out = reinterpret_cast<float4*>(out);

@@ -51,6 +51,7 @@ struct FieldArgs {
   int64_t M;
   float4* out;
   unsigned long long* stamps;  // diagnostic builds (-DAVR_STAMPS) only: per-block phase clocks
+  int debug;                   // diagnostic builds only: experiment flags (1: every fc layer uses block 0's weights)
 };
 
 #ifdef AVR_STAMPS

@@ -72,56 +72,72 @@ __device__ __forceinline__ void split4(const floatx4& x, float s, uint2& hi, uin
   lo = make_uint2(l0, l1);
 }
 
-// One K-chunk on resident A fragments: per sample group, the three products
-// into each feature tile (one accumulation chain of v_mfma_f32_16x16x32_f16
-// issues back to back at full rate, MI355X_MICROARCH.md). The B fragment of
-// the next (chunk, sample group) is read from LDS one group ahead.
+// One K-chunk on resident fragments A (this wave's FT tiles) and B (the 4
+// sample groups), in feature-tile pairs: pair p issues its 3 x 2 x 4 chained
+// v_mfma_f32_16x16x32_f16 (each accumulation chain issues back to back at full
+// rate, MI355X_MICROARCH.md) and the global loads of pair p of the NEXT chunk
+// into An, one load per few MFMAs (sched_group_barrier), so every A load has a
+// whole chunk of MFMAs to land in and its issue hides in the MFMA gaps. In the
+// last pair each B[sg] is refilled with the next chunk's fragment as soon as
+// its MFMAs have issued.
 template <int FT, bool ZERO>
-__device__ __forceinline__ void chunk_mfma(floatx4 (&acc)[FT][4], const FragX3 (&A)[FT], const uint4* X16, int c,
-                                           int cn, BPair& B, int g, int j) {
+__device__ __forceinline__ void chunk_step(floatx4 (&acc)[FT][4], const FragX3 (&A)[FT], FragX3 (&An)[FT],
+                                           const uint4* wn, BPair (&B)[4], const uint4* X16, int cn, int g, int j) {
+  constexpr int GS = FT >= 2 ? 2 : 1;       // tiles per group
+  constexpr int NG = FT / GS;
+  constexpr int NMF = 3 * GS * 4;           // MFMAs per group
+  constexpr int NLD = 2 * GS;               // global loads per group
+  constexpr int PER = NMF / (NLD + 1);
 #pragma unroll
-  for (int sg = 0; sg < 4; ++sg) {
-    const BPair Bn = read_b(X16, sg < 3 ? c : cn, (sg + 1) & 3, g, j);
-    __builtin_amdgcn_sched_barrier(0);
+  for (int p = 0; p < NG; ++p) {
 #pragma unroll
-    for (int ft = 0; ft < FT; ++ft) {
-      acc[ft][sg] = mfma32h(A[ft].hi, B.hi, ZERO ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[ft][sg]);
-      acc[ft][sg] = mfma32h(A[ft].hi, B.lo, acc[ft][sg]);
-      acc[ft][sg] = mfma32h(A[ft].lo, B.hi, acc[ft][sg]);
+    for (int q = 0; q < GS; ++q) An[GS * p + q] = load_frag(wn + 2 * 64 * (GS * p + q));
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+#pragma unroll
+      for (int q = 0; q < GS; ++q) {
+        const int ft = GS * p + q;
+        acc[ft][sg] = mfma32h(A[ft].hi, B[sg].hi, ZERO ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[ft][sg]);
+        acc[ft][sg] = mfma32h(A[ft].hi, B[sg].lo, acc[ft][sg]);
+        acc[ft][sg] = mfma32h(A[ft].lo, B[sg].hi, acc[ft][sg]);
+      }
+      if (p == NG - 1) B[sg] = read_b(X16, cn, sg, g, j);
     }
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NLD * PER, 0);
     __builtin_amdgcn_sched_barrier(0);
-    B = Bn;
   }
 }
 
 // acc (+)= W . X over KC chunks (KC even, runtime; ZERO: acc starts from 0).
 // W points at this wave's first fragment of chunk 0; consecutive chunks are
 // `cstride` fragments (32 B each) apart. A is double-buffered one chunk ahead
-// in registers.
+// in registers (the last chunk reloads itself: harmless, keeps the pattern).
 template <int FT, bool ZERO>
 __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], const uint4* __restrict__ W, int KC, int cstride,
                                         const uint4* X16, int lane) {
   const int g = lane >> 4, j = lane & 15;
   const uint4* wl = W + 2 * lane;
   FragX3 A0[FT], A1[FT];
+  BPair B[4];
 #pragma unroll
   for (int ft = 0; ft < FT; ++ft) A0[ft] = load_frag(wl + 2 * 64 * ft);
-  BPair B = read_b(X16, 0, 0, g, j);
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg) B[sg] = read_b(X16, 0, sg, g, j);
+  __builtin_amdgcn_sched_barrier(0);
   for (int c = 0; c < KC; c += 2) {
-    const uint4* w1 = wl + (int64_t)2 * (c + 1) * cstride;
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft) A1[ft] = load_frag(w1 + 2 * 64 * ft);
-    __builtin_amdgcn_sched_barrier(0);
     const int c2 = c + 2 < KC ? c + 2 : c + 1;
-    if (ZERO && c == 0)
-      chunk_mfma<FT, true>(acc, A0, X16, c, c + 1, B, g, j);
-    else
-      chunk_mfma<FT, false>(acc, A0, X16, c, c + 1, B, g, j);
+    const uint4* w1 = wl + (int64_t)2 * (c + 1) * cstride;
     const uint4* w2 = wl + (int64_t)2 * c2 * cstride;
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft) A0[ft] = load_frag(w2 + 2 * 64 * ft);
-    __builtin_amdgcn_sched_barrier(0);
-    chunk_mfma<FT, false>(acc, A1, X16, c + 1, c2, B, g, j);
+    if (ZERO && c == 0)
+      chunk_step<FT, true>(acc, A0, A1, w1, B, X16, c + 1, g, j);
+    else
+      chunk_step<FT, false>(acc, A0, A1, w1, B, X16, c + 1, g, j);
+    chunk_step<FT, false>(acc, A1, A0, w2, B, X16, c2, g, j);
   }
 }
 
@@ -264,10 +280,14 @@ template <int FT, bool BIAS>
 __device__ __forceinline__ float prep_input(floatx4 (&v)[FT][4], const floatx4 (&acc)[FT][4], float f,
                                             const float* __restrict__ bias, int wid, int g) {
   float mx = 0.f;
+  floatx4 bv[FT];   // all bias loads first (one wait, not one per tile)
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+    bv[ft] = BIAS ? *reinterpret_cast<const floatx4*>(bias + 16 * (FT * wid + ft) + 4 * g) : floatx4{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int ft = 0; ft < FT; ++ft) {
-    floatx4 b = {0.f, 0.f, 0.f, 0.f};
-    if (BIAS) b = *reinterpret_cast<const floatx4*>(bias + 16 * (FT * wid + ft) + 4 * g);
+    const floatx4 b = bv[ft];
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) {
       floatx4 x = BIAS ? acc[ft][sg] * f + b : acc[ft][sg] * f;
@@ -333,6 +353,12 @@ struct LdsPlan {
   static_assert(XB + TAIL <= BYTES, "X and tail must fit");
   static_assert(CAP * (256 * FT >= 1024 ? FT / 4 : 1) <= 4 * 64, "stage_rows: one lane per piece");
 };
+
+#ifdef AVR_STAMPS
+#define DBG_B(b) ((a.debug & 1) ? 0 : (b))
+#else
+#define DBG_B(b) (b)
+#endif
 
 template <int FT>
 __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
@@ -463,7 +489,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
     AVR_STAMP(6 + 5 * (b & 3));
     // fc_0 (from zero)
     const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
-    gemm_x3<FT, true>(t, P16 + L.x3_fc0[b] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
+    gemm_x3<FT, true>(t, P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
     AVR_STAMP(7 + 5 * (b & 3));
     // fc_1 input relu(t + b0)
     mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
@@ -472,14 +498,19 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
     // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
     const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
     const float r = S1 / S_h;
+    {
+      floatx4 bb[FT];   // all bias loads first (one wait, not one per tile)
 #pragma unroll
-    for (int ft = 0; ft < FT; ++ft) {
-      const floatx4 bb = *reinterpret_cast<const floatx4*>(a.packed + L.b_fc1[b] + 16 * (FT * wid + ft) + 4 * g);
+      for (int ft = 0; ft < FT; ++ft)
+        bb[ft] = *reinterpret_cast<const floatx4*>(a.packed + L.b_fc1[b] + 16 * (FT * wid + ft) + 4 * g) * S1;
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb * S1;
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb[ft];
     }
     S_h = S1;
-    gemm_x3<FT, false>(h, P16 + L.x3_fc1[b] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
+    gemm_x3<FT, false>(h, P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
     AVR_STAMP(9 + 5 * (b & 3));
   }
 

@@ -15,6 +15,8 @@ import avr._lib as L  # noqa: E402
 L.LIB_PATH = os.path.join(REPO, "adaptive-volume-rendering_amd", "build", "libavr_hip_stamps.so")
 lib = L.load(L.LIB_PATH)
 lib.avr_debug_set_stamps.argtypes = [ctypes.c_void_p]
+lib.avr_debug_set_flags.argtypes = [ctypes.c_int]
+lib.avr_debug_set_flags(int(os.environ.get('AVR_DEBUG', '0')))
 import bench  # noqa: E402
 
 dev = torch.device("cuda:0")
