@@ -150,12 +150,11 @@ __device__ __forceinline__ float z_feature(const SampleGeom& s, int k, int num_f
   return 0.f;
 }
 
-// sin(a) for the positional encoding, ~1.5 ulp (numpy's float32 sin: ~1.45):
-// Cody-Waite reduction by pi/2 (3-term split, fma) + Cephes minimax
-// polynomials on [-pi/4, pi/4]. About 20 VALU ops instead of the library
-// sinf's generic path; |a| > 8192 falls back to sinf.
-__device__ __forceinline__ float pe_sin(float a) {
-  if (fabsf(a) > 8192.f) return sinf(a);
+// sin(a) for the positional encoding, ~1.5 ulp for |a| <= 8192 (numpy's
+// float32 sin: ~1.45): Cody-Waite reduction by pi/2 (3-term split, fma) +
+// Cephes minimax polynomials on [-pi/4, pi/4], straight-line (~25 VALU ops).
+// Callers route |a| > 8192 to sinf.
+__device__ __forceinline__ float pe_sin_fast(float a) {
   const float j = __builtin_rintf(a * 0.6366197466850281f);
   float r = __builtin_fmaf(-j, 1.5707963705062866f, a);
   r = __builtin_fmaf(-j, -4.371138828673793e-08f, r);

@@ -408,16 +408,31 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
   float pe[kPeSlots], xo = 0.f, vo = 0.f;
   float mx = 0.f;
   {
-    const auto pick = [](const float* v, int i) { return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]); };
+    // straight-line: every slot computes (selects, no branches); slots past
+    // npe are zeroed; the rare |argument| > 8192 takes sinf (uniform branch)
+    float arg[kPeSlots];
+    bool big = false;
 #pragma unroll
     for (int i = 0; i < kPeSlots; ++i) {
       const int q = g + 4 * i, jj = q / 3, dd = q - 3 * jj;
-      const float freq = fmul(a.freq_factor, (float)(1 << (jj >> 1)));
+      const float x = dd == 0 ? xr[0] : (dd == 1 ? xr[1] : xr[2]);
+      const float freq = fmul(a.freq_factor, __builtin_ldexpf(1.0f, jj >> 1));
       const float phase = (jj & 1) ? 1.5707963705062866f : 0.f;  // fp32(pi/2)
-      pe[i] = q < npe ? pe_sin(fadd(phase, fmul(pick(xr, dd), freq))) : 0.f;
+      arg[i] = fadd(phase, fmul(x, freq));
+      pe[i] = pe_sin_fast(arg[i]);
+      big |= q < npe && fabsf(arg[i]) > 8192.f;
+    }
+    if (__builtin_expect(__any(big), 0)) {
+#pragma unroll
+      for (int i = 0; i < kPeSlots; ++i)
+        if (fabsf(arg[i]) > 8192.f) pe[i] = sinf(arg[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < kPeSlots; ++i) {
+      pe[i] = g + 4 * i < npe ? pe[i] : 0.f;
       mx = fmaxf(mx, fabsf(pe[i]));
     }
-    if (g < 3) { xo = pick(xr, g); vo = pick(vr, g); }
+    if (g < 3) { xo = g == 0 ? xr[0] : (g == 1 ? xr[1] : xr[2]); vo = g == 0 ? vr[0] : (g == 1 ? vr[1] : vr[2]); }
     mx = fmaxf(mx, fmaxf(fabsf(xo), fabsf(vo)));
     mx = wave_max(mx);
   }
