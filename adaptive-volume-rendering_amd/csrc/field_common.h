@@ -50,7 +50,7 @@ struct FieldArgs {
   const float* xyz; const float* vd;
   int64_t M;
   float4* out;
-  unsigned long long* stamps;  // diagnostic builds (-DAVR_STAMPS) only: per-block phase clocks
+  unsigned long long* stamps;  // diagnostic builds (-DAVR_STAMPS) only: per-block phase clocks (waves 0, 4)
   int debug;                   // diagnostic builds only: experiment flags (1: every fc layer uses block 0's weights)
 };
 
@@ -61,7 +61,8 @@ struct FieldArgs {
     unsigned long long _t;                                                                    \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");              \
     __builtin_amdgcn_sched_barrier(0);                                                        \
-    if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 32 + (k)] = _t;         \
+    if (a.stamps && (threadIdx.x & 255) == 0)                                                 \
+      a.stamps[(int64_t)blockIdx.x * 64 + 32 * (threadIdx.x >> 8) + (k)] = _t;                \
   } while (0)
 #else
 #define AVR_STAMP(k) do { } while (0)

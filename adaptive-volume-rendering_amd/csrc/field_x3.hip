@@ -117,7 +117,7 @@ __device__ __forceinline__ void chunk_step(floatx4 (&acc)[FT][4], const FragX3 (
 // W points at this wave's first fragment of chunk 0; consecutive chunks are
 // `cstride` fragments (32 B each) apart. A is double-buffered one chunk ahead
 // in registers (the last chunk reloads itself: harmless, keeps the pattern).
-template <int FT, bool ZERO>
+template <int FT, bool ZERO, bool SYNC>
 __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], const uint4* __restrict__ W, int KC, int cstride,
                                         const uint4* X16, int lane) {
   const int g = lane >> 4, j = lane & 15;
@@ -138,6 +138,11 @@ __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], const uint4* __re
     else
       chunk_step<FT, false>(acc, A0, A1, w1, B, X16, c + 1, g, j);
     chunk_step<FT, false>(acc, A1, A0, w2, B, X16, c2, g, j);
+    // two waves per SIMD: the older one would otherwise win the MFMA pipe and
+    // run a whole layer ahead, leaving its partner's epilogue unoverlapped;
+    // a plain barrier every two chunks keeps them in step (the MFMA pipe stays
+    // busy with the lagging wave meanwhile)
+    if (SYNC) __builtin_amdgcn_s_barrier();
   }
 }
 
@@ -168,58 +173,61 @@ constexpr unsigned kEmpty = 0xffffffffu;
 // Entry e = threadIdx.x (sample e>>2, corner e&3); tail->tex complete and
 // ht_key/ht_min initialised before the first barrier inside. Returns the
 // number of distinct texels; tail->slot is complete after the last barrier.
+// Entries live in threads 0..255 (waves 0..3); other waves only join the barriers.
 __device__ __forceinline__ int dedup_texels(ZTail* tail, int lane, int wid) {
   const int e = threadIdx.x;
+  const bool ent = e < 256;
   __syncthreads();
-  const unsigned tex = (unsigned)tail->tex[e];
+  const unsigned tex = ent ? (unsigned)tail->tex[e] : 0u;
   unsigned b = (tex * 2654435761u) >> 23;  // 9-bit bucket
-  for (;;) {
-    const unsigned old = atomicCAS(&tail->ht_key[b], kEmpty, tex);
-    if (old == kEmpty || old == tex) break;
-    b = (b + 1) & 511;
+  if (ent) {
+    for (;;) {
+      const unsigned old = atomicCAS(&tail->ht_key[b], kEmpty, tex);
+      if (old == kEmpty || old == tex) break;
+      b = (b + 1) & 511;
+    }
+    atomicMin(&tail->ht_min[b], (unsigned)e);
   }
-  atomicMin(&tail->ht_min[b], (unsigned)e);
   __syncthreads();
-  const int first = (int)tail->ht_min[b];
-  const bool is_first = first == e;
+  const int first = ent ? (int)tail->ht_min[b] : -1;
+  const bool is_first = ent && first == e;
   const unsigned long long m = __ballot(is_first);
   const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
-  if (lane == 0) tail->wtot[wid] = __popcll(m);
+  if (ent && lane == 0) tail->wtot[wid] = __popcll(m);
   __syncthreads();
   int off = 0;
 #pragma unroll
-  for (int w = 0; w < kFieldWaves; ++w) off += w < wid ? tail->wtot[w] : 0;
+  for (int w = 0; w < 4; ++w) off += w < wid ? tail->wtot[w] : 0;
   const int D = tail->wtot[0] + tail->wtot[1] + tail->wtot[2] + tail->wtot[3];
   if (is_first) {
     tail->uniq[off + pos] = (int)tex;
     tail->first_slot[e] = off + pos;
   }
   __syncthreads();
-  tail->slot[e] = tail->first_slot[first];
+  if (ent) tail->slot[e] = tail->first_slot[first];
   return D;
 }
 
 // Copy table rows uniq[lo .. lo+n) (row = HID floats) to stage rows 0 .. n
-// (stride RS bytes) by LDS-DMA; wave w takes pieces w, w+4, ... of 1 KiB.
+// (stride RS bytes) by LDS-DMA; wave w takes pieces w, w+NW, ... of 1 KiB.
 // The row indices are read from LDS up front (lane i holds the row of the
 // wave's i-th piece): an LDS read between two LDS-DMA issues would make the
 // compiler wait for the earlier DMA to land.
-template <int FT>
+template <int HID, int NW>
 __device__ __forceinline__ void stage_rows(char* stage, const float* __restrict__ table, const ZTail* tail, int lo,
                                            int n, int RS, int lane, int wid) {
-  constexpr int HID = 64 * FT;
   constexpr int ROWB = 4 * HID;                                  // bytes per row
   constexpr int PPR = ROWB >= 1024 ? ROWB / 1024 : 1;            // pieces per row
   constexpr int LANES = ROWB >= 1024 ? 64 : ROWB / 16;           // active lanes per piece
   const int npc = n * PPR;
-  const int mine = (npc - wid + kFieldWaves - 1) / kFieldWaves;  // pieces of this wave (<= 64 * PPR)
+  const int mine = (npc - wid + NW - 1) / NW;                    // pieces of this wave (<= 64)
   int rowv = 0;
   {
-    const int pc = wid + kFieldWaves * lane;
+    const int pc = wid + NW * lane;
     if (lane < mine) rowv = tail->uniq[lo + pc / PPR];
   }
   for (int i = 0; i < mine; ++i) {
-    const int pc = wid + kFieldWaves * i;
+    const int pc = wid + NW * i;
     const int r = pc / PPR, q = pc - r * PPR;
     const int row = __builtin_amdgcn_readlane(rowv, i);
     const char* src = reinterpret_cast<const char*>(table + (int64_t)row * HID) + 1024 * q + 16 * lane;
@@ -321,18 +329,22 @@ __device__ __forceinline__ float layer_scale(const float* packed, const Layout& 
   return pow2_scale_for(__uint_as_float(reinterpret_cast<const unsigned*>(packed + L.x3_hdr)[layer]));
 }
 
+template <int NW>
 __device__ __forceinline__ float red_max(const float* red) {
-  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float m = red[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w]);
+  return m;
 }
 
 // relu'd layer input -> LDS (two barriers: all reads of the previous X done /
 // all writes of the new X visible); returns the operand scale s_x
-template <int FT>
+template <int FT, int NW>
 __device__ __forceinline__ float publish(uint4* X16, const floatx4 (&v)[FT][4], float mx, float* red, int wid,
                                          int lane, int g, int j) {
   if (lane == 0) red[wid] = mx;
   __syncthreads();
-  const float s_x = pow2_scale_for(red_max(red));
+  const float s_x = pow2_scale_for(red_max<NW>(red));
   store_split<FT>(X16, v, s_x, wid, g, j);
   __syncthreads();
   return s_x;
@@ -340,18 +352,18 @@ __device__ __forceinline__ float publish(uint4* X16, const floatx4 (&v)[FT][4], 
 
 // LDS plan: X (KCX chunks x 8 KiB) from byte 0; the lin_z stage aliases X
 // (rows of RS bytes from byte 0); ZTail at the top of the allocation.
-template <int FT>
+template <int HID>
 struct LdsPlan {
-  static constexpr int KC = 2 * FT;
+  static constexpr int KC = HID / 32;
   static constexpr int KCX = KC > kX3InChunks ? KC : kX3InChunks;
   static constexpr int XB = KCX * 8192;
-  static constexpr int RS = 256 * FT + 16;
+  static constexpr int RS = 4 * HID + 16;
   static constexpr int TAIL = (int)((sizeof(ZTail) + 15) / 16 * 16);
   static constexpr int WANT = (XB > 96 * RS ? XB : 96 * RS) + TAIL;
   static constexpr int BYTES = WANT < 160 * 1024 ? WANT : 160 * 1024;
   static constexpr int CAP = (BYTES - TAIL) / RS;
   static_assert(XB + TAIL <= BYTES, "X and tail must fit");
-  static_assert(CAP * (256 * FT >= 1024 ? FT / 4 : 1) <= 4 * 64, "stage_rows: one lane per piece");
+  static_assert(CAP * (4 * HID >= 1024 ? HID / 256 : 1) <= 4 * 64, "stage_rows: one lane per piece");
 };
 
 #ifdef AVR_STAMPS
@@ -360,11 +372,16 @@ struct LdsPlan {
 #define DBG_B(b) (b)
 #endif
 
-template <int FT>
-__global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
-  using P = LdsPlan<FT>;
+// Work split: NW waves (4: one per SIMD; 8: two per SIMD, which doubles the
+// VALU issue rate of the epilogues and hides one wave's stalls behind the
+// other); wave w owns the FT 16-row feature tiles FT*w .. FT*w + FT-1.
+template <int FT, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
+  constexpr int HID = 16 * FT * NW;
+  using P = LdsPlan<HID>;
   constexpr int KC = P::KC;
-  constexpr int NTT = 4 * FT;                      // feature tiles of a hidden layer
+  constexpr int NTT = FT * NW;                     // feature tiles of a hidden layer
+  constexpr int PES = (6 * 7 + NW - 1) / NW;       // PE slots per lane (6 * num_freqs <= 42)
   extern __shared__ float lds[];
   uint4* X16 = reinterpret_cast<uint4*>(lds);      // KCX * 512 slots of 16 B
   char* stage = reinterpret_cast<char*>(lds);
@@ -372,30 +389,28 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
   float* red = tail->red;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, j = lane & 15;
+  const int gg = g + 4 * (wid >> 2);               // prologue: sub-lane of sample 16 (wid & 3) + j
   const int64_t base = (int64_t)blockIdx.x * kX3Samples;
   const Layout& L = a.L;
   const uint4* P16 = reinterpret_cast<const uint4*>(a.packed);  // 16-B units
 
   AVR_STAMP(0);
-  // ---- prologue: wave w prepares samples 16w + j (lanes g share the geometry).
-  // The 6 * num_freqs sines of a sample are spread over its 4 lanes (lane g:
-  // PE entries g, g + 4, ...; lanes 0-2 also own xyz_rot[g] / R viewdir[g]),
-  // then each value is written as fp16 hi/lo into its B-fragment slot; the
-  // padding features d_in .. 63 stay zero.
+  // ---- prologue: waves w and w+4 prepare samples 16 (w & 3) + j (the lanes
+  // share the geometry). The 6 * num_freqs sines of a sample are spread over
+  // its NW sub-lanes gg (PE entries gg, gg + NW, ...; sub-lanes 0-2 also own
+  // xyz_rot[gg] / R viewdir[gg]), then each value is written as fp16 hi/lo
+  // into its B-fragment slot; the padding features d_in .. 63 stay zero.
   {
-    uint4* xz = X16 + threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < 2 * kX3InChunks; ++i) xz[256 * i] = make_uint4(0u, 0u, 0u, 0u);
-    tail->ht_key[threadIdx.x] = kEmpty; tail->ht_key[threadIdx.x + 256] = kEmpty;
-    tail->ht_min[threadIdx.x] = kEmpty; tail->ht_min[threadIdx.x + 256] = kEmpty;
+    for (int i = threadIdx.x; i < 2 * kX3InChunks * 256; i += 64 * NW) X16[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = threadIdx.x; i < 512; i += 64 * NW) { tail->ht_key[i] = kEmpty; tail->ht_min[i] = kEmpty; }
   }
   const int npe = 6 * a.num_freqs;
   float xr[3], vr[3];
   {
-    const int s = 16 * wid + j;
+    const int s = 16 * (wid & 3) + j;
     const int64_t m = base + s;
     const SampleGeom geo = sample_geom(a, m < a.M ? m : a.M - 1);
-    if (g == 0) {
+    if (g == 0 && wid < 4) {
       *reinterpret_cast<int4*>(tail->tex + 4 * s) = make_int4(geo.bl.tex[0], geo.bl.tex[1], geo.bl.tex[2], geo.bl.tex[3]);
       *reinterpret_cast<float4*>(tail->w + 4 * s) = make_float4(geo.bl.w[0], geo.bl.w[1], geo.bl.w[2], geo.bl.w[3]);
     }
@@ -405,16 +420,16 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
   AVR_STAMP(27);
   const int D = a.n_lin_z > 0 ? dedup_texels(tail, lane, wid) : 0;
   AVR_STAMP(28);
-  float pe[kPeSlots], xo = 0.f, vo = 0.f;
+  float pe[PES], xo = 0.f, vo = 0.f;
   float mx = 0.f;
   {
     // straight-line: every slot computes (selects, no branches); slots past
     // npe are zeroed; the rare |argument| > 8192 takes sinf (uniform branch)
-    float arg[kPeSlots];
+    float arg[PES];
     bool big = false;
 #pragma unroll
-    for (int i = 0; i < kPeSlots; ++i) {
-      const int q = g + 4 * i, jj = q / 3, dd = q - 3 * jj;
+    for (int i = 0; i < PES; ++i) {
+      const int q = gg + NW * i, jj = q / 3, dd = q - 3 * jj;
       const float x = dd == 0 ? xr[0] : (dd == 1 ? xr[1] : xr[2]);
       const float freq = fmul(a.freq_factor, __builtin_ldexpf(1.0f, jj >> 1));
       const float phase = (jj & 1) ? 1.5707963705062866f : 0.f;  // fp32(pi/2)
@@ -424,15 +439,15 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
     }
     if (__builtin_expect(__any(big), 0)) {
 #pragma unroll
-      for (int i = 0; i < kPeSlots; ++i)
+      for (int i = 0; i < PES; ++i)
         if (fabsf(arg[i]) > 8192.f) pe[i] = sinf(arg[i]);
     }
 #pragma unroll
-    for (int i = 0; i < kPeSlots; ++i) {
-      pe[i] = g + 4 * i < npe ? pe[i] : 0.f;
+    for (int i = 0; i < PES; ++i) {
+      pe[i] = gg + NW * i < npe ? pe[i] : 0.f;
       mx = fmaxf(mx, fabsf(pe[i]));
     }
-    if (g < 3) { xo = g == 0 ? xr[0] : (g == 1 ? xr[1] : xr[2]); vo = g == 0 ? vr[0] : (g == 1 ? vr[1] : vr[2]); }
+    if (gg < 3) { xo = gg == 0 ? xr[0] : (gg == 1 ? xr[1] : xr[2]); vo = gg == 0 ? vr[0] : (gg == 1 ? vr[1] : vr[2]); }
     mx = fmaxf(mx, fmaxf(fabsf(xo), fabsf(vo)));
     mx = wave_max(mx);
   }
@@ -441,8 +456,8 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
   {
     if (lane == 0) red[wid] = mx;
     __syncthreads();
-    s_x = pow2_scale_for(red_max(red));
-    const int s = 16 * wid + j;
+    s_x = pow2_scale_for(red_max<NW>(red));
+    const int s = 16 * (wid & 3) + j;
     char* xb = reinterpret_cast<char*>(X16);
     // feature k -> chunk k>>5, lane group (k>>2)&3, element 4*((k>>4)&1) + (k&3)
     const auto put = [&](int k, float val) {
@@ -453,9 +468,9 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
       *reinterpret_cast<_Float16*>(xb + xidx(c, 1, gg, s) * 16 + 2 * e) = (_Float16)(y - (float)hi);
     };
 #pragma unroll
-    for (int i = 0; i < kPeSlots; ++i)
-      if (g + 4 * i < npe) put(3 + g + 4 * i, pe[i]);
-    if (g < 3) { put(g, xo); put(3 + npe + g, vo); }
+    for (int i = 0; i < PES; ++i)
+      if (gg + NW * i < npe) put(3 + gg + NW * i, pe[i]);
+    if (gg < 3) { put(gg, xo); put(3 + npe + gg, vo); }
     __syncthreads();
   }
 
@@ -471,7 +486,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
     for (int sg = 0; sg < 4; ++sg) h[ft][sg] = b * S_h;
   }
   AVR_STAMP(3);
-  gemm_x3<FT, false>(h, P16 + L.x3_in / 4 + 2 * 64 * FT * wid, kX3InChunks, 64 * NTT, X16, lane);
+  gemm_x3<FT, false, (NW > 4)>(h, P16 + L.x3_in / 4 + 2 * 64 * FT * wid, kX3InChunks, 64 * NTT, X16, lane);
   AVR_STAMP(4);
 
   for (int b = 0; b < a.n_blocks; ++b) {
@@ -480,7 +495,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
     if (b < a.n_lin_z) __syncthreads();  // every wave is done reading X (the stage aliases it)
     const float* table = a.table + b * a.table_stride;
     if (b < a.n_lin_z && D <= P::CAP) {
-      stage_rows<FT>(stage, table, tail, 0, D, P::RS, lane, wid);
+      stage_rows<HID, NW>(stage, table, tail, 0, D, P::RS, lane, wid);
       AVR_STAMP(29);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -492,7 +507,7 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
       for (int lo = 0; b < a.n_lin_z && lo < D; lo += P::CAP) {   // more distinct texels than the stage holds
         const int n = D - lo < P::CAP ? D - lo : P::CAP;
         if (lo > 0) __syncthreads();
-        stage_rows<FT>(stage, table, tail, lo, n, P::RS, lane, wid);
+        stage_rows<HID, NW>(stage, table, tail, lo, n, P::RS, lane, wid);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         blend_stage<FT, false>(h, v, mx, stage, tail, lo, n, P::RS, S_h, 1.0f / S_h, wid, g, j);
@@ -500,15 +515,15 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
       mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
     }
     AVR_STAMP(5 + 5 * (b & 3));
-    s_x = publish<FT>(X16, v, mx, red, wid, lane, g, j);
+    s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
     AVR_STAMP(6 + 5 * (b & 3));
     // fc_0 (from zero)
     const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
-    gemm_x3<FT, true>(t, P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
+    gemm_x3<FT, true, (NW > 4)>(t, P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
     AVR_STAMP(7 + 5 * (b & 3));
     // fc_1 input relu(t + b0)
     mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
-    s_x = publish<FT>(X16, v, mx, red, wid, lane, g, j);
+    s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
     AVR_STAMP(8 + 5 * (b & 3));
     // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
     const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
@@ -525,20 +540,21 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
         for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb[ft];
     }
     S_h = S1;
-    gemm_x3<FT, false>(h, P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
+    gemm_x3<FT, false, (NW > 4)>(h, P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
     AVR_STAMP(9 + 5 * (b & 3));
   }
 
-  // ---- lin_out(relu(h)): wave w computes the 16-row output tile for samples 16w + j.
+  // ---- lin_out(relu(h)): waves 0-3 compute the 16-row output tile for samples 16w + j.
   FragX3 Ao[KC];
-  {
-    const uint4* wo = P16 + L.x3_out / 4 + 2 * lane;
+  const uint4* wo = P16 + L.x3_out / 4 + 2 * lane;
+  if (wid < 4) {
 #pragma unroll
     for (int c = 0; c < KC; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
   }
   mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
-  s_x = publish<FT>(X16, v, mx, red, wid, lane, g, j);
+  s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
   AVR_STAMP(25);
+  if (wid >= 4) return;
   const float S = layer_scale(a.packed, L, 1) * s_x;
   floatx4 o = *reinterpret_cast<const floatx4*>(a.packed + L.b_out + 4 * g) * S;
   {
@@ -558,28 +574,28 @@ __global__ void __launch_bounds__(256, 1) field_x3_kernel(FieldArgs a) {
   if (g == 0 && m < a.M) a.out[m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
 }
 
-template <int FT>
+template <int FT, int NW>
 static int launch_x3(const FieldArgs& a, hipStream_t s) {
-  const size_t shm = LdsPlan<FT>::BYTES;
+  const size_t shm = LdsPlan<16 * FT * NW>::BYTES;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT, NW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
       return fail(AVR_E_HIP, "field_x3_kernel: cannot set dynamic LDS to %zu", shm);
     attr = true;
   }
   const int64_t blocks = (a.M + kX3Samples - 1) / kX3Samples;
   AVR_REQUIRE(blocks < (1ll << 31), "field: too many points");
-  field_x3_kernel<FT><<<(unsigned)blocks, 64 * kFieldWaves, shm, s>>>(a);
+  field_x3_kernel<FT, NW><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("field_x3_kernel");
 }
 
 int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s) {
   switch (d_hidden) {
-    case 64: return launch_x3<1>(a, s);
-    case 128: return launch_x3<2>(a, s);
-    case 256: return launch_x3<4>(a, s);
-    case 512: return launch_x3<8>(a, s);
+    case 64: return launch_x3<1, 4>(a, s);
+    case 128: return launch_x3<2, 4>(a, s);
+    case 256: return launch_x3<4, 4>(a, s);
+    case 512: return launch_x3<8, 4>(a, s);
   }
   return fail(AVR_E_UNSUPPORTED, "field x3: d_hidden %d", d_hidden);
 }

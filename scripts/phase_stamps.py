@@ -28,7 +28,7 @@ ro = torch.tensor([[0.3, -1.1, 0.5]], device=dev).expand(R, 3).contiguous()
 rd = torch.nn.functional.normalize(-ro + 0.3 * torch.randn(R, 3, device=dev), dim=-1)
 z = torch.sort(0.8 + torch.rand(R, N, device=dev), -1)[0]
 blocks = (R * N + 63) // 64
-stamps = torch.zeros(blocks * 32, dtype=torch.int64, device=dev)
+stamps = torch.zeros(blocks * 64, dtype=torch.int64, device=dev)
 with torch.no_grad():
     f.forward_rays(ro, rd, z, False)
     torch.cuda.synchronize()
@@ -37,7 +37,10 @@ with torch.no_grad():
     t0.record(); f.forward_rays(ro, rd, z, False); t1.record()
     torch.cuda.synchronize()
     lib.avr_debug_set_stamps(None)
-st = stamps.view(blocks, 32).cpu().numpy().astype(np.int64)
+st_all = stamps.view(blocks, 2, 32).cpu().numpy().astype(np.int64)
+st = st_all[:, 0]
+w4 = st_all[:, 1]
+have4 = (w4[:, 0] != 0).mean() > 0.99
 names = {0: "start", 27: "sample_geom", 28: "dedup texels", 1: "PE sines", 2: "publish X0", 3: "lin_in init",
          4: "lin_in gemm"}
 for b in range(4):
@@ -49,9 +52,12 @@ used.sort(key=lambda k: np.median(st[:, k] - st[:, 0]))
 print(f"kernel {t0.elapsed_time(t1):.2f} ms for {R * N} samples, {blocks} blocks")
 tot = np.median(st[:, used[-1]] - st[:, 0])
 prev = used[0]
+print(f"{'phase':28s} {'wave0':>10s}        {'end(w0)':>9s} {'end(w4)':>9s}")
 for k in used[1:]:
     d = np.median(st[:, k] - st[:, prev])
-    print(f"{names[k]:28s} {d:10.0f} cyc  {100 * d / tot:5.1f} %")
+    e0 = np.median(st[:, k] - st[:, 0])
+    e4 = np.median(w4[:, k] - st[:, 0]) if have4 else float("nan")
+    print(f"{names[k]:28s} {d:10.0f} cyc  {100 * d / tot:5.1f} % {e0:9.0f} {e4:9.0f}")
     prev = k
 print(f"{'total (median per block)':28s} {tot:10.0f} cyc")
 span = (st[:, used[-1]].max() - st[:, 0].min())
