@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(REPO, "adaptive-volume-rendering_amd"))
 sys.path.insert(0, REPO)
 import avr._lib as L  # noqa: E402
 
-L.LIB_PATH = os.path.join(REPO, "adaptive-volume-rendering_amd", "build", "libavr_hip_stamps.so")
+L.LIB_PATH = os.environ.get("STAMPS_LIB") or os.path.join(REPO, "adaptive-volume-rendering_amd", "build", "libavr_hip_stamps.so")
 lib = L.load(L.LIB_PATH)
 lib.avr_debug_set_stamps.argtypes = [ctypes.c_void_p]
 lib.avr_debug_set_flags.argtypes = [ctypes.c_int]
