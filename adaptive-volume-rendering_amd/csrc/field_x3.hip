@@ -117,15 +117,29 @@ __device__ __forceinline__ void chunk_step(floatx4 (&acc)[FT][4], const FragX3 (
 // W points at this wave's first fragment of chunk 0; consecutive chunks are
 // `cstride` fragments (32 B each) apart. A is double-buffered one chunk ahead
 // in registers (the last chunk reloads itself: harmless, keeps the pattern).
+// This wave's chunk-0 A fragments of a layer, loaded ahead of the layer
+// (before the publish that precedes it) so the GEMM starts on landed data.
+// Only the first kPrefetch tiles (the first group of chunk 0) are prefetched:
+// more would push the epilogue into spills, and a scratch store waits for
+// every outstanding load.
+constexpr int kPrefetch = 2;
+
+template <int FT>
+__device__ __forceinline__ void prefetch_a(FragX3 (&A0)[FT], const uint4* __restrict__ W, int lane) {
+#pragma unroll
+  for (int ft = 0; ft < (FT < kPrefetch ? FT : kPrefetch); ++ft) A0[ft] = load_frag(W + 2 * lane + 2 * 64 * ft);
+}
+
+// A0 holds chunk 0 (prefetch_a).
 template <int FT, bool ZERO, bool SYNC>
-__device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], const uint4* __restrict__ W, int KC, int cstride,
-                                        const uint4* X16, int lane) {
+__device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W, int KC,
+                                        int cstride, const uint4* X16, int lane) {
   const int g = lane >> 4, j = lane & 15;
   const uint4* wl = W + 2 * lane;
-  FragX3 A0[FT], A1[FT];
+  FragX3 A1[FT];
   BPair B[4];
 #pragma unroll
-  for (int ft = 0; ft < FT; ++ft) A0[ft] = load_frag(wl + 2 * 64 * ft);
+  for (int ft = kPrefetch; ft < FT; ++ft) A0[ft] = load_frag(wl + 2 * 64 * ft);
 #pragma unroll
   for (int sg = 0; sg < 4; ++sg) B[sg] = read_b(X16, 0, sg, g, j);
   __builtin_amdgcn_sched_barrier(0);
@@ -277,6 +291,11 @@ __device__ __forceinline__ void blend_stage(floatx4 (&h)[FT][4], floatx4 (&v)[FT
   }
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not
+// for its outstanding global loads (the next layer's weight prefetch stays in
+// flight; __syncthreads would drain it).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) v = fmaxf(v, __shfl_xor(v, d, 64));
@@ -343,10 +362,10 @@ template <int FT, int NW>
 __device__ __forceinline__ float publish(uint4* X16, const floatx4 (&v)[FT][4], float mx, float* red, int wid,
                                          int lane, int g, int j) {
   if (lane == 0) red[wid] = mx;
-  __syncthreads();
+  lds_barrier();
   const float s_x = pow2_scale_for(red_max<NW>(red));
   store_split<FT>(X16, v, s_x, wid, g, j);
-  __syncthreads();
+  lds_barrier();
   return s_x;
 }
 
@@ -451,11 +470,14 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     mx = fmaxf(mx, fmaxf(fabsf(xo), fabsf(vo)));
     mx = wave_max(mx);
   }
+  FragX3 A0[FT];   // chunk 0 of the next GEMM's weights, prefetched before the publish ahead of it
+  const uint4* Win = P16 + L.x3_in / 4 + 2 * 64 * FT * wid;
+  prefetch_a<FT>(A0, Win, lane);
   AVR_STAMP(1);
   float s_x;
   {
     if (lane == 0) red[wid] = mx;
-    __syncthreads();
+    lds_barrier();
     s_x = pow2_scale_for(red_max<NW>(red));
     const int s = 16 * (wid & 3) + j;
     char* xb = reinterpret_cast<char*>(X16);
@@ -471,7 +493,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     for (int i = 0; i < PES; ++i)
       if (gg + NW * i < npe) put(3 + gg + NW * i, pe[i]);
     if (gg < 3) { put(gg, xo); put(3 + npe + gg, vo); }
-    __syncthreads();
+    lds_barrier();
   }
 
   AVR_STAMP(2);
@@ -486,13 +508,13 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     for (int sg = 0; sg < 4; ++sg) h[ft][sg] = b * S_h;
   }
   AVR_STAMP(3);
-  gemm_x3<FT, false, (NW > 4)>(h, P16 + L.x3_in / 4 + 2 * 64 * FT * wid, kX3InChunks, 64 * NTT, X16, lane);
+  gemm_x3<FT, false, (NW > 4)>(h, A0, Win, kX3InChunks, 64 * NTT, X16, lane);
   AVR_STAMP(4);
 
   for (int b = 0; b < a.n_blocks; ++b) {
     // + lin_z[b](interp latent) (models.py ResnetFC: x = x + lin_z[b](z) before block b)
     // (fused with the fc_0 input prep: v = relu(h), mx)
-    if (b < a.n_lin_z) __syncthreads();  // every wave is done reading X (the stage aliases it)
+    if (b < a.n_lin_z) lds_barrier();  // every wave is done reading X (the stage aliases it)
     const float* table = a.table + b * a.table_stride;
     if (b < a.n_lin_z && D <= P::CAP) {
       stage_rows<HID, NW>(stage, table, tail, 0, D, P::RS, lane, wid);
@@ -515,14 +537,18 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
     }
     AVR_STAMP(5 + 5 * (b & 3));
+    const uint4* W0 = P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
+    prefetch_a<FT>(A0, W0, lane);
     s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
     AVR_STAMP(6 + 5 * (b & 3));
     // fc_0 (from zero)
     const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
-    gemm_x3<FT, true, (NW > 4)>(t, P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
+    gemm_x3<FT, true, (NW > 4)>(t, A0, W0, KC, 64 * NTT, X16, lane);
     AVR_STAMP(7 + 5 * (b & 3));
     // fc_1 input relu(t + b0)
     mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
+    const uint4* W1 = P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
+    prefetch_a<FT>(A0, W1, lane);
     s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
     AVR_STAMP(8 + 5 * (b & 3));
     // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
@@ -540,19 +566,24 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
         for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb[ft];
     }
     S_h = S1;
-    gemm_x3<FT, false, (NW > 4)>(h, P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid, KC, 64 * NTT, X16, lane);
+    gemm_x3<FT, false, (NW > 4)>(h, A0, W1, KC, 64 * NTT, X16, lane);
     AVR_STAMP(9 + 5 * (b & 3));
   }
 
   // ---- lin_out(relu(h)): waves 0-3 compute the 16-row output tile for samples 16w + j.
+  // (a quarter of lin_out's A fragments are loaded ahead of the publish, the rest after)
   FragX3 Ao[KC];
   const uint4* wo = P16 + L.x3_out / 4 + 2 * lane;
   if (wid < 4) {
 #pragma unroll
-    for (int c = 0; c < KC; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
+    for (int c = 0; c < KC / 4; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
   }
   mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
   s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+  if (wid < 4) {
+#pragma unroll
+    for (int c = KC / 4; c < KC; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
+  }
   AVR_STAMP(25);
   if (wid >= 4) return;
   const float S = layer_scale(a.packed, L, 1) * s_x;
