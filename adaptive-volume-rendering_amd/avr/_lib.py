@@ -54,6 +54,13 @@ _SIGS = {
     "avr_composite_fwd": [c_void_p, c_void_p, i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_composite_bwd": [c_void_p, c_void_p, i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p],
+    "avr_march_state_bytes": [i64, ctypes.POINTER(i64)],
+    "avr_march_init": [i64, c_void_p, c_void_p, c_void_p],
+    "avr_march_gather": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_int, c_int, c_int, c_void_p, c_void_p,
+                         c_void_p, c_void_p],
+    "avr_march_composite": [c_void_p, c_void_p, c_void_p, i64, c_int, c_int, c_int, c_float, c_float, c_void_p,
+                            c_void_p, c_void_p, c_void_p],
+    "avr_march_finish": [c_void_p, i64, c_int, c_void_p, c_void_p, c_void_p],
     "avr_field_packed_floats": [ctypes.POINTER(FieldDims), ctypes.POINTER(i64)],
     "avr_field_pack": [ctypes.POINTER(FieldDims), ctypes.POINTER(ResnetFCWeights), c_void_p, c_void_p],
     "avr_field_latent_table": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],

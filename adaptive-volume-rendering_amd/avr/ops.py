@@ -3,6 +3,8 @@
 All tensors are device tensors owned by PyTorch; every launch is enqueued on
 torch's current HIP stream. No function here has a host/CPU implementation.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -166,3 +168,44 @@ def points(ro, rd, z):
     pts = torch.addcmul(ro.reshape(R, 1, 3), rd.reshape(R, 1, 3), z.reshape(R, N, 1))
     vd = rd.reshape(R, 1, 3).expand(R, N, 3)
     return pts.reshape(R * N, 3), vd.reshape(R * N, 3)
+
+
+def march_fine(ro, rd, z, field_fn, t_stop, white_back=True, infinity=1.8, chunk=64):
+    """Fine pass with early ray termination (BASELINE config 4; not in the
+    reference): the samples z (R, N) are evaluated front to back in chunks of
+    `chunk`, and a ray leaves the active set once its transmittance drops
+    below `t_stop` (its skipped tail changes rgb by <= t_stop).
+    field_fn(ro_c, rd_c, z_c) -> (n_act * C, 4) evaluates the field on a chunk.
+    Returns rgb (R, 3), dist (R,), and the number of field samples evaluated."""
+    R, N = z.shape
+    ro, rd, z = _f32c(ro.reshape(R, 3)), _f32c(rd.reshape(R, 3)), _f32c(z)
+    require_device(ro, rd, z)
+    dev, s = z.device, stream_of(z)
+    nbytes = ctypes.c_int64()
+    call("avr_march_state_bytes", R, ctypes.byref(nbytes))
+    state = torch.empty(max(nbytes.value, 8), device=dev, dtype=torch.uint8)
+    active = torch.empty(max(R, 1), device=dev, dtype=torch.int32)
+    spare = torch.empty_like(active)
+    count = torch.zeros(1, device=dev, dtype=torch.int32)
+    call("avr_march_init", R, ptr(state), ptr(active), s)
+    n_act, evaluated = R, 0
+    for c0 in range(0, N, chunk):
+        if n_act == 0:
+            break
+        C = min(chunk, N - c0)
+        ro_c = torch.empty(n_act, 3, device=dev, dtype=F32)
+        rd_c = torch.empty_like(ro_c)
+        z_c = torch.empty(n_act, C, device=dev, dtype=F32)
+        call("avr_march_gather", ptr(ro), ptr(rd), ptr(z), ptr(active), n_act, N, c0, C, ptr(ro_c), ptr(rd_c),
+             ptr(z_c), s)
+        f_c = _f32c(field_fn(ro_c, rd_c, z_c).reshape(n_act, C, 4))
+        evaluated += n_act * C
+        count.zero_()
+        call("avr_march_composite", ptr(z), ptr(f_c), ptr(active), n_act, N, c0, C, float(infinity), float(t_stop),
+             ptr(state), ptr(spare), ptr(count), s)
+        active, spare = spare, active
+        n_act = int(count.item()) if c0 + C < N else 0
+    rgb = torch.empty(R, 3, device=dev, dtype=F32)
+    dist = torch.empty(R, device=dev, dtype=F32)
+    call("avr_march_finish", ptr(state), R, 1 if white_back else 0, ptr(rgb), ptr(dist), s)
+    return rgb, dist, evaluated

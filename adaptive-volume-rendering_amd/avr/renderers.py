@@ -95,6 +95,12 @@ class VolumeRenderer(nn.Module):
         self.seed = None          # None: torch RNG draws (reference order); int: in-kernel Philox
         self._offset = 0
         self.last_path = None     # "fused" | "module" (for tests / introspection)
+        # Early ray termination of the fine pass (BASELINE config 4, not in the
+        # reference): None = evaluate every sample (reference behaviour); a
+        # float T_stop stops a ray once its transmittance drops below it
+        # (inference only; rgb changes by <= T_stop).
+        self.t_stop = None
+        self.last_fine_samples = 0
 
     @classmethod
     def from_conf(cls, conf, white_back=True):
@@ -102,6 +108,27 @@ class VolumeRenderer(nn.Module):
                    n_coarse=conf.get_int("n_coarse", 32), n_fine=conf.get_int("n_fine", 16),
                    n_fine_depth=conf.get_int("n_fine_depth", 8), depth_std=conf.get_float("depth_std", 0.01),
                    white_back=conf.get_float("white_back", white_back))
+
+    def _fine_early_termination(self, ro, rd, z_sorted, radiance_field, fuse, SB, R):
+        """Fine pass with early ray termination at transmittance < self.t_stop
+        (BASELINE config 4, inference only; ops.march_fine)."""
+        Nt = z_sorted.shape[-1]
+        zs = z_sorted.reshape(SB, R, Nt)
+        rgbs, dists, self.last_fine_samples = [], [], 0
+        for b in range(SB):
+            def fn(ro_c, rd_c, z_c, b=b):
+                if fuse:
+                    return radiance_field.fused().forward_rays(ro_c, rd_c, z_c, False, sb=b)
+                pts, vd = ops.points(ro_c, rd_c, z_c)
+                xyz = torch.zeros(SB, pts.shape[0], 3, device=pts.device, dtype=pts.dtype)
+                vds = torch.zeros_like(xyz)
+                xyz[b], vds[b] = pts, vd
+                return radiance_field(xyz, viewdirs=vds, coarse=False)[b]
+            rgb_b, dist_b, n = ops.march_fine(ro[b], rd[b], zs[b], fn, self.t_stop, self.white_back)
+            rgbs.append(rgb_b)
+            dists.append(dist_b)
+            self.last_fine_samples += n
+        return torch.cat(rgbs, 0), torch.cat(dists, 0)
 
     def _draws(self, SB, R, dev, noise):
         """The reference's RNG draws in its order (renderers.py:14, :41, :45, :63)."""
@@ -153,8 +180,12 @@ class VolumeRenderer(nn.Module):
             w_c.detach(), zc, near, far, nf, self.n_fine_depth, self.depth_std,
             u=None if draws is None else draws["u"], u2=None if draws is None else draws["u2"],
             noise_depth=None if draws is None else draws["depth"], seed=seed, offset=off)
-        ff = field(z_sorted, False)
-        rgb_f, dist_f, _ = ops.composite(z_sorted, ff, self.white_back)
+        if self.t_stop is not None and not torch.is_grad_enabled():
+            rgb_f, dist_f = self._fine_early_termination(ro, rd, z_sorted, radiance_field, fuse, SB, R)
+        else:
+            ff = field(z_sorted, False)
+            rgb_f, dist_f, _ = ops.composite(z_sorted, ff, self.white_back)
+            self.last_fine_samples = z_sorted.numel()
         depth = ops.depth_from_world(ro, rd, dist_f.reshape(SB, R), c2w_info)
         assert z_sorted.shape[-1] == Nt
         return rgb_c.reshape(SB, R, 3), rgb_f.reshape(SB, R, 3), depth, depth

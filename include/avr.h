@@ -99,6 +99,25 @@ int avr_composite_bwd(const float* z, const float* field, int64_t n_rays, int n_
                       float infinity, const float* grad_rgb, const float* grad_dist, const float* grad_weights,
                       float* grad_field, void* stream);
 
+/* ----------------------------------------------- fine pass, early termination
+ * BASELINE config 4 (not in the reference; SURVEY §8d "C4 early termination":
+ * stop when T < T_stop, fine pass only). The fine samples z (n_rays, N) are
+ * consumed front to back in chunks [c0, c0 + C) (C <= 64): gather the active
+ * rays' (ro, rd, z chunk), evaluate the field on them, composite the chunk
+ * into the per-ray state (fp64 T and sums, the same terms and T carry as
+ * avr_composite_fwd) and append the rays with T >= t_stop to active_next
+ * (*n_next counts them; zero it first). finish writes rgb (+ 1 - sum w on a
+ * white background) and dist. The skipped tail changes rgb by <= t_stop.
+ * state: opaque, avr_march_state_bytes(n_rays) bytes of device memory.        */
+int avr_march_state_bytes(int64_t n_rays, int64_t* n_bytes);
+int avr_march_init(int64_t n_rays, void* state, int32_t* active, void* stream);
+int avr_march_gather(const float* ro, const float* rd, const float* z, const int32_t* active, int64_t n_act,
+                     int n_samples, int c0, int chunk, float* ro_c, float* rd_c, float* z_c, void* stream);
+int avr_march_composite(const float* z, const float* field_c, const int32_t* active, int64_t n_act,
+                        int n_samples, int c0, int chunk, float infinity, float t_stop, void* state,
+                        int32_t* active_next, int32_t* n_next, void* stream);
+int avr_march_finish(const void* state, int64_t n_rays, int white_back, float* rgb, float* dist, void* stream);
+
 /* ------------------------------------------------------------------- field
  * NewPixelNeRFNet.forward — models.py:739-863 with PositionalEncoding :41-87,
  * SpatialEncoder.index :245-274 (bilinear, border, align_corners=True),

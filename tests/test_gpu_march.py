@@ -1,0 +1,117 @@
+"""Early ray termination of the fine pass (BASELINE config 4; SURVEY §8d
+"C4 early termination: stop when T < T_stop ... the rgb error is <= T_stop",
+not in the reference). Checked against the same renderer without termination
+(whose parity with the reference is pinned in test_gpu_parity.py)."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import build_net, to_np
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def T(a):
+    return torch.as_tensor(np.asarray(a), device=DEV)
+
+
+def _scene(golden, precision, R, seed=7):
+    from oracle import synth
+    g = golden("g4_field_full.npz")
+    net = build_net(g, DEV, precision)
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    x_pix = torch.rand(1, R, 2, generator=gen).to(DEV)
+    c2w = T(synth.orbit_cam2world(0.7)).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
+    K = T(synth.default_intrinsics())[None]
+    return net, x_pix, c2w, K
+
+
+def _render(net, x_pix, c2w, K, t_stop, n_coarse=128, n_fine=64):
+    from avr.renderers import VolumeRenderer
+    rend = VolumeRenderer(0.8, 1.8, n_coarse, n_fine, 0, 0.01, True)
+    rend.seed = 99
+    rend.t_stop = t_stop
+    with torch.no_grad():
+        rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
+    torch.cuda.synchronize()
+    return rgb_c, rgb_f, depth, rend
+
+
+@pytest.mark.parametrize("precision", ["fp32", "x3"])
+def test_termination_off_equals_full_pass(golden, precision):
+    """t_stop = 0 never terminates: the chunked fine pass reproduces the
+    single-launch composite (same terms, same fp64 T carry; only the fp64
+    sum association and the white-background sum order differ)."""
+    net, x_pix, c2w, K = _scene(golden, precision, 4096)
+    _, rgb_a, depth_a, ra = _render(net, x_pix, c2w, K, None)
+    _, rgb_b, depth_b, rb = _render(net, x_pix, c2w, K, 0.0)
+    assert rb.last_fine_samples == ra.last_fine_samples == 4096 * 192
+    np.testing.assert_allclose(to_np(rgb_b), to_np(rgb_a), atol=1e-6, rtol=0)
+    np.testing.assert_allclose(to_np(depth_b), to_np(depth_a), atol=1e-5, rtol=0)
+
+
+@pytest.mark.parametrize("dense", [False, True])
+@pytest.mark.parametrize("t_stop", [1e-5, 1e-2, 0.3])
+def test_termination_error_bound(golden, t_stop, dense):
+    """rgb moves by at most t_stop (the skipped tail's total weight), the
+    distance by at most t_stop * max(zz), and fewer samples are evaluated
+    once rays actually terminate (dense: the fixture field with its sigma
+    output biased up, so rays saturate inside the sample range)."""
+    net, x_pix, c2w, K = _scene(golden, "x3", 8192)
+    if dense:
+        with torch.no_grad():
+            for mlp in (net.mlp_coarse, net.mlp_fine):
+                mlp.lin_out.bias[3] += 30.0
+    rgb_c0, rgb_a, depth_a, ra = _render(net, x_pix, c2w, K, None)
+    rgb_c1, rgb_b, depth_b, rb = _render(net, x_pix, c2w, K, t_stop)
+    np.testing.assert_array_equal(to_np(rgb_c1), to_np(rgb_c0))   # the coarse pass is untouched
+    d_rgb = float((rgb_b - rgb_a).abs().max())
+    assert d_rgb <= t_stop + 2e-6, d_rgb
+    d_depth = float((depth_b - depth_a).abs().max())
+    assert d_depth <= 2.0 * t_stop + 2e-5, d_depth
+    assert rb.last_fine_samples <= ra.last_fine_samples
+    if dense:
+        assert rb.last_fine_samples < ra.last_fine_samples
+
+
+def test_termination_module_path_matches_fused(golden):
+    """The same loop drives a plain nn.Module field (the renderer's module
+    path); with the fp32 field both agree to field rounding."""
+    net, x_pix, c2w, K = _scene(golden, "fp32", 2048)
+
+    class Plain(torch.nn.Module):
+        def __init__(self, inner):
+            super().__init__()
+            self.inner = inner
+
+        def forward(self, xyz, coarse=True, viewdirs=None):
+            return self.inner.forward_torch(xyz, coarse=coarse, viewdirs=viewdirs)
+
+    _, rgb_f, depth_f, rf = _render(net, x_pix, c2w, K, 0.05)
+    _, rgb_m, depth_m, rm = _render(Plain(net), x_pix, c2w, K, 0.05)
+    assert rf.last_path == "fused" and rm.last_path == "module"
+    np.testing.assert_allclose(to_np(rgb_m), to_np(rgb_f), atol=2e-4)
+    np.testing.assert_allclose(to_np(depth_m), to_np(depth_f), atol=2e-4)
+
+
+def test_march_abi_edge_cases():
+    """Zero rays, a single chunk shorter than 64, rays that die in chunk 0."""
+    from avr import ops
+    R, N = 5, 40
+    z = torch.sort(0.8 + torch.rand(R, N, device=DEV), -1)[0]
+    ro = torch.zeros(R, 3, device=DEV)
+    rd = torch.tensor([[0.0, 0.0, 1.0]], device=DEV).expand(R, 3).contiguous()
+    dense = torch.cat([torch.rand(R, N, 3, device=DEV), torch.full((R, N, 1), 1e3, device=DEV)], -1)
+    calls = []
+
+    def fn(ro_c, rd_c, z_c):
+        calls.append(z_c.shape)
+        return dense[: z_c.shape[0], : z_c.shape[1]].reshape(-1, 4)
+
+    rgb, dist, n = ops.march_fine(ro, rd, z, fn, 1e-5, True, chunk=16)
+    assert n == R * 16 and calls == [(R, 16)]   # everything opaque after the first chunk
+    rgb_ref, dist_ref, _ = ops.composite_fwd(z, dense.reshape(R, N, 4).contiguous())
+    np.testing.assert_allclose(to_np(rgb), to_np(rgb_ref), atol=1e-5)
+    rgb0, dist0, n0 = ops.march_fine(ro[:0], rd[:0], z[:0], fn, 1e-5, True)
+    assert n0 == 0 and rgb0.shape == (0, 3) and dist0.shape == (0,)
