@@ -46,29 +46,10 @@ def reference_flops_per_sample(d_in=42, d_latent=512, d_hidden=512, n_blocks=3, 
                 + d_hidden * d_out)
 
 
-def build_scene(device, seed=0):
-    from avr.conf import default_conf
-    from avr.models import NewPixelNeRFNet
-    torch.manual_seed(seed)
-    net = NewPixelNeRFNet(default_conf()["model"])
-    with torch.no_grad():
-        for mlp in (net.mlp_coarse, net.mlp_fine):
-            for blk in mlp.blocks:     # reference zero-inits fc_1 (identity blocks); use N(0, 0.02)
-                blk.fc_1.weight.normal_(0.0, 0.02)
-    net = net.to(device).eval()
-    for p in net.parameters():
-        p.requires_grad_(False)
-    g = torch.Generator(device="cpu").manual_seed(seed + 1)
-    latent = torch.randn(1, 512, 64, 64, generator=g).to(device)
-    net.encoder.set_latent(latent)
-    poses = torch.zeros(1, 3, 4)
-    poses[0, :3, :3] = torch.eye(3)
-    poses[0, 2, 3] = 1.3
-    net.poses = poses.to(device)
-    net.focal = torch.tensor([[131.25, -131.25]], device=device)
-    net.c = torch.tensor([[64.0, 64.0]], device=device)
-    net.image_shape = torch.tensor([128.0, 128.0], device=device)
-    return net
+def build_scene(device, seed=0, sigma_bias=0.0):
+    """avr.scene.synthetic_scene: default.conf field (fc_1 ~ N(0, 0.02)), random 512x64x64 latent."""
+    from avr.scene import synthetic_scene
+    return synthetic_scene(device, seed, sigma_bias=sigma_bias)
 
 
 def orbit_c2w(angle, radius=1.3, z_height=0.4):
@@ -162,6 +143,11 @@ def main():
     ap.add_argument("--precision", choices=["x3", "fp32"], default="x3",
                     help="field MFMA path: split-fp16 (3 products, fp32 accumulate) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", type=int, choices=[3, 4], default=3,
+                    help="BASELINE config: 3 = 65536 random rays (default); 4 = one 800x800 frame per step "
+                         "with fine-pass early termination at T_stop 1e-5")
+    ap.add_argument("--sigma-bias", type=float, default=0.0,
+                    help="density bias of the synthetic field (config 4: opacity of the scene)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -178,16 +164,24 @@ def main():
     from avr.renderers import VolumeRenderer
     avr.load_library()
 
-    net = build_scene(device)
+    net = build_scene(device, sigma_bias=args.sigma_bias)
     net.field_precision = args.precision
     fused = net.fused()
     timer = FieldTimer()
     timer.wrap(fused)
-    R = args.rays
     rend = VolumeRenderer(0.8, 1.8, args.n_coarse, args.n_fine, 0, 0.01, True)
     rend.seed = 1234 + rank
-    g = torch.Generator(device="cpu").manual_seed(100 + rank)
-    x_pix = torch.rand(1, R, 2, generator=g).to(device)
+    if args.config == 4:
+        # one full 800x800 frame per step (get_opencv_pixel_coordinates grid), fine pass with early
+        # termination at T_stop = 1e-5; with N GPUs each rank renders its own frame
+        from avr.video import get_opencv_pixel_coordinates
+        x_pix = get_opencv_pixel_coordinates(800, 800).reshape(1, -1, 2).to(device)
+        R = x_pix.shape[1]
+        rend.t_stop = 1e-5
+    else:
+        R = args.rays
+        g = torch.Generator(device="cpu").manual_seed(100 + rank)
+        x_pix = torch.rand(1, R, 2, generator=g).to(device)
     c2w = orbit_c2w(0.7 + 0.5 * rank).to(device).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
     K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]], device=device)
     gathered = None
@@ -214,8 +208,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    fine_evaluated = 0
     for _ in range(args.steps):
         out = step()
+        fine_evaluated += rend.last_fine_samples
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -255,8 +251,12 @@ def main():
         "dtype": "fp32" if args.precision == "fp32" else "fp32 (field products as 3 fp16 MFMA terms)",
         "data": "synthetic rays (x_pix ~ U[0,1)^2, orbit pose), random-init default.conf field, random 512x64x64 "
                 "latent",
-        "config": {"workload": f"BASELINE config 3: {R} rays/GPU x ({args.n_coarse} coarse + {args.n_fine} fine, "
-                               "n_fine_depth 0), conf/default.conf PixelNeRF field (3x512 ResnetFC, d_latent 512)",
+        "config": {"workload": (f"BASELINE config 3: {R} rays/GPU x ({args.n_coarse} coarse + {args.n_fine} fine, "
+                                "n_fine_depth 0), conf/default.conf PixelNeRF field (3x512 ResnetFC, d_latent 512)")
+                   if args.config == 3 else
+                   (f"BASELINE config 4: 800x800 frame ({R} rays)/GPU x ({args.n_coarse} coarse + {args.n_fine} "
+                    f"fine), fine-pass early termination T_stop 1e-5, sigma bias {args.sigma_bias}, "
+                    "conf/default.conf PixelNeRF field"),
                    "rays_per_gpu": R, "n_coarse": args.n_coarse, "n_fine": args.n_fine,
                    "field_samples_per_ray": samples_per_ray, "parallelism": f"ray-shard x{world} + RCCL gather"},
         "roofline": {
@@ -278,6 +278,9 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as f:
             line["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+    if args.config == 4:
+        line["config"]["fine_samples_evaluated_fraction"] = round(
+            fine_evaluated / (args.steps * R * (args.n_coarse + args.n_fine)), 4)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     if rank == 0:

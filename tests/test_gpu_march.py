@@ -115,3 +115,18 @@ def test_march_abi_edge_cases():
     np.testing.assert_allclose(to_np(rgb), to_np(rgb_ref), atol=1e-5)
     rgb0, dist0, n0 = ops.march_fine(ro[:0], rd[:0], z[:0], fn, 1e-5, True)
     assert n0 == 0 and rgb0.shape == (0, 3) and dist0.shape == (0,)
+
+
+def test_render_cli_small(tmp_path, capsys):
+    """The full-frame CLI (python -m avr.render) on a tiny frame: JSON line,
+    PPM frames, early termination counted."""
+    import json
+    from avr import render
+    render.main(["--frames", "2", "--res", "32", "--n-coarse", "64", "--n-fine", "32", "--t-stop", "1e-5",
+                 "--sigma-bias", "30", "--warmup", "0", "--out", str(tmp_path)])
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line["rays_per_frame"] == 32 * 32 and line["frames"] == 2
+    assert 0 < line["fine_samples_fraction"] < 1.0
+    for i in range(2):
+        data = (tmp_path / f"frame_{i:03d}.ppm").read_bytes()
+        assert data.startswith(b"P6\n32 32\n255\n") and len(data) == len(b"P6\n32 32\n255\n") + 32 * 32 * 3
