@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -53,7 +53,10 @@ _SIGS = {
                         c_void_p, u64, u64, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_composite_fwd": [c_void_p, c_void_p, i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_composite_bwd": [c_void_p, c_void_p, i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
-                          c_void_p],
+                          c_void_p, c_void_p],
+    "avr_sample_coarse_rays": [c_void_p, c_void_p, i64, c_int, c_void_p, u64, u64, c_void_p, c_void_p],
+    "avr_raymarch": [ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_march_state_bytes": [i64, ctypes.POINTER(i64)],
     "avr_march_init": [i64, c_void_p, c_void_p, c_void_p],
     "avr_march_gather": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_int, c_int, c_int, c_void_p, c_void_p,

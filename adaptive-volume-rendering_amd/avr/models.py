@@ -271,7 +271,8 @@ class NewPixelNeRFNet(nn.Module):
 
     def can_fuse(self, xyz):
         from .field import fused_eligible
-        return (self.use_fused and xyz.is_cuda and not (torch.is_grad_enabled() and self._needs_grad())
+        return (self.use_fused and xyz.is_cuda
+                and not (torch.is_grad_enabled() and (self._needs_grad() or xyz.requires_grad))
                 and fused_eligible(self))
 
     def _needs_grad(self):

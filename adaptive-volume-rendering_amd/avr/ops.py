@@ -120,28 +120,30 @@ def composite_fwd(z, field, white_back=True, infinity=1.8, want_weights=True):
     return rgb, dist, w
 
 
-def composite_bwd(z, field, grad_rgb, grad_dist, grad_w, white_back=True, infinity=1.8):
+def composite_bwd(z, field, grad_rgb, grad_dist, grad_w, white_back=True, infinity=1.8, want_grad_z=False):
+    """Gradients of volume_integral: d/d field (R,N,4) and, if want_grad_z, d/dz (R,N)."""
     R, N = z.shape
     grad_rgb = _f32c(grad_rgb.reshape(R, 3))
     grad_dist = None if grad_dist is None else _f32c(grad_dist.reshape(R))
     grad_w = None if grad_w is None else _f32c(grad_w.reshape(R, N))
     require_device(grad_rgb, grad_dist, grad_w)
     gfield = torch.empty(R, N, 4, device=z.device, dtype=F32)
+    gz = torch.empty(R, N, device=z.device, dtype=F32) if want_grad_z else None
     call("avr_composite_bwd", ptr(z), ptr(field), R, N, int(bool(white_back)), float(infinity), ptr(grad_rgb),
-         ptr(grad_dist), ptr(grad_w), ptr(gfield), stream_of(z))
-    return gfield
+         ptr(grad_dist), ptr(grad_w), ptr(gfield), ptr(gz), stream_of(z))
+    return (gfield, gz) if want_grad_z else gfield
 
 
 class _Composite(torch.autograd.Function):
     """Autograd node for volume_integral: gradients flow to (rgb, sigma) of the
-    field output; z carries none (as in VolumeRenderer)."""
+    field output and, when z requires grad (AdaptiveVolumeRenderer's band), to z."""
 
     @staticmethod
     def forward(ctx, z, field, white_back, infinity):
-        z = _f32c(z.detach())
+        zd = _f32c(z.detach())
         field = _f32c(field.detach())
-        rgb, dist, w = composite_fwd(z, field, white_back, infinity, want_weights=True)
-        ctx.save_for_backward(z, field)
+        rgb, dist, w = composite_fwd(zd, field, white_back, infinity, want_weights=True)
+        ctx.save_for_backward(zd, field)
         ctx.white_back, ctx.infinity = white_back, infinity
         return rgb, dist, w
 
@@ -150,13 +152,15 @@ class _Composite(torch.autograd.Function):
         z, field = ctx.saved_tensors
         if g_rgb is None:
             g_rgb = torch.zeros(z.shape[0], 3, device=z.device, dtype=F32)
-        gfield = composite_bwd(z, field, g_rgb, g_dist, g_w, ctx.white_back, ctx.infinity)
-        return None, gfield, None, None
+        want_z = ctx.needs_input_grad[0]
+        out = composite_bwd(z, field, g_rgb, g_dist, g_w, ctx.white_back, ctx.infinity, want_grad_z=want_z)
+        gfield, gz = out if want_z else (out, None)
+        return gz, gfield if ctx.needs_input_grad[1] else None, None, None
 
 
 def composite(z, field, white_back=True, infinity=1.8):
     """Differentiable volume_integral on (R,N) z and (R,N,4) field."""
-    if torch.is_grad_enabled() and field.requires_grad:
+    if torch.is_grad_enabled() and (field.requires_grad or z.requires_grad):
         return _Composite.apply(z, field, white_back, infinity)
     return composite_fwd(z, field, white_back, infinity)
 
@@ -209,3 +213,45 @@ def march_fine(ro, rd, z, field_fn, t_stop, white_back=True, infinity=1.8, chunk
     dist = torch.empty(R, device=dev, dtype=F32)
     call("avr_march_finish", ptr(state), R, 1 if white_back else 0, ptr(rgb), ptr(dist), s)
     return rgb, dist, evaluated
+
+
+def sample_coarse_rays(near, far, n_samples, noise=None, seed=0, offset=0):
+    """sample_coarse with per-ray bounds near/far (R,) -> z (R, n_samples)
+    (renderers.py:4-24 called with tensors, as AdaptiveVolumeRenderer does)."""
+    near, far = _f32c(near.reshape(-1)), _f32c(far.reshape(-1))
+    R = near.shape[0]
+    require_device(near, far)
+    z = torch.empty(R, n_samples, device=near.device, dtype=F32)
+    if noise is not None:
+        noise = _f32c(noise.reshape(R, n_samples))
+    call("avr_sample_coarse_rays", ptr(near), ptr(far), R, n_samples, ptr(noise), int(seed), int(offset), ptr(z),
+         stream_of(z))
+    return z
+
+
+def depth_of_points(world, c2w_info):
+    """depth_from_world(world, cam2world) for explicit world points (SB, R, 3) -> (SB, R)."""
+    c2w, sb_stride, ray_stride = c2w_info
+    SB, R, _ = world.shape
+    world = _f32c(world)
+    depth = torch.empty(SB, R, device=world.device, dtype=F32)
+    call("avr_depth_from_world", ptr(world), None, None, ptr(c2w), sb_stride, ray_stride, SB, R, ptr(depth), None,
+         stream_of(world))
+    return depth
+
+
+def raymarch(view, gate_table, lstm, out_layer, ro, rd, init_dist, steps, trace=False):
+    """LSTM ray march (renderers.py:329-343): ro, rd, init_dist (R,) ->
+    world (R, 3), final_dist (R,) [, trace (steps+1, R, 3)]. gate_table
+    (H*W, 64) = per-texel W_ih projection of the latent."""
+    R = ro.shape[0]
+    ro, rd, d0 = _f32c(ro.reshape(R, 3)), _f32c(rd.reshape(R, 3)), _f32c(init_dist.reshape(R))
+    ps = [_f32c(t.detach()) for t in (gate_table, lstm.weight_hh, lstm.bias_ih, lstm.bias_hh,
+                                      out_layer.weight.reshape(-1), out_layer.bias.reshape(-1))]
+    require_device(ro, rd, d0, *ps)
+    world = torch.empty(R, 3, device=ro.device, dtype=F32)
+    fd = torch.empty(R, device=ro.device, dtype=F32)
+    tr = torch.empty(steps + 1, R, 3, device=ro.device, dtype=F32) if trace else None
+    call("avr_raymarch", ctypes.byref(view), *[ptr(t) for t in ps], ptr(ro), ptr(rd), ptr(d0), R, int(steps),
+         ptr(world), ptr(fd), ptr(tr), stream_of(ro))
+    return (world, fd, tr) if trace else (world, fd)

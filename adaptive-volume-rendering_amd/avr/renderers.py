@@ -36,10 +36,16 @@ def sample_coarse(near_depth, far_depth, num_samples: int, device: torch.device,
     """renderers.py:4-24. near/far (SB, R) -> z (SB, R, num_samples).
     Draws rand_like(z) like the reference unless `noise` is given."""
     SB, R = near_depth.shape
-    near, far = float(near_depth.reshape(-1)[0]), float(far_depth.reshape(-1)[0])
     if noise is None:
         noise = _noise((SB, R, num_samples), near_depth, "rand")
-    z = ops.sample_coarse(near, far, SB * R, num_samples, near_depth.device, noise=noise).reshape(SB, R, num_samples)
+    if torch.is_grad_enabled() and (near_depth.requires_grad or far_depth.requires_grad):
+        # differentiable in near/far (AdaptiveVolumeRenderer's band): the same fp32 ops as renderers.py:10-14
+        span = far_depth - near_depth
+        steps = torch.arange(num_samples, dtype=torch.float32, device=near_depth.device) / num_samples
+        z = (near_depth[..., None] + span[..., None] * steps) + (noise * span[..., None]) / num_samples
+    else:
+        z = ops.sample_coarse_rays(near_depth.expand(SB, R), far_depth.expand(SB, R), num_samples,
+                                   noise=noise).reshape(SB, R, num_samples)
     if infinity != -1:
         z = torch.cat([z[..., 1:], torch.full_like(z[..., :1], float(infinity))], -1)
     return z
@@ -189,3 +195,167 @@ class VolumeRenderer(nn.Module):
         depth = ops.depth_from_world(ro, rd, dist_f.reshape(SB, R), c2w_info)
         assert z_sorted.shape[-1] == Nt
         return rgb_c.reshape(SB, R, 3), rgb_f.reshape(SB, R, 3), depth, depth
+
+
+# ---------------------------------------------------------------- adaptive renderers
+def init_recurrent_weights(self):
+    """utils.py:109-118 (only matches nn.GRU/LSTM/RNN: a no-op on the LSTMCell
+    the renderers use, which keeps torch's default init, as in the reference)."""
+    for m in self.modules():
+        if type(m) in [nn.GRU, nn.LSTM, nn.RNN]:
+            for name, param in m.named_parameters():
+                if "weight_ih" in name:
+                    nn.init.kaiming_normal_(param.data)
+                elif "weight_hh" in name:
+                    nn.init.orthogonal_(param.data)
+                elif "bias" in name:
+                    param.data.fill_(0)
+
+
+def lstm_forget_gate_init(lstm_layer):
+    """utils.py:121-126: forget-gate biases (second quarter) = 1."""
+    for name, parameter in lstm_layer.named_parameters():
+        if "bias" not in name:
+            continue
+        n = parameter.size(0)
+        parameter.data[n // 4:n // 2].fill_(1.0)
+
+
+class _LSTMMarch(nn.Module):
+    """The march shared by Raymarcher and AdaptiveVolumeRenderer
+    (renderers.py:320-343 and :413-432): LSTMCell(num_feature_channels -> 16)
+    on the field's latent features, Linear(16 -> 1) signed distance, x += rd * sd.
+
+    fused: a fusable NewPixelNeRFNet and no gradient -> one HIP kernel for all
+    steps (avr_raymarch) on a per-texel projection of the latent through the
+    LSTM input weights; module: the reference's loop on phi(return_features=True)."""
+
+    def __init__(self, num_feature_channels, raymarch_steps):
+        super().__init__()
+        self.n_feature_channels = num_feature_channels
+        self.steps = raymarch_steps
+        hidden_size = 16
+        self.lstm = nn.LSTMCell(input_size=self.n_feature_channels, hidden_size=hidden_size)
+        self.lstm.apply(init_recurrent_weights)
+        lstm_forget_gate_init(self.lstm)
+        self.out_layer = nn.Linear(hidden_size, 1)
+        self.counter = 0
+        self._gate_cache = None
+        self.last_path = None
+
+    def _initial_distance(self, SB, num_rays, device, noise):
+        if noise is not None and "initial_distance" in noise:
+            return noise["initial_distance"].reshape(SB, num_rays, 1).to(device)
+        # renderers.py:322 / :402: drawn on the CPU generator, then moved
+        return torch.zeros((SB, num_rays, 1)).normal_(mean=0.8, std=5e-2).to(device)
+
+    def _gate_table(self, phi):
+        lat = phi.encoder.latent
+        w = self.lstm.weight_ih
+        key = (lat.data_ptr(), lat._version, tuple(lat.shape), w.data_ptr(), w._version)
+        if self._gate_cache is not None and self._gate_cache[0] == key:
+            return self._gate_cache[1]
+        C = lat.shape[1]
+        # (H*W, C) @ (C, 64): the LSTM input projection of every latent texel (a plain library GEMM)
+        table = torch.matmul(lat[0].detach().reshape(C, -1).t().float(), w.detach().t().float()).contiguous()
+        self._gate_cache = (key, table, lat, w)
+        return table
+
+    def can_fuse(self, phi, ros):
+        return (ros.shape[0] == 1 and not torch.is_grad_enabled() and hasattr(phi, "can_fuse")
+                and phi.can_fuse(ros) and phi.encoder.latent.shape[1] == self.n_feature_channels)
+
+    def march(self, ros, rds, init_dist, phi):
+        """-> final world coordinates (SB, R, 3)."""
+        SB, num_rays, _ = ros.shape
+        if self.can_fuse(phi, ros):
+            self.last_path = "fused"
+            world, _ = ops.raymarch(phi.fused().view(0), self._gate_table(phi), self.lstm, self.out_layer,
+                                    ros[0], rds[0], init_dist[0, :, 0], self.steps)
+            return world.reshape(SB, num_rays, 3)
+        self.last_path = "module"
+        world_coords = [ros + rds * init_dist]
+        states = [None]
+        for _ in range(self.steps):
+            v = phi(world_coords[-1].reshape(SB, -1, 3), viewdirs=rds.reshape(SB, -1, 3), return_features=True)
+            state = self.lstm(v.reshape(-1, self.n_feature_channels), states[-1])
+            if state[0].requires_grad:
+                state[0].register_hook(lambda x: x.clamp(min=-10, max=10))
+            signed_distance = self.out_layer(state[0]).view(SB, num_rays, 1)
+            world_coords.append(world_coords[-1] + rds * signed_distance)
+            states.append(state)
+        return world_coords[-1]
+
+
+class Raymarcher(_LSTMMarch):
+    """renderers.py:290-358: LSTM march, then the coarse field at the final
+    point -> (rgb, None, depth, depth)."""
+
+    def __init__(self, num_feature_channels, raymarch_steps):
+        super().__init__(num_feature_channels, raymarch_steps)
+
+    def forward(self, cam2world, intrinsics, xy_pix, phi, noise=None):
+        SB, num_rays, _ = xy_pix.shape
+        ros, rds, c2w_info = ops.world_rays(xy_pix, intrinsics, cam2world)
+        init = self._initial_distance(SB, num_rays, xy_pix.device, noise)
+        world = self.march(ros, rds, init, phi)
+        self.counter += 1
+        output = phi(world.reshape(SB, -1, 3), viewdirs=rds.reshape(SB, -1, 3), coarse=True, return_features=False)
+        rgb = output[..., :3].reshape(SB, num_rays, 3)
+        final_depth = ops.depth_of_points(world, c2w_info).reshape(SB, num_rays, -1)
+        return rgb, None, final_depth, final_depth
+
+    @classmethod
+    def from_conf(cls, conf, raymarch_steps):
+        return cls(num_feature_channels=conf.get_int("num_feature_channels", 512), raymarch_steps=raymarch_steps)
+
+
+class AdaptiveVolumeRenderer(_LSTMMarch):
+    """renderers.py:360-557: LSTM march to a surface estimate, the coarse field
+    at it, then n_coarse stratified samples in [d - epsilon, d + epsilon]
+    (d = (x - ro)_x / rd_x, quirk kept), the fine field on them, volume
+    integral and depth -> (rgb_coarse, rgb, depth_coarse, depth_map)."""
+
+    def __init__(self, num_feature_channels, raymarch_steps, epsilon, n_coarse, white_back):
+        super().__init__(num_feature_channels, raymarch_steps)
+        self.epsilon = epsilon
+        self.n_coarse = n_coarse
+        self.white_back = white_back
+
+    def forward(self, cam2world, intrinsics, xy_pix, phi, debug=False, noise=None):
+        SB, num_rays, _ = xy_pix.shape
+        dev = xy_pix.device
+        ros, rds, c2w_info = ops.world_rays(xy_pix, intrinsics, cam2world)
+        init = self._initial_distance(SB, num_rays, dev, noise)
+        world = self.march(ros, rds, init, phi)
+        # coarse image at the marched point
+        output_coarse = phi(world.reshape(SB, -1, 3), viewdirs=rds.reshape(SB, -1, 3), coarse=True,
+                            return_features=False)
+        rgb_coarse = output_coarse[..., :3].reshape(SB, num_rays, 3)
+        depth_coarse = ops.depth_of_points(world, c2w_info).reshape(SB, num_rays, -1)
+        # band around the marched distance (renderers.py:490-496); the sort is a no-op on stratified z
+        final_distance = (world[..., 0] - ros[..., 0]) / rds[..., 0]
+        u = None if noise is None else noise.get("band")
+        z_vals = sample_coarse(final_distance - self.epsilon, final_distance + self.epsilon, self.n_coarse, dev,
+                               noise=u)
+        z_vals_sorted, _ = torch.sort(z_vals, dim=-1)
+        fuse = (SB == 1 and not torch.is_grad_enabled() and hasattr(phi, "can_fuse") and phi.can_fuse(xy_pix))
+        if fuse:
+            field = phi.fused().forward_rays(ros[0], rds[0], z_vals_sorted[0], False).reshape(SB, num_rays,
+                                                                                               self.n_coarse, 4)
+        else:
+            pts, vd = ops.points(ros.reshape(-1, 3), rds.reshape(-1, 3), z_vals_sorted.reshape(-1, self.n_coarse))
+            if z_vals_sorted.requires_grad:   # gradient to the band through the sample points
+                pts = ros.unsqueeze(-2) + rds.unsqueeze(-2) * z_vals_sorted.unsqueeze(-1)
+            field = phi(pts.reshape(SB, -1, 3), coarse=False, viewdirs=vd.reshape(SB, -1, 3),
+                        return_features=False).reshape(SB, num_rays, self.n_coarse, 4)
+        rgb, distance_map, _ = volume_integral(z_vals_sorted, field[..., 3:], field[..., :3],
+                                               white_back=self.white_back)
+        depth_map = ops.depth_from_world(ros, rds, distance_map.reshape(SB, num_rays), c2w_info)
+        return rgb_coarse, rgb, depth_coarse, depth_map
+
+    @classmethod
+    def from_conf(cls, conf, white_back=False):
+        return cls(num_feature_channels=conf.get_int("num_feature_channels", 512),
+                   raymarch_steps=conf.get_int("raymarch_steps", 10), epsilon=conf.get_float("epsilon", 0.05),
+                   n_coarse=conf.get_int("n_coarse", 20), white_back=conf.get_float("white_back", white_back))

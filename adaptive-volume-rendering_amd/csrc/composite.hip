@@ -119,13 +119,17 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(const float* __restr
 // S_n    = sum_{m>n} g_w_m w_m
 // dL/da_n = g_w_n T_n - S_n / t_n           (cumprod backward, no zero inputs: t >= 1e-10)
 // dL/dsigma_n = dL/da_n * exp(-sigma_n d_n) * d_n
+// z (AdaptiveVolumeRenderer trains its band through it): d_n = z_{n+1} - z_n
+// (n < N-1), zz_n = z_{n+1}; with gd_n = dL/da_n * exp(-sigma_n d_n) * sigma_n,
+// dL/dz_m = [m >= 1] (gd_{m-1} + Gd w_{m-1}) - [m <= N-2] gd_m.
 __global__ void __launch_bounds__(256) composite_bwd_kernel(const float* __restrict__ z,
                                                             const float4* __restrict__ field, int64_t n_rays, int N,
                                                             int white_back, float infinity,
                                                             const float* __restrict__ grad_rgb,
                                                             const float* __restrict__ grad_dist,
                                                             const float* __restrict__ grad_w,
-                                                            float4* __restrict__ grad_field) {
+                                                            float4* __restrict__ grad_field,
+                                                            float* __restrict__ grad_z) {
   extern __shared__ double dsm[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t ray = (int64_t)blockIdx.x * kCompWaves + wid;
@@ -162,19 +166,31 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(const float* __restr
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const double Q = carryQ;
+  double carryZ = 0.0;   // gd + Gd w of the previous round's last sample
   for (int base = 0; base < N; base += 64) {
     const int n = base + lane;
-    if (n >= N) break;
-    const float4 f = fr[n];
-    const SampleTerms s = sample_terms(zr, n, N, f.w, infinity);
-    const float T = Tbuf[n];
-    const float w = fmul(s.alpha, T);
-    const double gw = (double)G0 * f.x + (double)G1 * f.y + (double)G2 * f.z + (double)Gd * s.zz - (double)Gbg +
-                      (grad_w ? (double)grad_w[ray * N + n] : 0.0);
-    const double S = Q - qpre[n];
-    const double ga = gw * (double)T - S / (double)s.t;
-    const double gs = ga * (double)s.e * (double)s.d;
-    grad_field[ray * N + n] = make_float4(fmul(G0, w), fmul(G1, w), fmul(G2, w), (float)gs);
+    const bool ok = n < N;
+    double vz = 0.0, gd = 0.0;
+    if (ok) {
+      const float4 f = fr[n];
+      const SampleTerms s = sample_terms(zr, n, N, f.w, infinity);
+      const float T = Tbuf[n];
+      const float w = fmul(s.alpha, T);
+      const double gw = (double)G0 * f.x + (double)G1 * f.y + (double)G2 * f.z + (double)Gd * s.zz - (double)Gbg +
+                        (grad_w ? (double)grad_w[ray * N + n] : 0.0);
+      const double S = Q - qpre[n];
+      const double ga = gw * (double)T - S / (double)s.t;
+      const double gs = ga * (double)s.e * (double)s.d;
+      grad_field[ray * N + n] = make_float4(fmul(G0, w), fmul(G1, w), fmul(G2, w), (float)gs);
+      if (n < N - 1) gd = ga * (double)s.e * (double)f.w;
+      vz = gd + (n < N - 1 ? (double)Gd * w : 0.0);
+    }
+    if (grad_z) {   // wave-uniform
+      double prev = __shfl_up(vz, 1, 64);
+      if (lane == 0) prev = carryZ;
+      carryZ = __shfl(vz, 63, 64);
+      if (ok) grad_z[ray * N + n] = (float)((n >= 1 ? prev : 0.0) - gd);
+    }
   }
 }
 
@@ -196,7 +212,7 @@ extern "C" int avr_composite_fwd(const float* z, const float* field, int64_t n_r
 
 extern "C" int avr_composite_bwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
                                  float infinity, const float* grad_rgb, const float* grad_dist,
-                                 const float* grad_weights, float* grad_field, void* stream) {
+                                 const float* grad_weights, float* grad_field, float* grad_z, void* stream) {
   AVR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples <= 1024, "avr_composite_bwd: n_samples must be in [1,1024]");
   if (n_rays == 0) return AVR_OK;
   AVR_REQUIRE(z && field && grad_rgb && grad_field, "avr_composite_bwd: null pointer");
@@ -204,6 +220,6 @@ extern "C" int avr_composite_bwd(const float* z, const float* field, int64_t n_r
   const unsigned grid = (unsigned)((n_rays + kCompWaves - 1) / kCompWaves);
   composite_bwd_kernel<<<grid, 64 * kCompWaves, shm, as_stream(stream)>>>(
       z, reinterpret_cast<const float4*>(field), n_rays, n_samples, white_back, infinity, grad_rgb, grad_dist,
-      grad_weights, reinterpret_cast<float4*>(grad_field));
+      grad_weights, reinterpret_cast<float4*>(grad_field), grad_z);
   return check_launch("composite_bwd_kernel");
 }

@@ -356,17 +356,7 @@ static int field_common(const avr_field_dims* dims, const avr_view_desc* view, c
   a->table = table;
   a->table_stride = (int64_t)view->latent_h * view->latent_w * dims->d_hidden;
   a->L = L;
-  for (int i = 0; i < 3; ++i) {
-    for (int k = 0; k < 3; ++k) a->v.R[3 * i + k] = view->poses[4 * i + k];
-    a->v.t[i] = view->poses[4 * i + 3];
-  }
-  for (int i = 0; i < 2; ++i) {
-    a->v.focal[i] = view->focal[i];
-    a->v.c[i] = view->c[i];
-    a->v.scale[i] = view->latent_scaling[i] / view->image_shape[i];  // models.py:263 (fp32 div)
-  }
-  a->v.H = view->latent_h;
-  a->v.W = view->latent_w;
+  view_from_desc(view, &a->v);
   a->n_blocks = dims->n_blocks;
   a->n_lin_z = dims->n_lin_z;
   a->num_freqs = dims->num_freqs;

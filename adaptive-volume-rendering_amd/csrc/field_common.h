@@ -37,6 +37,21 @@ struct View {
   int H, W;
 };
 
+// Source view for the latent lookup (poses = world->camera [R | t], models.py:719-727).
+inline void view_from_desc(const avr_view_desc* d, View* v) {
+  for (int i = 0; i < 3; ++i) {
+    for (int k = 0; k < 3; ++k) v->R[3 * i + k] = d->poses[4 * i + k];
+    v->t[i] = d->poses[4 * i + 3];
+  }
+  for (int i = 0; i < 2; ++i) {
+    v->focal[i] = d->focal[i];
+    v->c[i] = d->c[i];
+    v->scale[i] = d->latent_scaling[i] / d->image_shape[i];  // models.py:263 (fp32 div)
+  }
+  v->H = d->latent_h;
+  v->W = d->latent_w;
+}
+
 struct FieldArgs {
   const float* packed;
   const float* table;
@@ -96,6 +111,31 @@ struct SampleGeom {
   Bilinear bl;
 };
 
+// Rotated point xr = R x -> bilinear corners/weights of the source-view latent:
+// camera point xr + t, pinhole uv, uv * scale - 1, then grid_sample bilinear /
+// border / align_corners=True (models.py:753-760, SpatialEncoder.index :260-273).
+__device__ __forceinline__ Bilinear bilinear_from_rot(const View& v, const float* xr_in) {
+  Bilinear bl;
+  const float xc0 = fadd(xr_in[0], v.t[0]), xc1 = fadd(xr_in[1], v.t[1]), xc2 = fadd(xr_in[2], v.t[2]);
+  const float u = fadd(fmul(fdiv(-xc0, xc2), v.focal[0]), v.c[0]);
+  const float w = fadd(fmul(fdiv(-xc1, xc2), v.focal[1]), v.c[1]);
+  const float gx = fsub(fmul(u, v.scale[0]), 1.0f), gy = fsub(fmul(w, v.scale[1]), 1.0f);
+  float ix = fmul(fdiv(fadd(gx, 1.0f), 2.0f), (float)(v.W - 1));
+  float iy = fmul(fdiv(fadd(gy, 1.0f), 2.0f), (float)(v.H - 1));
+  ix = fminf(fmaxf(ix, 0.f), (float)(v.W - 1));
+  iy = fminf(fmaxf(iy, 0.f), (float)(v.H - 1));
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const float wx1 = fsub(ix, fx0), wy1 = fsub(iy, fy0);
+  const float wx0 = fsub(fadd(fx0, 1.0f), ix), wy0 = fsub(fadd(fy0, 1.0f), iy);
+  const int X0 = (int)fx0, Y0 = (int)fy0;
+  const int X1 = X0 + 1 < v.W ? X0 + 1 : v.W - 1, Y1 = Y0 + 1 < v.H ? Y0 + 1 : v.H - 1;
+  bl.tex[0] = Y0 * v.W + X0; bl.w[0] = fmul(wx0, wy0);
+  bl.tex[1] = Y0 * v.W + X1; bl.w[1] = fmul(wx1, wy0);
+  bl.tex[2] = Y1 * v.W + X0; bl.w[2] = fmul(wx0, wy1);
+  bl.tex[3] = Y1 * v.W + X1; bl.w[3] = fmul(wx1, wy1);
+  return bl;
+}
+
 __device__ __forceinline__ SampleGeom sample_geom(const FieldArgs& a, int64_t mm) {
   float x0, x1, x2, d0, d1, d2;
   if (a.z) {
@@ -113,24 +153,14 @@ __device__ __forceinline__ SampleGeom sample_geom(const FieldArgs& a, int64_t mm
   SampleGeom s;
   s.xr[0] = dot3(v.R + 0, x0, x1, x2); s.xr[1] = dot3(v.R + 3, x0, x1, x2); s.xr[2] = dot3(v.R + 6, x0, x1, x2);
   s.vr[0] = dot3(v.R + 0, d0, d1, d2); s.vr[1] = dot3(v.R + 3, d0, d1, d2); s.vr[2] = dot3(v.R + 6, d0, d1, d2);
-  const float xc0 = fadd(s.xr[0], v.t[0]), xc1 = fadd(s.xr[1], v.t[1]), xc2 = fadd(s.xr[2], v.t[2]);
-  const float u = fadd(fmul(fdiv(-xc0, xc2), v.focal[0]), v.c[0]);
-  const float w = fadd(fmul(fdiv(-xc1, xc2), v.focal[1]), v.c[1]);
-  const float gx = fsub(fmul(u, v.scale[0]), 1.0f), gy = fsub(fmul(w, v.scale[1]), 1.0f);
-  float ix = fmul(fdiv(fadd(gx, 1.0f), 2.0f), (float)(v.W - 1));
-  float iy = fmul(fdiv(fadd(gy, 1.0f), 2.0f), (float)(v.H - 1));
-  ix = fminf(fmaxf(ix, 0.f), (float)(v.W - 1));
-  iy = fminf(fmaxf(iy, 0.f), (float)(v.H - 1));
-  const float fx0 = floorf(ix), fy0 = floorf(iy);
-  const float wx1 = fsub(ix, fx0), wy1 = fsub(iy, fy0);
-  const float wx0 = fsub(fadd(fx0, 1.0f), ix), wy0 = fsub(fadd(fy0, 1.0f), iy);
-  const int X0 = (int)fx0, Y0 = (int)fy0;
-  const int X1 = X0 + 1 < v.W ? X0 + 1 : v.W - 1, Y1 = Y0 + 1 < v.H ? Y0 + 1 : v.H - 1;
-  s.bl.tex[0] = Y0 * v.W + X0; s.bl.w[0] = fmul(wx0, wy0);
-  s.bl.tex[1] = Y0 * v.W + X1; s.bl.w[1] = fmul(wx1, wy0);
-  s.bl.tex[2] = Y1 * v.W + X0; s.bl.w[2] = fmul(wx0, wy1);
-  s.bl.tex[3] = Y1 * v.W + X1; s.bl.w[3] = fmul(wx1, wy1);
+  s.bl = bilinear_from_rot(v, s.xr);
   return s;
+}
+
+// World point -> bilinear corners of the source-view latent (models.py:753-760, :260-273).
+__device__ __forceinline__ Bilinear bilinear_at(const View& v, float x0, float x1, float x2) {
+  const float xr[3] = {dot3(v.R + 0, x0, x1, x2), dot3(v.R + 3, x0, x1, x2), dot3(v.R + 6, x0, x1, x2)};
+  return bilinear_from_rot(v, xr);
 }
 
 // Feature k of z_feature (models.py:763-789): [xyz_rot (3), PE (6*num_freqs),

@@ -95,15 +95,21 @@ __global__ void __launch_bounds__(256) depth_kernel(const float* __restrict__ ro
 #pragma unroll
     for (int q = 0; q < 4; ++q) a[p][q] = (double)T[4 * p + q];
   invert<4>(a, inv);
-  const float d = dist[i];
   double z = inv[2][3];
+  if (rd) {
+    const float d = dist[i];
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const float w = fadd(ro[3 * i + q], fmul(rd[3 * i + q], d));  // ros + rds * dist (renderers.py:274)
-    z += inv[2][q] * (double)w;
+    for (int q = 0; q < 3; ++q) {
+      const float w = fadd(ro[3 * i + q], fmul(rd[3 * i + q], d));  // ros + rds * dist (renderers.py:274)
+      z += inv[2][q] * (double)w;
+    }
+  } else {  // ro holds world points (renderers.py:346, :459: depth of the raymarcher's final coords)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) z += inv[2][q] * (double)ro[3 * i + q];
   }
   depth[i] = (float)(-z);
-  if (ddepth) ddepth[i] = (float)(-(inv[2][0] * rd[3 * i] + inv[2][1] * rd[3 * i + 1] + inv[2][2] * rd[3 * i + 2]));
+  if (ddepth && rd)
+    ddepth[i] = (float)(-(inv[2][0] * rd[3 * i] + inv[2][1] * rd[3 * i + 1] + inv[2][2] * rd[3 * i + 2]));
 }
 
 }  // namespace avr
@@ -128,7 +134,7 @@ extern "C" int avr_depth_from_world(const float* ro, const float* rd, const floa
   AVR_REQUIRE(n_sb >= 0 && n_rays >= 0, "avr_depth_from_world: negative size");
   const int64_t n = n_sb * n_rays;
   if (n == 0) return AVR_OK;
-  AVR_REQUIRE(ro && rd && dist && c2w && depth, "avr_depth_from_world: null pointer");
+  AVR_REQUIRE(ro && (!rd || dist) && c2w && depth, "avr_depth_from_world: null pointer");
   depth_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(ro, rd, dist, c2w, c2w_sb_stride,
                                                                            c2w_ray_stride, n_sb, n_rays, depth,
                                                                            ddepth_ddist);

@@ -31,6 +31,24 @@ __global__ void __launch_bounds__(256) sample_coarse_kernel(float near_, float f
   z[i] = fadd(fadd(near_, fmul(span, step)), fdiv(fmul(u, span), (float)n));
 }
 
+// sample_coarse with per-ray bounds (AdaptiveVolumeRenderer's band around the
+// raymarched distance, renderers.py:492-493: near = d - eps, far = d + eps).
+__global__ void __launch_bounds__(256) sample_coarse_rays_kernel(const float* __restrict__ near_,
+                                                                 const float* __restrict__ far_, int64_t n_rays,
+                                                                 int n, const float* __restrict__ noise,
+                                                                 uint64_t seed, uint64_t offset,
+                                                                 float* __restrict__ z) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rays * n) return;
+  const int64_t r = i / n;
+  const int s = (int)(i - r * n);
+  const float nr = near_[r];
+  const float span = fsub(far_[r], nr);
+  const float step = fdiv((float)s, (float)n);
+  const float u = noise ? noise[i] : philox_uniform(seed, offset + (uint64_t)r, (uint32_t)s, kStreamCoarse);
+  z[i] = fadd(fadd(nr, fmul(span, step)), fdiv(fmul(u, span), (float)n));
+}
+
 // torch-CPU fp32 row sum (ATen vectorised reduction): four 8-lane accumulators
 // over full groups of four 8-vectors, leftover vectors into accumulator 0,
 // ((a0+a1)+a2)+a3, then the scalar tail, then the 8 lanes in order.
@@ -167,6 +185,18 @@ extern "C" int avr_sample_coarse(float near_, float far_, int64_t n_rays, int n_
   sample_coarse_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(near_, far_, n_rays, n_samples,
                                                                                  noise, seed, offset, z);
   return check_launch("sample_coarse_kernel");
+}
+
+extern "C" int avr_sample_coarse_rays(const float* near_, const float* far_, int64_t n_rays, int n_samples,
+                                      const float* noise, uint64_t seed, uint64_t offset, float* z, void* stream) {
+  AVR_REQUIRE(n_rays >= 0 && n_samples > 0, "avr_sample_coarse_rays: bad sizes");
+  const int64_t n = n_rays * n_samples;
+  if (n == 0) return AVR_OK;
+  AVR_REQUIRE(near_ && far_ && z, "avr_sample_coarse_rays: null pointer");
+  sample_coarse_rays_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(near_, far_, n_rays,
+                                                                                       n_samples, noise, seed,
+                                                                                       offset, z);
+  return check_launch("sample_coarse_rays_kernel");
 }
 
 extern "C" int avr_sample_fine(const float* weights, const float* z_coarse, float near_, float far_, int64_t n_rays,

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 1
+#define AVR_ABI_VERSION 2
 #define AVR_MAX_BLOCKS 8
 
 enum {
@@ -54,7 +54,9 @@ int avr_world_rays(const float* x_pix, const float* K, const float* c2w, int64_t
 /* depth_from_world(ro + rd*dist, c2w) — renderers.py:274-275, utils.py:358-361
  * (transform_world2cam :270-281, a general 4x4 inverse per ray).
  *   dist (n_sb, n_rays) -> depth (n_sb, n_rays)
- *   ddepth_ddist (n_sb, n_rays) or NULL: d depth / d dist, for autograd.        */
+ *   ddepth_ddist (n_sb, n_rays) or NULL: d depth / d dist, for autograd.
+ *   rd = NULL: ro holds world points (dist unused) — depth_from_world of the
+ *   raymarcher's final coordinates (renderers.py:346, :459).                   */
 int avr_depth_from_world(const float* ro, const float* rd, const float* dist, const float* c2w,
                          int64_t c2w_sb_stride, int64_t c2w_ray_stride, int64_t n_sb, int64_t n_rays,
                          float* depth, float* ddepth_ddist, void* stream);
@@ -66,6 +68,11 @@ int avr_depth_from_world(const float* ro, const float* rd, const float* dist, co
  *   keyed on (seed, offset + ray, sample).                                     */
 int avr_sample_coarse(float near_, float far_, int64_t n_rays, int n_samples, const float* noise,
                       uint64_t seed, uint64_t offset, float* z, void* stream);
+
+/* sample_coarse with per-ray near/far (n_rays) — AdaptiveVolumeRenderer's band
+ * around the raymarched distance (renderers.py:492-493).                        */
+int avr_sample_coarse_rays(const float* near_, const float* far_, int64_t n_rays, int n_samples,
+                           const float* noise, uint64_t seed, uint64_t offset, float* z, void* stream);
 
 /* sample_fine + sample_depth + clamp + sort(cat(...)) — renderers.py:27-54,
  * :56-66, :252-258.
@@ -91,13 +98,14 @@ int avr_sample_fine(const float* weights, const float* z_coarse, float near_, fl
 int avr_composite_fwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
                       float infinity, float* rgb, float* dist, float* weights, void* stream);
 
-/* Gradient of volume_integral w.r.t. (r, g, b, sigma) (autograd of
- * renderers.py:78-112; z carries no gradient in VolumeRenderer).
+/* Gradient of volume_integral (autograd of renderers.py:78-112).
  *   grad_rgb (n_rays,3), grad_dist (n_rays) or NULL, grad_weights (n_rays,N)
- *   or NULL -> grad_field (n_rays, N, 4).                                      */
+ *   or NULL -> grad_field (n_rays, N, 4) = d/d(r, g, b, sigma), and grad_z
+ *   (n_rays, N) or NULL = d/dz (VolumeRenderer's z carries no gradient;
+ *   AdaptiveVolumeRenderer's band does, renderers.py:492-508).               */
 int avr_composite_bwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
                       float infinity, const float* grad_rgb, const float* grad_dist, const float* grad_weights,
-                      float* grad_field, void* stream);
+                      float* grad_field, float* grad_z, void* stream);
 
 /* ----------------------------------------------- fine pass, early termination
  * BASELINE config 4 (not in the reference; SURVEY §8d "C4 early termination":
@@ -181,6 +189,21 @@ int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_desc* view, co
 int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
                          const float* table, const float* xyz, const float* viewdirs, int64_t n_points,
                          float* out, void* stream);
+
+/* --------------------------------------------------------- LSTM ray marcher
+ * Raymarcher / AdaptiveVolumeRenderer march (renderers.py:313-351, :380-432):
+ * x = ro + rd * init_dist, then `steps` x { v = latent features at x
+ * (bilinear, models.py:753-823), (h, c) = LSTMCell(v, (h, c)) with hidden 16,
+ * sd = out_layer(h), x += rd * sd }; world (n_rays, 3) = final x, final_dist
+ * (n_rays) or NULL = (x - ro)_x / rd_x (renderers.py:490, quirk kept), trace
+ * ((steps + 1), n_rays, 3) or NULL = every x. gate_table (H*W, 64) =
+ * latent (C, H*W)^T . weight_ih^T (C = feature channels), the input projection
+ * per texel; w_hh (64, 16), b_ih / b_hh (64), w_out (16), b_out (1) are the
+ * LSTMCell / Linear parameters in torch layout.                               */
+int avr_raymarch(const avr_view_desc* view, const float* gate_table, const float* w_hh, const float* b_ih,
+                 const float* b_hh, const float* w_out, const float* b_out, const float* ro, const float* rd,
+                 const float* init_dist, int64_t n_rays, int steps, float* world, float* final_dist, float* trace,
+                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -292,3 +292,66 @@ def render(cam2world, intrinsics, x_pix, field, near, far, n_coarse, n_fine, n_f
                    z_sorted=zs, field_fine=ff, dist_fine=dist_f, ro=ro, rd=rd)
         return rgb_c, rgb_f, depth, depth, aux
     return rgb_c, rgb_f, depth, depth
+
+
+# ----------------------------------------------------------------------------- adaptive renderer
+def _sigmoid(x):
+    return (1.0 / (1.0 + np.exp(-x.astype(np.float64)))).astype(F32)
+
+
+def lstm_cell(x, h, c, w_ih, w_hh, b_ih, b_hh):
+    """torch.nn.LSTMCell: gates = x W_ih^T + b_ih + h W_hh^T + b_hh, order i f g o."""
+    x = np.asarray(x, F32)
+    gates = ((x @ np.asarray(w_ih, F32).T).astype(F32) + b_ih) + ((h @ np.asarray(w_hh, F32).T).astype(F32) + b_hh)
+    H = h.shape[-1]
+    i, f, g, o = (gates[:, k * H:(k + 1) * H] for k in range(4))
+    i, f, o = _sigmoid(i), _sigmoid(f), _sigmoid(o)
+    g = np.tanh(g.astype(np.float64)).astype(F32)
+    c2 = (f * c + i * g).astype(F32)
+    h2 = (o * np.tanh(c2.astype(np.float64)).astype(F32)).astype(F32)
+    return h2, c2
+
+
+def raymarch(ro, rd, init_dist, field, lstm, out_w, out_b, steps):
+    """The LSTM march of Raymarcher / AdaptiveVolumeRenderer (renderers.py:320-343,
+    :404-432): x = ro + rd d0; steps x {v = latent at x (return_features=True,
+    models.py:822-823); (h, c) = LSTMCell(v); sd = out_layer(h); x += rd sd}.
+    ro, rd (R,3), init_dist (R,1); lstm = (w_ih, w_hh, b_ih, b_hh).
+    Returns the list of x per step (steps + 1 entries)."""
+    R = ro.shape[0]
+    x = (ro + rd * init_dist).astype(F32)
+    h = np.zeros((R, 16), F32)
+    c = np.zeros((R, 16), F32)
+    trace = [x]
+    for _ in range(steps):
+        v, _ = field.features(x, rd)
+        h, c = lstm_cell(v, h, c, *lstm)
+        sd = ((h @ np.asarray(out_w, F32).reshape(1, 16).T).astype(F32) + np.asarray(out_b, F32)).astype(F32)
+        x = (x + rd * sd).astype(F32)
+        trace.append(x)
+    return trace
+
+
+def adaptive_render(cam2world, intrinsics, x_pix, field, lstm, out_w, out_b, steps, epsilon, n_coarse, white_back,
+                    init_dist, band_noise):
+    """AdaptiveVolumeRenderer.forward (renderers.py:380-547) with explicit noise:
+    init_dist (SB,R,1) ~ N(0.8, 0.05) and the band's rand_like (SB,R,n_coarse).
+    Returns (rgb_coarse, rgb, depth_coarse (SB,R,1), depth_map (SB,R), trace)."""
+    x_pix = np.asarray(x_pix, F32)
+    SB, R, _ = x_pix.shape
+    assert SB == 1
+    ro, rd = get_world_rays(x_pix, intrinsics, cam2world)
+    trace = raymarch(ro[0], rd[0], np.asarray(init_dist, F32)[0], field, lstm, out_w, out_b, steps)
+    world = trace[-1][None]
+    out_c = field(world, rd, coarse=True)
+    rgb_coarse = out_c[..., :3]
+    depth_coarse = depth_from_world(world, cam2world)[..., None]
+    fd = ((world[..., 0] - ro[..., 0]) / rd[..., 0]).astype(F32)
+    z = sample_coarse((fd - F32(epsilon)).astype(F32), (fd + F32(epsilon)).astype(F32), n_coarse, band_noise)
+    z = np.sort(z, -1)
+    pts = ro[..., None, :] + rd[..., None, :] * z[..., None]
+    vd = np.broadcast_to(rd[..., None, :], pts.shape)
+    f = field(pts.reshape(SB, -1, 3), vd.reshape(SB, -1, 3), coarse=False).reshape(SB, R, n_coarse, 4)
+    rgb, dist, _ = volume_integral(z, f[..., 3:4], f[..., :3], white_back)
+    depth_map = depth_from_world(ro + rd * dist, cam2world)
+    return rgb_coarse, rgb, depth_coarse, depth_map, trace

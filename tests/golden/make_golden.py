@@ -355,6 +355,40 @@ def g5_forward(R):
         assert depth2 is depth
 
 
+def g6_adaptive(R):
+    """AdaptiveVolumeRenderer.forward (renderers.py:380-547) on the small field
+    (d_latent 64 -> num_feature_channels 64): LSTM parameters, the N(0.8, 0.05)
+    initial distances, the band's rand_like, every point the LSTM queried, and
+    the four outputs."""
+    net, meta, params = build_field(REF_M, 64, 3, 1000, 1, (8, 8), 40, True)
+    torch.manual_seed(77)
+    avr = REF_R.AdaptiveVolumeRenderer(num_feature_channels=64, raymarch_steps=10, epsilon=0.05, n_coarse=20,
+                                       white_back=True)
+    x_pix = synth.hashed_uniform((1, R, 2), 61, 0.2, 0.8)
+    K = synth.default_intrinsics()[None]
+    c2w = torch.from_numpy(synth.orbit_cam2world(0.9)).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
+    queries = []
+
+    def rf(xyz, viewdirs=None, coarse=True, return_features=False):
+        queries.append((xyz.detach().clone(), return_features, coarse))
+        return net(xyz, coarse=coarse, viewdirs=viewdirs, return_features=return_features)
+
+    torch.manual_seed(1234)
+    init = torch.zeros((1, R, 1)).normal_(mean=0.8, std=5e-2)
+    torch.manual_seed(1234)
+    with Capture() as cap, torch.no_grad():
+        rgb_c, rgb, depth_c, depth = avr(c2w, torch.from_numpy(K), torch.from_numpy(x_pix), rf)
+    band = cap.get("rand_like")[0]
+    trace = np.stack([q[0].numpy()[0] for q in queries if q[1]] + [queries[10][0].numpy()[0]], 0)
+    assert len(queries) == 12 and not queries[10][1] and queries[10][2] and not queries[11][2]
+    lstm = {f"lstm_{k}": v.detach().numpy() for k, v in avr.lstm.state_dict().items()}
+    save("g6_adaptive.npz", x_pix=x_pix, K=K, c2w_one=c2w[0, 0].numpy(), init_dist=init.numpy(),
+         band_noise=band.numpy(), trace=trace, out_w=avr.out_layer.weight.detach().numpy(),
+         out_b=avr.out_layer.bias.detach().numpy(), steps=10, epsilon=np.float32(0.05), n_coarse=20,
+         rgb_coarse=rgb_c.numpy(), rgb=rgb.numpy(), depth_coarse=depth_c.numpy(), depth=depth.numpy(),
+         **lstm, **meta, **params)
+
+
 if __name__ == "__main__":
     REF_U, REF_R, REF_M = import_reference()
     torch.set_num_threads(8)
@@ -364,3 +398,4 @@ if __name__ == "__main__":
     g3_geometry(64)
     g4_field()
     g5_forward(64)
+    g6_adaptive(48)
