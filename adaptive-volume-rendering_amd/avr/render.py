@@ -52,6 +52,10 @@ def main(argv=None):
     ap.add_argument("--latent", default=None, help=".npy latent map (1, 512, H, W)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--warmup", type=int, default=1, help="untimed frames first")
+    ap.add_argument("--renderer", choices=["volume", "adaptive"], default="volume",
+                    help="VolumeRenderer (coarse/fine) or AdaptiveVolumeRenderer (LSTM march + band)")
+    ap.add_argument("--raymarch-steps", type=int, default=10)
+    ap.add_argument("--epsilon", type=float, default=0.05)
     ap.add_argument("--out", default=None, help="directory for frame_XXX.ppm")
     args = ap.parse_args(argv)
 
@@ -68,14 +72,20 @@ def main(argv=None):
 
     from . import load_library
     from .parallel import render_sharded
-    from .renderers import VolumeRenderer
+    from .renderers import AdaptiveVolumeRenderer, VolumeRenderer
     from .scene import INTRINSICS
     from .video import get_opencv_pixel_coordinates, orbit_cam2world, to_uint8, write_ppm
     load_library()
     net = build_net(args, device)
-    rend = VolumeRenderer(args.near, args.far, args.n_coarse, args.n_fine, 0, 0.01, True)
-    rend.seed = 1234
-    rend.t_stop = args.t_stop
+    if args.renderer == "adaptive":
+        torch.manual_seed(args.seed + 2)
+        rend = AdaptiveVolumeRenderer(net.d_latent, args.raymarch_steps, args.epsilon, args.n_coarse, True).to(device)
+        samples_per_ray = args.n_coarse + 1 + args.raymarch_steps   # band + coarse point (+ LSTM lookups)
+    else:
+        rend = VolumeRenderer(args.near, args.far, args.n_coarse, args.n_fine, 0, 0.01, True)
+        rend.seed = 1234
+        rend.t_stop = args.t_stop
+        samples_per_ray = args.n_coarse + args.n_fine
     K = torch.tensor([INTRINSICS], device=device)
     H = W = args.res
     x_pix = get_opencv_pixel_coordinates(H, W).reshape(1, -1, 2).to(device)
@@ -100,7 +110,7 @@ def main(argv=None):
     for c2w in poses:
         rend.last_fine_samples = 0
         _, rgb_f, _, _ = render(c2w)
-        fine_samples += rend.last_fine_samples
+        fine_samples += getattr(rend, "last_fine_samples", 0)
         frames.append(rgb_f)
     torch.cuda.synchronize()
     if dist is not None:
@@ -117,7 +127,8 @@ def main(argv=None):
             for i, f in enumerate(frames):
                 write_ppm(os.path.join(args.out, f"frame_{i:03d}.ppm"), to_uint8(f[0].reshape(H, W, 3).cpu().numpy()))
         total_fine = args.frames * n * (args.n_coarse + args.n_fine)
-        print(json.dumps({"frames": args.frames, "res": args.res, "rays_per_frame": n, "n_gpus": world,
+        print(json.dumps({"renderer": args.renderer, "samples_per_ray": samples_per_ray,
+                          "frames": args.frames, "res": args.res, "rays_per_frame": n, "n_gpus": world,
                           "seconds": round(secs, 4), "rays_per_s": round(args.frames * n / secs, 1),
                           "t_stop": args.t_stop, "precision": args.precision, "sigma_bias": args.sigma_bias,
                           "fine_samples_evaluated": fine_samples,
