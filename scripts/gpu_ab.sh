@@ -7,5 +7,5 @@ mkdir -p gpurun_out/ab
 for lib in $STAMPS_LIBS; do
   echo "=== $lib"
   STAMPS_LIB=$PWD/$lib timeout -k 10 300 python scripts/phase_stamps.py > gpurun_out/ab/$(basename $lib).txt 2>&1 || exit 1
-  grep -E "kernel|total" gpurun_out/ab/$(basename $lib).txt
+  grep -E "${AB_GREP:-kernel|total}" gpurun_out/ab/$(basename $lib).txt
 done
