@@ -97,3 +97,12 @@ def test_model_state_dict_keys_match_reference_layout():
     mv = NewPixelNeRFNet(default_conf(multiview=True)["model"])
     mv.encoder.set_latent(torch.zeros(1, 512, 4, 4))
     assert fused_eligible(mv) and len(mv.mlp_coarse.lin_z) == 3 and mv.mlp_coarse.n_blocks == 5
+
+
+def test_graft_entry_build():
+    """__graft_entry__.build(): make (no-op when built) + load + ABI check."""
+    import importlib
+    import sys
+    sys.path.insert(0, REPO)
+    ge = importlib.import_module("__graft_entry__")
+    ge.build()
