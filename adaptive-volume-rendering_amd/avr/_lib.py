@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -71,6 +71,13 @@ _SIGS = {
                            c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p],
     "avr_field_fwd_points": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
                              c_void_p, i64, c_void_p, c_void_p],
+    "avr_field_train_sizes": [ctypes.POINTER(FieldDims), i64, ctypes.POINTER(i64), ctypes.POINTER(i64)],
+    "avr_field_bwd_packed_floats": [ctypes.POINTER(FieldDims), ctypes.POINTER(i64)],
+    "avr_field_pack_bwd": [ctypes.POINTER(FieldDims), ctypes.POINTER(ResnetFCWeights), c_void_p, c_void_p],
+    "avr_field_fwd_points_train": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
+                                   c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p],
+    "avr_field_bwd": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p,
+                      c_void_p],
 }
 EXPORTED = ("avr_version", "avr_last_error_string", "avr_device_count") + tuple(_SIGS)
 

@@ -65,6 +65,7 @@ class _Packed:
         self.dims = dims
         self.packed = packed
         self.tables = {}
+        self.bwd = None
 
 
 PRECISIONS = {"fp32": _lib.FIELD_FP32, "x3": _lib.FIELD_X3}
@@ -124,8 +125,23 @@ class FusedField:
         call("avr_field_pack", ctypes.byref(dims), ctypes.byref(w), ptr(packed), stream_of(packed))
         entry = _Packed(dims, packed, None)
         entry._keep = keep
+        entry.weights = w
         self._packed[coarse] = (key, entry)
         return entry
+
+    def packed_bwd(self, coarse, entry=None):
+        """Transposed fc_0 / fc_1 fragments for the backward kernel, cached with
+        the forward blob (rebuilt whenever a parameter changes)."""
+        entry = entry or self.packed(coarse)
+        if getattr(entry, "bwd", None) is None:
+            dims = entry.dims
+            n = ctypes.c_int64(0)
+            _lib.check(_lib.load().avr_field_bwd_packed_floats(ctypes.byref(dims), ctypes.byref(n)),
+                       "avr_field_bwd_packed_floats")
+            bwd = torch.empty(n.value, device=entry.packed.device, dtype=F32)
+            call("avr_field_pack_bwd", ctypes.byref(dims), ctypes.byref(entry.weights), ptr(bwd), stream_of(bwd))
+            entry.bwd = bwd
+        return entry.bwd
 
     def table(self, coarse, sb=0):
         entry = self.packed(coarse)
@@ -192,3 +208,124 @@ class FusedField:
             call("avr_field_fwd_points", ctypes.byref(entry.dims), ctypes.byref(self.view(sb)), ptr(entry.packed),
                  ptr(table), ptr(p), ptr(v), B, ptr(out[sb]), stream_of(p))
         return out
+
+    # ----------------------------------------------------------- training
+    def forward_train(self, xyz, viewdirs, coarse):
+        """The rf(xyz, viewdirs, coarse) protocol with autograd: HIP forward that
+        keeps every GEMM input, HIP backward through the ResnetFC, weight
+        gradients as GEMMs over the samples (see _FieldTrain)."""
+        mlp = self._mlp(coarse)
+        names = train_param_names(mlp)
+        params = [dict(mlp.named_parameters())[n] for n in names]
+        return _FieldTrain.apply(self, coarse, names, xyz, viewdirs, self.net.encoder.latent, *params)
+
+
+def train_param_names(mlp):
+    """The ResnetFC parameters the training path differentiates, in a fixed order."""
+    names = ["lin_in.weight", "lin_in.bias", "lin_out.weight", "lin_out.bias"]
+    for b in range(mlp.n_blocks):
+        names += [f"blocks.{b}.fc_0.weight", f"blocks.{b}.fc_0.bias", f"blocks.{b}.fc_1.weight", f"blocks.{b}.fc_1.bias"]
+    for b in range(min(mlp.combine_layer, mlp.n_blocks)):
+        names += [f"lin_z.{b}.weight", f"lin_z.{b}.bias"]
+    return names
+
+
+class _FieldTrain(torch.autograd.Function):
+    """Autograd of NewPixelNeRFNet.forward (models.py:739-863) for train.py's
+    loss.backward() (train.py:108-114).
+
+    forward: avr_field_fwd_points_train per scene (x3 MFMA, the inference
+    kernel plus a store of every hidden GEMM input and its relu mask).
+    backward: avr_field_bwd runs the input-gradient chain (lin_out^T, then
+    fc_1^T / fc_0^T per block with the relu masks, x3 MFMA) and writes the
+    gradient at every layer output; the weight gradients are then plain GEMMs
+    over the samples, dW = G^T act (hipBLASLt through torch.mm), and the biases
+    column sums. lin_z[b] differentiates against the interpolated latent
+    (grid_sample, as models.py:266-273), and the latent map gets the
+    grid_sample adjoint of sum_b G_z[b] W_z[b] when it requires grad."""
+
+    @staticmethod
+    def forward(ctx, fused, coarse, names, xyz, viewdirs, latent, *params):
+        SB, B, _ = xyz.shape
+        entry = fused.packed(coarse)
+        dims = entry.dims
+        dims.precision = _lib.FIELD_X3
+        H, nb = dims.d_hidden, dims.n_blocks
+        act_n, mask_n = ctypes.c_int64(0), ctypes.c_int64(0)
+        _lib.check(_lib.load().avr_field_train_sizes(ctypes.byref(dims), B, ctypes.byref(act_n), ctypes.byref(mask_n)),
+                   "avr_field_train_sizes")
+        out = torch.empty(SB, B, 4, device=xyz.device, dtype=F32)
+        acts, masks = [], []
+        vd = viewdirs.reshape(SB, B, 3)
+        for sb in range(SB):
+            p = xyz[sb].detach().to(F32).contiguous()
+            v = vd[sb].detach().to(F32).contiguous()
+            require_device(p, v)
+            act = torch.empty(2 * nb + 1, B, H, device=xyz.device, dtype=F32)
+            mask = torch.empty(max(mask_n.value, 1), device=xyz.device, dtype=torch.int32)
+            call("avr_field_fwd_points_train", ctypes.byref(dims), ctypes.byref(fused.view(sb)), ptr(entry.packed),
+                 ptr(fused.table(coarse, sb)), ptr(p), ptr(v), B, ptr(out[sb]), ptr(act), ptr(mask), stream_of(p))
+            acts.append(act)
+            masks.append(mask)
+        entry.dims.precision = PRECISIONS[fused.precision]
+        ctx.fused, ctx.coarse, ctx.names, ctx.entry = fused, coarse, names, entry
+        ctx.acts, ctx.masks = acts, masks
+        ctx.save_for_backward(xyz, viewdirs, latent, out, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        xyz, viewdirs, latent, out, *params = ctx.saved_tensors
+        fused, entry, names = ctx.fused, ctx.entry, ctx.names
+        net = fused.net
+        P = dict(zip(names, params))
+        dims = entry.dims
+        dims.precision = _lib.FIELD_X3
+        H, nb, nz = dims.d_hidden, dims.n_blocks, dims.n_lin_z
+        SB, B, _ = xyz.shape
+        bwd = fused.packed_bwd(ctx.coarse, entry)
+        grad_out = grad_out.to(F32).contiguous()
+        want_latent = ctx.needs_input_grad[5] and not net.stop_encoder_grad
+        if B == 0:
+            zeros = tuple(torch.zeros_like(p) if ctx.needs_input_grad[6 + i] else None for i, p in enumerate(params))
+            return (None, None, None, None, None, torch.zeros_like(latent) if want_latent else None) + zeros
+        # MLP inputs the weight gradients contract against (the same torch code as forward_torch)
+        with torch.no_grad():
+            lat_feat, z_feature = net.mlp_inputs(xyz.detach(), viewdirs.detach())
+        grads = {n: torch.zeros_like(P[n]) for n in names}
+        dZ = torch.zeros(SB * B, net.d_latent, device=xyz.device, dtype=F32) if want_latent else None
+        for sb in range(SB):
+            G = torch.empty(2 * nb + 1, B, H, device=xyz.device, dtype=F32)
+            go = grad_out[sb].contiguous()
+            call("avr_field_bwd", ctypes.byref(dims), ptr(entry.packed), ptr(bwd), ptr(out[sb]), ptr(go),
+                 ptr(ctx.masks[sb]), B, ptr(G), stream_of(G))
+            act = ctx.acts[sb]
+            y = out[sb]
+            d4 = torch.cat([go[:, :3] * ((1.0 - y[:, :3]) * y[:, :3]), go[:, 3:] * (y[:, 3:] > 0)], -1)
+            grads["lin_out.weight"] += d4.t() @ act[2 * nb]
+            grads["lin_out.bias"] += d4.sum(0)
+            for b in range(nb):
+                grads[f"blocks.{b}.fc_0.weight"] += G[2 * b].t() @ act[2 * b]
+                grads[f"blocks.{b}.fc_0.bias"] += G[2 * b].sum(0)
+                grads[f"blocks.{b}.fc_1.weight"] += G[2 * b + 1].t() @ act[2 * b + 1]
+                grads[f"blocks.{b}.fc_1.bias"] += G[2 * b + 1].sum(0)
+            rows = slice(sb * B, (sb + 1) * B)
+            grads["lin_in.weight"] += G[2 * nb].t() @ z_feature[rows]
+            grads["lin_in.bias"] += G[2 * nb].sum(0)
+            for b in range(nz):
+                Gz = G[2 * b - 1] if b > 0 else G[2 * nb]
+                grads[f"lin_z.{b}.weight"] += Gz.t() @ lat_feat[rows]
+                grads[f"lin_z.{b}.bias"] += Gz.sum(0)
+                if dZ is not None:
+                    dZ[rows] += Gz @ P[f"lin_z.{b}.weight"].detach()
+            del G
+        ctx.acts = ctx.masks = None
+        entry.dims.precision = PRECISIONS[fused.precision]
+        d_latent = None
+        if dZ is not None:
+            with torch.enable_grad():
+                lat = latent.detach().requires_grad_(True)
+                feat, _ = net.mlp_inputs(xyz.detach(), viewdirs.detach(), latent=lat)
+                (d_latent,) = torch.autograd.grad(feat, lat, dZ)
+        return (None, None, None, None, None, d_latent) + tuple(
+            grads[n] if ctx.needs_input_grad[6 + i] else None for i, n in enumerate(names))

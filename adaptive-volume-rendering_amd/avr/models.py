@@ -224,6 +224,7 @@ class NewPixelNeRFNet(nn.Module):
         self.num_objs, self.num_views_per_obj = 0, 1
         self.use_fused = True           # HIP field under no_grad (avr.field)
         self.field_precision = "x3"     # "x3" split-fp16 MFMA | "fp32" MFMA
+        self.hip_backward = True        # autograd through the HIP field (avr.field._FieldTrain)
         self._fused = None
 
     def encode_latent(self, latent, poses, focal, c=None, image_shape=None):
@@ -278,18 +279,35 @@ class NewPixelNeRFNet(nn.Module):
     def _needs_grad(self):
         return any(p.requires_grad for p in self.parameters()) or self.encoder.latent.requires_grad
 
+    def can_train_fused(self, xyz, viewdirs):
+        """Autograd on the HIP path: parameters / latent need gradients, the
+        points do not (VolumeRenderer training; the adaptive renderer's band
+        points carry a gradient and take forward_torch)."""
+        from .field import fused_eligible
+        return (self.use_fused and self.hip_backward and xyz.is_cuda and torch.is_grad_enabled()
+                and not xyz.requires_grad and viewdirs is not None and not viewdirs.requires_grad
+                and fused_eligible(self))
+
     def forward(self, xyz, coarse=True, viewdirs=None, far=False, return_features=False):
         if not return_features and self.can_fuse(xyz):
             return self.fused().forward_points(xyz, viewdirs, coarse)
+        if not return_features and self.can_train_fused(xyz, viewdirs):
+            return self.fused().forward_train(xyz, viewdirs, coarse)
         return self.forward_torch(xyz, coarse, viewdirs, far, return_features)
 
-    def forward_torch(self, xyz, coarse=True, viewdirs=None, far=False, return_features=False):
-        """models.py:739-863 as PyTorch ops (the autograd path)."""
+    def mlp_inputs(self, xyz, viewdirs, latent=None):
+        """(latent features (SB*B, d_latent), z_feature (SB*B, d_in)) at the
+        points: the MLP input halves of models.py:753-823 (forward_torch's code;
+        `latent` overrides the encoder's map, for its gradient)."""
+        return self._inputs(xyz, viewdirs, latent)[:2]
+
+    def _inputs(self, xyz, viewdirs, latent_map=None):
         SB, B, _ = xyz.shape
         NS = self.num_views_per_obj
         xyz = repeat_interleave(xyz, NS)
         xyz_rot = torch.matmul(self.poses[:, None, :3, :3], xyz.unsqueeze(-1))[..., 0]
         xyz = xyz_rot + self.poses[:, None, :3, 3]
+        z_feature = latent = None
         if self.d_in > 0:
             if self.use_xyz:
                 z_feature = (xyz_rot if self.normalize_z else xyz).reshape(-1, 3)
@@ -303,15 +321,31 @@ class NewPixelNeRFNet(nn.Module):
                 z_feature = torch.cat((z_feature, vd), dim=1)
             if self.use_code and self.use_code_viewdirs:
                 z_feature = self.code(z_feature)
-            mlp_input = z_feature
         if self.use_encoder:
             uv = -xyz[:, :, :2] / xyz[:, :, 2:]
             uv = uv * repeat_interleave(self.focal.unsqueeze(1), NS if self.focal.shape[0] > 1 else 1)
             uv = uv + repeat_interleave(self.c.unsqueeze(1), NS if self.c.shape[0] > 1 else 1)
-            latent = self.encoder.index(uv, None, self.image_shape)
+            if latent_map is None:
+                latent = self.encoder.index(uv, None, self.image_shape)
+            else:
+                held = self.encoder.latent
+                try:
+                    self.encoder.latent = latent_map
+                    latent = self.encoder.index(uv, None, self.image_shape)
+                finally:
+                    self.encoder.latent = held
             if self.stop_encoder_grad:
                 latent = latent.detach()
             latent = latent.transpose(1, 2).reshape(-1, self.latent_size)
+        return latent, z_feature, B
+
+    def forward_torch(self, xyz, coarse=True, viewdirs=None, far=False, return_features=False):
+        """models.py:739-863 as PyTorch ops (the autograd path)."""
+        SB = xyz.shape[0]
+        latent, z_feature, B = self._inputs(xyz, viewdirs)
+        if self.d_in > 0:
+            mlp_input = z_feature
+        if self.use_encoder:
             mlp_input = latent if self.d_in == 0 else torch.cat((latent, z_feature), dim=-1)
         if return_features:
             return latent

@@ -66,6 +66,17 @@ static int make_layout(const avr_field_dims* d, Layout* L) {
   return AVR_OK;
 }
 
+static int make_bwd_layout(const avr_field_dims* d, BwdLayout* LB) {
+  const int64_t S = (int64_t)(d->d_hidden / 32) * (d->d_hidden / 16) * 64 * 8;   // floats per x3 hidden layer
+  int64_t o = 64;
+  for (int b = 0; b < d->n_blocks; ++b) {
+    LB->fc0t[b] = o; o += S;
+    LB->fc1t[b] = o; o += S;
+  }
+  LB->total = o;
+  return AVR_OK;
+}
+
 // ----------------------------------------------------------------- packing
 // dst[(t*NTo + ot)*64 + l][r] = W[16ot + (l&15)][16t + 4(l>>4) + r]  (zero padded)
 __global__ void pack_linear_kernel(const float* __restrict__ W, int out_dim, int in_dim, int NTo, int KTi,
@@ -102,8 +113,9 @@ __global__ void absmax_kernel(const float* __restrict__ W, int64_t n, unsigned* 
 // x3 fragments: dst[((c*FTt + ft)*64 + l)*16 + {e, 8+e}] = (hi, lo) of
 // W[16ft + (l&15)][32c + (e<4 ? 4g+e : 16+4g+e-4)] * s_w, g = l>>4, with
 // s_w = 2^(14 - ceil-exponent of max|W|) from the layer's header word.
-__global__ void pack_x3_kernel(const float* __restrict__ W, int out_dim, int in_dim, int KC, int FTt,
-                               const unsigned* __restrict__ maxbits, _Float16* __restrict__ dst) {
+// (rs, cs) = element strides of W's rows / columns: (in_dim, 1) for W, (1, ld) for W^T.
+__global__ void pack_x3_kernel(const float* __restrict__ W, int out_dim, int in_dim, int64_t rs, int64_t cs, int KC,
+                               int FTt, const unsigned* __restrict__ maxbits, _Float16* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = (int64_t)KC * FTt * 64 * 8;
   if (i >= n) return;
@@ -115,7 +127,7 @@ __global__ void pack_x3_kernel(const float* __restrict__ W, int out_dim, int in_
   const int row = 16 * ft + (l & 15);
   const int col = 32 * c + (e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4));
   const float sw = pow2_scale_for(__uint_as_float(*maxbits));
-  const float v = (row < out_dim && col < in_dim) ? W[(int64_t)row * in_dim + col] * sw : 0.f;
+  const float v = (row < out_dim && col < in_dim) ? W[(int64_t)row * rs + (int64_t)col * cs] * sw : 0.f;
   const _Float16 hi = (_Float16)v;
   const _Float16 lo = (_Float16)(v - (float)hi);
   const int64_t base = (((int64_t)c * FTt + ft) * 64 + l) * 16;
@@ -296,14 +308,16 @@ static int pack_linear(const float* W, int out_dim, int in_dim, int NTo, int KTi
 }
 
 static int pack_x3(const float* W, int out_dim, int in_dim, int KC, int FTt, unsigned* maxbits, float* dst,
-                   hipStream_t s) {
+                   hipStream_t s, bool transpose = false) {
   AVR_REQUIRE(W, "avr_field_pack: null weight tensor");
   const int64_t nw = (int64_t)out_dim * in_dim;
   absmax_kernel<<<(unsigned)((nw + 255) / 256 < 256 ? (nw + 255) / 256 : 256), 256, 0, s>>>(W, nw, maxbits);
   int rc = check_launch("absmax_kernel");
   if (rc) return rc;
   const int64_t n = (int64_t)KC * FTt * 64 * 8;
-  pack_x3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(W, out_dim, in_dim, KC, FTt, maxbits,
+  // transpose: W is (in_dim, out_dim) row-major and the fragments hold W^T
+  const int64_t rs = transpose ? 1 : in_dim, cs = transpose ? out_dim : 1;
+  pack_x3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(W, out_dim, in_dim, rs, cs, KC, FTt, maxbits,
                                                             reinterpret_cast<_Float16*>(dst));
   return check_launch("pack_x3_kernel");
 }
@@ -430,6 +444,89 @@ extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_wei
     if ((rc = pack_x3(w->fc1_w[b], H, H, KC, NT, hdr + 3 + 2 * b, packed + L.x3_fc1[b], s))) return rc;
   }
   return AVR_OK;
+}
+
+extern "C" int avr_field_bwd_packed_floats(const avr_field_dims* dims, int64_t* n_floats) {
+  Layout L;
+  BwdLayout LB;
+  const int rc = make_layout(dims, &L);
+  if (rc) return rc;
+  AVR_REQUIRE(n_floats, "avr_field_bwd_packed_floats: null output");
+  make_bwd_layout(dims, &LB);
+  *n_floats = LB.total;
+  return AVR_OK;
+}
+
+extern "C" int avr_field_pack_bwd(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed_bwd,
+                                  void* stream) {
+  Layout L;
+  BwdLayout LB;
+  int rc = make_layout(dims, &L);
+  if (rc) return rc;
+  AVR_REQUIRE(w && packed_bwd, "avr_field_pack_bwd: null pointer");
+  make_bwd_layout(dims, &LB);
+  hipStream_t s = as_stream(stream);
+  unsigned* hdr = reinterpret_cast<unsigned*>(packed_bwd);
+  if (hipMemsetAsync(hdr, 0, 64 * sizeof(float), s) != hipSuccess) return fail(AVR_E_HIP, "avr_field_pack_bwd: memset");
+  const int H = dims->d_hidden, KC = H / 32, NT = H / 16;
+  for (int b = 0; b < dims->n_blocks; ++b) {
+    if ((rc = pack_x3(w->fc0_w[b], H, H, KC, NT, hdr + 2 + 2 * b, packed_bwd + LB.fc0t[b], s, true))) return rc;
+    if ((rc = pack_x3(w->fc1_w[b], H, H, KC, NT, hdr + 3 + 2 * b, packed_bwd + LB.fc1t[b], s, true))) return rc;
+  }
+  return AVR_OK;
+}
+
+extern "C" int avr_field_train_sizes(const avr_field_dims* dims, int64_t n_points, int64_t* act_floats,
+                                     int64_t* mask_words_out) {
+  Layout L;
+  const int rc = make_layout(dims, &L);
+  if (rc) return rc;
+  AVR_REQUIRE(n_points >= 0 && act_floats && mask_words_out, "avr_field_train_sizes: bad argument");
+  const int64_t layers = 2 * dims->n_blocks + 1;
+  const int64_t blocks = (n_points + kX3Samples - 1) / kX3Samples;
+  *act_floats = layers * n_points * dims->d_hidden;
+  *mask_words_out = layers * blocks * 4 * mask_words(dims->d_hidden / 64) * 64;
+  return AVR_OK;
+}
+
+extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
+                                          const float* table, const float* xyz, const float* viewdirs,
+                                          int64_t n_points, float* out, float* act, uint32_t* mask, void* stream) {
+  FieldArgs a{};
+  int rc = field_common(dims, view, packed, table, &a);
+  if (rc) return rc;
+  AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_fwd_points_train: the training path is x3 only");
+  AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points_train: bad size");
+  AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && out && act && mask), "avr_field_fwd_points_train: null pointer");
+  a.xyz = xyz; a.vd = viewdirs; a.n_samples = 1;
+  a.M = n_points;
+  a.out = reinterpret_cast<float4*>(out);
+  a.act = act;
+  a.mask = mask;
+  if (a.M == 0) return AVR_OK;
+  return dispatch_field_x3(dims->d_hidden, a, as_stream(stream));
+}
+
+extern "C" int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd,
+                             const float* out, const float* grad_out, const uint32_t* mask, int64_t n_points,
+                             float* grads, void* stream) {
+  BwdArgs a{};
+  int rc = make_layout(dims, &a.L);
+  if (rc) return rc;
+  AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_bwd: the training path is x3 only");
+  AVR_REQUIRE(n_points >= 0, "avr_field_bwd: bad size");
+  if (n_points == 0) return AVR_OK;
+  AVR_REQUIRE(packed && packed_bwd && out && grad_out && mask && grads, "avr_field_bwd: null pointer");
+  make_bwd_layout(dims, &a.LB);
+  a.packed = packed;
+  a.packed_bwd = packed_bwd;
+  a.n_blocks = dims->n_blocks;
+  a.M = n_points;
+  a.out = reinterpret_cast<const float4*>(out);
+  a.grad_out = reinterpret_cast<const float4*>(grad_out);
+  a.mask = mask;
+  a.G = grads;
+  return dispatch_field_bwd_x3(dims->d_hidden, a, as_stream(stream));
 }
 
 extern "C" int avr_field_latent_table(const avr_field_dims* dims, const float* packed, const float* latent, int H,

@@ -1,0 +1,178 @@
+// Backward of the radiance field's ResnetFC: the input-gradient chain of
+// autograd through models.py:856-862 (sigmoid rgb, relu sigma), lin_out
+// (:592), every ResnetBlockFC (:454-470, dx = fc_1(relu(fc_0(relu(x)))),
+// out = x + dx) and the lin_z residual adds (:578-581), in reverse:
+//   dx  = W_out^T d_out  (x) [a_out > 0]                      (G[2 nb] is written last)
+//   per block b = nb-1 .. 0:
+//     G1_b = dx                                               -> G[2b + 1]
+//     G0_b = (W1_b^T G1_b) (x) [r_b > 0]                      -> G[2b]
+//     dx   = dx + (W0_b^T G0_b) (x) [a_b > 0]                 (gradient at block b's input)
+//   G_in = dx                                                 -> G[2 nb]
+// G[l] pairs with the forward's saved GEMM input act[l] (a_b = act[2b],
+// r_b = act[2b+1], a_out = act[2 nb]): dW = G[l]^T act[l] and db = sum G[l]
+// are plain GEMMs / reductions over the samples, done by the caller.
+//
+// The two 512x512 products per block run on the forward's split-fp16 MFMA
+// machinery (x3_gemm.h) with W^T packed in the same fragment order
+// (avr_field_pack_bwd). Per 64-sample workgroup the chain needs only the relu
+// masks of the forward (1 bit per value, 16 B per lane and layer), so nothing
+// but the gradients themselves goes through HBM.
+#include "x3_gemm.h"
+
+namespace avr {
+
+template <int FT>
+__device__ __forceinline__ floatx4 masked(const floatx4& v, const unsigned* mb, int ft, int sg) {
+  const int idx = (ft * 4 + sg) * 4;
+  const unsigned bits = mb[idx >> 5] >> (idx & 31);
+  floatx4 r;
+  r.x = (bits & 1u) ? v.x : 0.f;
+  r.y = (bits & 2u) ? v.y : 0.f;
+  r.z = (bits & 4u) ? v.z : 0.f;
+  r.w = (bits & 8u) ? v.w : 0.f;
+  return r;
+}
+
+template <int FT, int NW>
+__device__ __forceinline__ void load_mask(unsigned (&mb)[mask_words(FT)], const unsigned* mask, int layer, int lane,
+                                          int wid) {
+  constexpr int MW = mask_words(FT);
+  const unsigned* mk = mask + (((int64_t)layer * gridDim.x + blockIdx.x) * NW + wid) * MW * 64 + lane;
+#pragma unroll
+  for (int q = 0; q < MW; ++q) mb[q] = mk[q * 64];
+}
+
+template <int FT, int NW>
+__device__ __forceinline__ void store_rows(float* G, const floatx4 (&v)[FT][4], int64_t base, int64_t M, int wid,
+                                           int g, int j) {
+  constexpr int HID = 16 * FT * NW;
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      const int64_t m = base + 16 * sg + j;
+      if (m < M) *reinterpret_cast<floatx4*>(G + m * HID + 16 * (FT * wid + ft) + 4 * g) = v[ft][sg];
+    }
+}
+
+template <int FT>
+__device__ __forceinline__ float absmax(const floatx4 (&v)[FT][4]) {
+  float mx = 0.f;
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      const floatx4 x = v[ft][sg];
+      mx = fmaxf(fmaxf(mx, fabsf(x.x)), fmaxf(fabsf(x.y), fmaxf(fabsf(x.z), fabsf(x.w))));
+    }
+  return wave_max(mx);
+}
+
+__device__ __forceinline__ float bwd_scale(const float* packed_bwd, int layer) {
+  return pow2_scale_for(__uint_as_float(reinterpret_cast<const unsigned*>(packed_bwd)[layer]));
+}
+
+template <int FT, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
+  constexpr int HID = 16 * FT * NW;
+  constexpr int KC = HID / 32;
+  constexpr int NTT = FT * NW;
+  constexpr int MW = mask_words(FT);
+  extern __shared__ float lds[];
+  uint4* X16 = reinterpret_cast<uint4*>(lds);   // KC chunks x 8 KiB, the forward's operand layout
+  float* red = lds + KC * 2048;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int64_t base = (int64_t)blockIdx.x * kX3Samples;
+  const int64_t HM = a.M * HID;
+  const int nb = a.n_blocks;
+  const uint4* PB = reinterpret_cast<const uint4*>(a.packed_bwd);
+
+  floatx4 dx[FT][4], t[FT][4];
+  unsigned mb[MW];
+  // ---- d out: sigmoid' from the saved output (torch: g * (1 - y) * y), relu' (y > 0)
+  float d4[4][4];
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg) {
+    const int64_t m = base + 16 * sg + j;
+    const bool ok = m < a.M;
+    const float4 o = a.out[ok ? m : a.M - 1], go = a.grad_out[ok ? m : a.M - 1];
+    d4[sg][0] = ok ? go.x * ((1.f - o.x) * o.x) : 0.f;
+    d4[sg][1] = ok ? go.y * ((1.f - o.y) * o.y) : 0.f;
+    d4[sg][2] = ok ? go.z * ((1.f - o.z) * o.z) : 0.f;
+    d4[sg][3] = ok && o.w > 0.f ? go.w : 0.f;
+  }
+  load_mask<FT, NW>(mb, a.mask, 2 * nb, lane, wid);
+  // ---- lin_out^T: W_out (4 x HID) from the fp32 fragments, row k of tile `tile` at lane k + 16 g
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    const int tile = FT * wid + ft;
+    floatx4 w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = *reinterpret_cast<const floatx4*>(a.packed + a.L.w_out + ((int64_t)tile * 64 + k + 16 * g) * 4);
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      const floatx4 acc = ((w[0] * d4[sg][0] + w[1] * d4[sg][1]) + w[2] * d4[sg][2]) + w[3] * d4[sg][3];
+      dx[ft][sg] = masked<FT>(acc, mb, ft, sg);
+    }
+  }
+
+  FragX3 A0[FT];
+  for (int b = nb - 1; b >= 0; --b) {
+    // ---- fc_1^T
+    store_rows<FT, NW>(a.G + (2 * b + 1) * HM, dx, base, a.M, wid, g, j);
+    const uint4* W1 = PB + a.LB.fc1t[b] / 4 + 2 * 64 * FT * wid;
+    prefetch_a<FT>(A0, W1, lane);
+    float s_x = publish<FT, NW>(X16, dx, absmax<FT>(dx), red, wid, lane, g, j);
+    load_mask<FT, NW>(mb, a.mask, 2 * b + 1, lane, wid);
+    gemm_x3<FT, true, false>(t, A0, W1, KC, 64 * NTT, X16, lane);
+    float inv = 1.0f / (bwd_scale(a.packed_bwd, 3 + 2 * b) * s_x);
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) t[ft][sg] = masked<FT>(t[ft][sg] * inv, mb, ft, sg);
+    store_rows<FT, NW>(a.G + 2 * b * HM, t, base, a.M, wid, g, j);
+    // ---- fc_0^T
+    const uint4* W0 = PB + a.LB.fc0t[b] / 4 + 2 * 64 * FT * wid;
+    prefetch_a<FT>(A0, W0, lane);
+    s_x = publish<FT, NW>(X16, t, absmax<FT>(t), red, wid, lane, g, j);
+    load_mask<FT, NW>(mb, a.mask, 2 * b, lane, wid);
+    gemm_x3<FT, true, false>(t, A0, W0, KC, 64 * NTT, X16, lane);
+    inv = 1.0f / (bwd_scale(a.packed_bwd, 2 + 2 * b) * s_x);
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) dx[ft][sg] += masked<FT>(t[ft][sg] * inv, mb, ft, sg);
+  }
+  store_rows<FT, NW>(a.G + 2 * nb * HM, dx, base, a.M, wid, g, j);
+}
+
+template <int FT, int NW>
+static int launch_bwd(const BwdArgs& a, hipStream_t s) {
+  constexpr int HID = 16 * FT * NW;
+  const size_t shm = (size_t)(HID / 32) * 8192 + 64;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bwd_x3_kernel<FT, NW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
+      return fail(AVR_E_HIP, "field_bwd_x3_kernel: cannot set dynamic LDS to %zu", shm);
+    attr = true;
+  }
+  const int64_t blocks = (a.M + kX3Samples - 1) / kX3Samples;
+  AVR_REQUIRE(blocks < (1ll << 31), "field backward: too many points");
+  field_bwd_x3_kernel<FT, NW><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
+  return check_launch("field_bwd_x3_kernel");
+}
+
+int dispatch_field_bwd_x3(int d_hidden, const BwdArgs& a, hipStream_t s) {
+  switch (d_hidden) {
+    case 64: return launch_bwd<1, 4>(a, s);
+    case 128: return launch_bwd<2, 4>(a, s);
+    case 256: return launch_bwd<4, 4>(a, s);
+    case 512: return launch_bwd<8, 4>(a, s);
+  }
+  return fail(AVR_E_UNSUPPORTED, "field backward: d_hidden %d", d_hidden);
+}
+
+}  // namespace avr

@@ -31,6 +31,19 @@ struct Layout {
   int64_t total;          // floats
 };
 
+// Backward blob (avr_field_pack_bwd): header (64 words, max|W| bits per layer
+// in the forward's numbering) + x3 fragments of fc_0[b]^T and fc_1[b]^T in the
+// forward's [c][ft][lane] order.
+struct BwdLayout {
+  int64_t fc0t[AVR_MAX_BLOCKS], fc1t[AVR_MAX_BLOCKS];
+  int64_t total;          // floats
+};
+
+// Training forward / backward (x3 path): relu masks of the 2 * n_blocks + 1
+// GEMM inputs, one bit per (feature, sample) a lane holds, bit
+// (ft * 4 + sg) * 4 + r; words [layer][workgroup][wave][word][lane].
+__host__ __device__ constexpr int mask_words(int FT) { return (FT * 16 + 31) / 32; }
+
 struct View {
   float R[9], t[3];
   float focal[2], c[2], scale[2];
@@ -65,6 +78,8 @@ struct FieldArgs {
   const float* xyz; const float* vd;
   int64_t M;
   float4* out;
+  float* act;                  // training forward: GEMM inputs, (2 n_blocks + 1, M, d_hidden) fp32, or null
+  unsigned* mask;              //   and their relu masks (see mask_words)
   unsigned long long* stamps;  // diagnostic builds (-DAVR_STAMPS) only: per-block phase clocks (waves 0, 4)
   int debug;                   // diagnostic builds only: experiment flags (1: every fc layer uses block 0's weights)
 };
@@ -212,5 +227,20 @@ __device__ __forceinline__ float pow2_scale_for(float maxabs) {
 }
 
 int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s);
+
+struct BwdArgs {
+  const float* packed;      // forward blob: lin_out fp32 fragments
+  const float* packed_bwd;  // backward blob (BwdLayout)
+  Layout L;
+  BwdLayout LB;
+  int n_blocks;
+  int64_t M;
+  const float4* out;        // field output (sigmoid rgb, relu sigma)
+  const float4* grad_out;
+  const unsigned* mask;
+  float* G;                 // (2 n_blocks + 1, M, d_hidden) layer-output gradients
+};
+
+int dispatch_field_bwd_x3(int d_hidden, const BwdArgs& a, hipStream_t s);
 
 }  // namespace avr

@@ -1,0 +1,224 @@
+// Split-fp16 ("x3") MFMA building blocks shared by the field forward
+// (field_x3.hip) and backward (field_bwd.hip) kernels: the LDS operand layout,
+// the hi/lo split, the K-chunk GEMM loop with weights streamed one chunk ahead,
+// and the publish step that turns a layer's register values into the next
+// GEMM's LDS operand.
+#pragma once
+#include "field_common.h"
+
+// Contraction is fine for the field's own arithmetic (bias / interpolation /
+// scaling); the geometry helpers use __f*_rn intrinsics, which never contract.
+#pragma clang fp contract(fast)
+
+namespace avr {
+
+struct FragX3 {
+  half8 hi, lo;
+};
+
+__device__ __forceinline__ FragX3 load_frag(const uint4* p) {
+  FragX3 f;
+  const uint4 a = p[0], b = p[1];
+  f.hi = __builtin_bit_cast(half8, a);
+  f.lo = __builtin_bit_cast(half8, b);
+  return f;
+}
+
+// LDS X: 16-B slot (chunk c, part 0 = hi / 1 = lo, lane group g, sample s)
+// holding the 8 fp16 B-operand elements e of that lane: feature
+// 32c + 16*(e>>2) + 4g + (e&3). Writers place a tile's 4 values at byte 8*(tile&1).
+__device__ __forceinline__ int xidx(int c, int part, int g, int s) { return ((c * 2 + part) * 4 + g) * 64 + s; }
+
+struct BPair {
+  half8 hi, lo;
+};
+
+__device__ __forceinline__ BPair read_b(const uint4* X16, int c, int sg, int g, int j) {
+  BPair b;
+  b.hi = __builtin_bit_cast(half8, X16[xidx(c, 0, g, 16 * sg + j)]);
+  b.lo = __builtin_bit_cast(half8, X16[xidx(c, 1, g, 16 * sg + j)]);
+  return b;
+}
+
+// hi = fp16(x*s), lo = fp16(x*s - hi): one packed convert per pair for hi and
+// one v_fma_mix{lo,hi}_f16 per value for lo (x*s is exact: s is a power of two)
+__device__ __forceinline__ void split4(const floatx4& x, float s, uint2& hi, uint2& lo) {
+  const floatx4 y = x * s;
+  unsigned h0, h1, l0, l1;
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h0) : "v"(y.x), "v"(y.y));
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h1) : "v"(y.z), "v"(y.w));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l0) : "v"(x.x), "v"(s), "v"(h0));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l0) : "v"(x.y), "v"(s), "v"(h0));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l1) : "v"(x.z), "v"(s), "v"(h1));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l1) : "v"(x.w), "v"(s), "v"(h1));
+  hi = make_uint2(h0, h1);
+  lo = make_uint2(l0, l1);
+}
+
+// One K-chunk on resident fragments A (this wave's FT tiles) and B (the 4
+// sample groups), in feature-tile pairs: pair p issues its 3 x 2 x 4 chained
+// v_mfma_f32_16x16x32_f16 (each accumulation chain issues back to back at full
+// rate, MI355X_MICROARCH.md) and the global loads of pair p of the NEXT chunk
+// into An, one load per few MFMAs (sched_group_barrier), so every A load has a
+// whole chunk of MFMAs to land in and its issue hides in the MFMA gaps. In the
+// last pair each B[sg] is refilled with the next chunk's fragment as soon as
+// its MFMAs have issued.
+template <int FT, bool ZERO>
+__device__ __forceinline__ void chunk_step(floatx4 (&acc)[FT][4], const FragX3 (&A)[FT], FragX3 (&An)[FT],
+                                           const uint4* wn, BPair (&B)[4], const uint4* X16, int cn, int g, int j) {
+  constexpr int GS = FT >= 2 ? 2 : 1;       // tiles per group
+  constexpr int NG = FT / GS;
+  constexpr int NMF = 3 * GS * 4;           // MFMAs per group
+  constexpr int NLD = 2 * GS;               // global loads per group
+  constexpr int PER = NMF / (NLD + 1);
+#pragma unroll
+  for (int p = 0; p < NG; ++p) {
+#pragma unroll
+    for (int q = 0; q < GS; ++q) An[GS * p + q] = load_frag(wn + 2 * 64 * (GS * p + q));
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+#pragma unroll
+      for (int q = 0; q < GS; ++q) {
+        const int ft = GS * p + q;
+        acc[ft][sg] = mfma32h(A[ft].hi, B[sg].hi, ZERO ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[ft][sg]);
+        acc[ft][sg] = mfma32h(A[ft].hi, B[sg].lo, acc[ft][sg]);
+        acc[ft][sg] = mfma32h(A[ft].lo, B[sg].hi, acc[ft][sg]);
+      }
+      if (p == NG - 1) B[sg] = read_b(X16, cn, sg, g, j);
+    }
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NLD * PER, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// acc (+)= W . X over KC chunks (KC even, runtime; ZERO: acc starts from 0).
+// W points at this wave's first fragment of chunk 0; consecutive chunks are
+// `cstride` fragments (32 B each) apart. A is double-buffered one chunk ahead
+// in registers (the last chunk reloads itself: harmless, keeps the pattern).
+// This wave's chunk-0 A fragments of a layer, loaded ahead of the layer
+// (before the publish that precedes it) so the GEMM starts on landed data.
+// Only the first kPrefetch tiles (the first group of chunk 0) are prefetched:
+// more would push the epilogue into spills, and a scratch store waits for
+// every outstanding load.
+constexpr int kPrefetch = 2;
+
+template <int FT>
+__device__ __forceinline__ void prefetch_a(FragX3 (&A0)[FT], const uint4* __restrict__ W, int lane) {
+#pragma unroll
+  for (int ft = 0; ft < (FT < kPrefetch ? FT : kPrefetch); ++ft) A0[ft] = load_frag(W + 2 * lane + 2 * 64 * ft);
+}
+
+// A0 holds chunk 0 (prefetch_a).
+template <int FT, bool ZERO, bool SYNC>
+__device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W, int KC,
+                                        int cstride, const uint4* X16, int lane) {
+  const int g = lane >> 4, j = lane & 15;
+  const uint4* wl = W + 2 * lane;
+  FragX3 A1[FT];
+  BPair B[4];
+#pragma unroll
+  for (int ft = kPrefetch; ft < FT; ++ft) A0[ft] = load_frag(wl + 2 * 64 * ft);
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg) B[sg] = read_b(X16, 0, sg, g, j);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int c = 0; c < KC; c += 2) {
+    const int c2 = c + 2 < KC ? c + 2 : c + 1;
+    const uint4* w1 = wl + (int64_t)2 * (c + 1) * cstride;
+    const uint4* w2 = wl + (int64_t)2 * c2 * cstride;
+    if (ZERO && c == 0)
+      chunk_step<FT, true>(acc, A0, A1, w1, B, X16, c + 1, g, j);
+    else
+      chunk_step<FT, false>(acc, A0, A1, w1, B, X16, c + 1, g, j);
+    chunk_step<FT, false>(acc, A1, A0, w2, B, X16, c2, g, j);
+    // two waves per SIMD: the older one would otherwise win the MFMA pipe and
+    // run a whole layer ahead, leaving its partner's epilogue unoverlapped;
+    // a plain barrier every two chunks keeps them in step (the MFMA pipe stays
+    // busy with the lagging wave meanwhile)
+    if (SYNC) __builtin_amdgcn_s_barrier();
+  }
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not
+// for its outstanding global loads (the next layer's weight prefetch stays in
+// flight; __syncthreads would drain it).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = fmaxf(v, __shfl_xor(v, d, 64));
+  return v;
+}
+
+// v = relu(acc * f [+ bias]) (one read of the accumulators), returns the wave max
+template <int FT, bool BIAS>
+__device__ __forceinline__ float prep_input(floatx4 (&v)[FT][4], const floatx4 (&acc)[FT][4], float f,
+                                            const float* __restrict__ bias, int wid, int g) {
+  float mx = 0.f;
+  floatx4 bv[FT];   // all bias loads first (one wait, not one per tile)
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+    bv[ft] = BIAS ? *reinterpret_cast<const floatx4*>(bias + 16 * (FT * wid + ft) + 4 * g) : floatx4{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    const floatx4 b = bv[ft];
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      floatx4 x = BIAS ? acc[ft][sg] * f + b : acc[ft][sg] * f;
+      x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
+      v[ft][sg] = x;
+      mx = fmaxf(fmaxf(mx, x.x), fmaxf(fmaxf(x.y, x.z), x.w));
+    }
+  }
+  return wave_max(mx);
+}
+
+// X <- split(v * s_x) for this wave's feature tiles
+template <int FT>
+__device__ __forceinline__ void store_split(uint4* X16, const floatx4 (&v)[FT][4], float s_x, int wid, int g, int j) {
+  char* base = reinterpret_cast<char*>(X16);
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    const int ftg = FT * wid + ft;
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      uint2 hi, lo;
+      split4(v[ft][sg], s_x, hi, lo);
+      const int s = 16 * sg + j;
+      *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 0, g, s) * 16 + (ftg & 1) * 8) = hi;
+      *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 1, g, s) * 16 + (ftg & 1) * 8) = lo;
+    }
+  }
+}
+
+__device__ __forceinline__ float layer_scale(const float* packed, const Layout& L, int layer) {
+  return pow2_scale_for(__uint_as_float(reinterpret_cast<const unsigned*>(packed + L.x3_hdr)[layer]));
+}
+
+template <int NW>
+__device__ __forceinline__ float red_max(const float* red) {
+  float m = red[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w]);
+  return m;
+}
+
+// relu'd layer input -> LDS (two barriers: all reads of the previous X done /
+// all writes of the new X visible); returns the operand scale s_x
+template <int FT, int NW>
+__device__ __forceinline__ float publish(uint4* X16, const floatx4 (&v)[FT][4], float mx, float* red, int wid,
+                                         int lane, int g, int j) {
+  if (lane == 0) red[wid] = mx;
+  lds_barrier();
+  const float s_x = pow2_scale_for(red_max<NW>(red));
+  store_split<FT>(X16, v, s_x, wid, g, j);
+  lds_barrier();
+  return s_x;
+}
+
+}  // namespace avr

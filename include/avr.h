@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 2
+#define AVR_ABI_VERSION 3
 #define AVR_MAX_BLOCKS 8
 
 enum {
@@ -189,6 +189,35 @@ int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_desc* view, co
 int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
                          const float* table, const float* xyz, const float* viewdirs, int64_t n_points,
                          float* out, void* stream);
+
+/* ---------------------------------------------------------- field training
+ * Autograd of NewPixelNeRFNet.forward for train.py:108-114 (loss.backward()
+ * through the ResnetFC: models.py:541-592, :454-470, :856-862), on the x3
+ * path (dims->precision must be AVR_FIELD_X3).
+ *
+ * Forward: avr_field_fwd_points_train = avr_field_fwd_points that also writes
+ *   act  (2 n_blocks + 1, n_points, d_hidden) fp32: the relu'd input of every
+ *        hidden GEMM, act[2b] = relu(x) into fc_0 of block b, act[2b+1] =
+ *        relu(fc_0 out) into fc_1, act[2 n_blocks] = relu(x) into lin_out;
+ *   mask (mask_words) their relu masks (opaque, read by avr_field_bwd).
+ * Backward: avr_field_bwd, given the forward's out and d loss / d out
+ * (n_points, 4), writes grads (2 n_blocks + 1, n_points, d_hidden):
+ *   grads[2b]   = d loss / d fc_0[b] output (pre-relu),
+ *   grads[2b+1] = d loss / d fc_1[b] output,
+ *   grads[2 n_blocks] = d loss / d lin_in output.
+ * so that dW = grads[l]^T act[l] and db = column sums of grads[l] (fc layers;
+ * lin_in with the MLP input, lin_z[b] with the interpolated latent and
+ * grads[2b-1] (b >= 1) or grads[2 n_blocks] (b = 0), the gradient at block
+ * b's input). packed_bwd: avr_field_bwd_packed_floats floats, filled by
+ * avr_field_pack_bwd (fc_0 / fc_1 transposed, x3 fragments).                    */
+int avr_field_train_sizes(const avr_field_dims* dims, int64_t n_points, int64_t* act_floats, int64_t* mask_words);
+int avr_field_bwd_packed_floats(const avr_field_dims* dims, int64_t* n_floats);
+int avr_field_pack_bwd(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed_bwd, void* stream);
+int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
+                               const float* table, const float* xyz, const float* viewdirs, int64_t n_points,
+                               float* out, float* act, uint32_t* mask, void* stream);
+int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd, const float* out,
+                  const float* grad_out, const uint32_t* mask, int64_t n_points, float* grads, void* stream);
 
 /* --------------------------------------------------------- LSTM ray marcher
  * Raymarcher / AdaptiveVolumeRenderer march (renderers.py:313-351, :380-432):
