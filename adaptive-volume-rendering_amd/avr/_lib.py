@@ -43,6 +43,15 @@ class ViewDesc(ctypes.Structure):
                 ("latent_scaling", c_float * 2), ("latent_h", c_int), ("latent_w", c_int)]
 
 
+AVR_WGRAD_MAX_LAYERS = 16
+
+
+class WGradLayer(ctypes.Structure):
+    _fields_ = [("grad", c_void_p), ("ld_grad", i64), ("input", c_void_p), ("ld_input", i64),
+                ("out_dim", c_int), ("in_dim", c_int), ("grad_max", c_void_p), ("input_max", c_void_p),
+                ("partial", c_void_p), ("bias_partial", c_void_p)]
+
+
 # name -> argtypes (all return int status)
 _SIGS = {
     "avr_world_rays": [c_void_p, c_void_p, c_void_p, i64, i64, i64, i64, c_void_p, c_void_p, c_void_p],
@@ -75,9 +84,10 @@ _SIGS = {
     "avr_field_bwd_packed_floats": [ctypes.POINTER(FieldDims), ctypes.POINTER(i64)],
     "avr_field_pack_bwd": [ctypes.POINTER(FieldDims), ctypes.POINTER(ResnetFCWeights), c_void_p, c_void_p],
     "avr_field_fwd_points_train": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
-                                   c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p],
+                                   c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "avr_field_bwd": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p,
-                      c_void_p],
+                      i64, c_void_p, c_void_p],
+    "avr_weight_grads": [ctypes.POINTER(WGradLayer), c_int, i64, c_int, c_void_p],
 }
 EXPORTED = ("avr_version", "avr_last_error_string", "avr_device_count") + tuple(_SIGS)
 

@@ -235,14 +235,16 @@ class _FieldTrain(torch.autograd.Function):
     loss.backward() (train.py:108-114).
 
     forward: avr_field_fwd_points_train per scene (x3 MFMA, the inference
-    kernel plus a store of every hidden GEMM input and its relu mask).
-    backward: avr_field_bwd runs the input-gradient chain (lin_out^T, then
-    fc_1^T / fc_0^T per block with the relu masks, x3 MFMA) and writes the
-    gradient at every layer output; the weight gradients are then plain GEMMs
-    over the samples, dW = G^T act (hipBLASLt through torch.mm), and the biases
-    column sums. lin_z[b] differentiates against the interpolated latent
-    (grid_sample, as models.py:266-273), and the latent map gets the
-    grid_sample adjoint of sum_b G_z[b] W_z[b] when it requires grad."""
+    kernel plus a store of every hidden GEMM input, its relu mask and the
+    layer's running max) into one (layers, SB * B, d_hidden) buffer.
+    backward: avr_field_bwd runs the input-gradient chain per scene (lin_out^T,
+    then fc_1^T / fc_0^T per block with the relu masks, x3 MFMA) and writes the
+    gradient at every layer output; avr_weight_grads then forms every weight
+    and bias gradient in one batched split-K x3 GEMM over all samples
+    (fc_0 / fc_1 against the saved inputs, lin_z against the interpolated latent
+    (grid_sample, models.py:266-273), lin_in against the positional-encoded
+    input). The latent map gets the grid_sample adjoint of sum_b G_z[b] W_z[b]
+    when it requires grad."""
 
     @staticmethod
     def forward(ctx, fused, coarse, names, xyz, viewdirs, latent, *params):
@@ -251,78 +253,95 @@ class _FieldTrain(torch.autograd.Function):
         dims = entry.dims
         dims.precision = _lib.FIELD_X3
         H, nb = dims.d_hidden, dims.n_blocks
+        n_l, Mt = 2 * nb + 1, SB * B
         act_n, mask_n = ctypes.c_int64(0), ctypes.c_int64(0)
         _lib.check(_lib.load().avr_field_train_sizes(ctypes.byref(dims), B, ctypes.byref(act_n), ctypes.byref(mask_n)),
                    "avr_field_train_sizes")
-        out = torch.empty(SB, B, 4, device=xyz.device, dtype=F32)
-        acts, masks = [], []
+        dev = xyz.device
+        out = torch.empty(SB, B, 4, device=dev, dtype=F32)
+        act = torch.empty(n_l, Mt, H, device=dev, dtype=F32)
+        act_max = torch.zeros(n_l, device=dev, dtype=torch.int32)
+        masks = []
         vd = viewdirs.reshape(SB, B, 3)
         for sb in range(SB):
             p = xyz[sb].detach().to(F32).contiguous()
             v = vd[sb].detach().to(F32).contiguous()
             require_device(p, v)
-            act = torch.empty(2 * nb + 1, B, H, device=xyz.device, dtype=F32)
-            mask = torch.empty(max(mask_n.value, 1), device=xyz.device, dtype=torch.int32)
+            mask = torch.empty(max(mask_n.value, 1), device=dev, dtype=torch.int32)
             call("avr_field_fwd_points_train", ctypes.byref(dims), ctypes.byref(fused.view(sb)), ptr(entry.packed),
-                 ptr(fused.table(coarse, sb)), ptr(p), ptr(v), B, ptr(out[sb]), ptr(act), ptr(mask), stream_of(p))
-            acts.append(act)
+                 ptr(fused.table(coarse, sb)), ptr(p), ptr(v), B, ptr(out[sb]),
+                 ctypes.c_void_p(act.data_ptr() + sb * B * H * 4), Mt, ptr(mask), ptr(act_max), stream_of(p))
             masks.append(mask)
         entry.dims.precision = PRECISIONS[fused.precision]
         ctx.fused, ctx.coarse, ctx.names, ctx.entry = fused, coarse, names, entry
-        ctx.acts, ctx.masks = acts, masks
+        ctx.act, ctx.act_max, ctx.masks = act, act_max, masks
         ctx.save_for_backward(xyz, viewdirs, latent, out, *params)
         return out
 
     @staticmethod
     def backward(ctx, grad_out):
+        from .ops import _max_bits, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         fused, entry, names = ctx.fused, ctx.entry, ctx.names
         net = fused.net
         P = dict(zip(names, params))
         dims = entry.dims
-        dims.precision = _lib.FIELD_X3
         H, nb, nz = dims.d_hidden, dims.n_blocks, dims.n_lin_z
         SB, B, _ = xyz.shape
-        bwd = fused.packed_bwd(ctx.coarse, entry)
-        grad_out = grad_out.to(F32).contiguous()
+        n_l, Mt = 2 * nb + 1, SB * B
         want_latent = ctx.needs_input_grad[5] and not net.stop_encoder_grad
         if B == 0:
             zeros = tuple(torch.zeros_like(p) if ctx.needs_input_grad[6 + i] else None for i, p in enumerate(params))
             return (None, None, None, None, None, torch.zeros_like(latent) if want_latent else None) + zeros
-        # MLP inputs the weight gradients contract against (the same torch code as forward_torch)
+        dev = xyz.device
+        dims.precision = _lib.FIELD_X3
+        bwd = fused.packed_bwd(ctx.coarse, entry)
+        grad_out = grad_out.to(F32).contiguous()
+        G = torch.empty(n_l, Mt, H, device=dev, dtype=F32)
+        g_max = torch.zeros(n_l, device=dev, dtype=torch.int32)
+        for sb in range(SB):
+            call("avr_field_bwd", ctypes.byref(dims), ptr(entry.packed), ptr(bwd), ptr(out[sb]), ptr(grad_out[sb]),
+                 ptr(ctx.masks[sb]), B, ctypes.c_void_p(G.data_ptr() + sb * B * H * 4), Mt, ptr(g_max), stream_of(G))
+        entry.dims.precision = PRECISIONS[fused.precision]
+        act, act_max = ctx.act, ctx.act_max
+        ctx.act = ctx.act_max = ctx.masks = None
+        # MLP inputs the lin_z / lin_in gradients contract against (forward_torch's code)
         with torch.no_grad():
             lat_feat, z_feature = net.mlp_inputs(xyz.detach(), viewdirs.detach())
-        grads = {n: torch.zeros_like(P[n]) for n in names}
-        dZ = torch.zeros(SB * B, net.d_latent, device=xyz.device, dtype=F32) if want_latent else None
-        for sb in range(SB):
-            G = torch.empty(2 * nb + 1, B, H, device=xyz.device, dtype=F32)
-            go = grad_out[sb].contiguous()
-            call("avr_field_bwd", ctypes.byref(dims), ptr(entry.packed), ptr(bwd), ptr(out[sb]), ptr(go),
-                 ptr(ctx.masks[sb]), B, ptr(G), stream_of(G))
-            act = ctx.acts[sb]
-            y = out[sb]
-            d4 = torch.cat([go[:, :3] * ((1.0 - y[:, :3]) * y[:, :3]), go[:, 3:] * (y[:, 3:] > 0)], -1)
-            grads["lin_out.weight"] += d4.t() @ act[2 * nb]
-            grads["lin_out.bias"] += d4.sum(0)
-            for b in range(nb):
-                grads[f"blocks.{b}.fc_0.weight"] += G[2 * b].t() @ act[2 * b]
-                grads[f"blocks.{b}.fc_0.bias"] += G[2 * b].sum(0)
-                grads[f"blocks.{b}.fc_1.weight"] += G[2 * b + 1].t() @ act[2 * b + 1]
-                grads[f"blocks.{b}.fc_1.bias"] += G[2 * b + 1].sum(0)
-            rows = slice(sb * B, (sb + 1) * B)
-            grads["lin_in.weight"] += G[2 * nb].t() @ z_feature[rows]
-            grads["lin_in.bias"] += G[2 * nb].sum(0)
-            for b in range(nz):
-                Gz = G[2 * b - 1] if b > 0 else G[2 * nb]
-                grads[f"lin_z.{b}.weight"] += Gz.t() @ lat_feat[rows]
-                grads[f"lin_z.{b}.bias"] += Gz.sum(0)
-                if dZ is not None:
-                    dZ[rows] += Gz @ P[f"lin_z.{b}.weight"].detach()
-            del G
-        ctx.acts = ctx.masks = None
-        entry.dims.precision = PRECISIONS[fused.precision]
+            d_in = z_feature.shape[1]
+            zf = torch.nn.functional.pad(z_feature.to(F32), (0, (-d_in) % 4)).contiguous()
+            lat_feat = lat_feat.to(F32).contiguous()
+        lat_max = _max_bits(latent)          # |interpolated latent| <= max |latent| (convex blend)
+        zf_max = _max_bits(zf)
+        Gz = [G[2 * b - 1] if b > 0 else G[2 * nb] for b in range(nz)]
+        layers = []
+        for b in range(nb):
+            layers.append((G[2 * b], act[2 * b], g_max[2 * b:2 * b + 1], act_max[2 * b:2 * b + 1], True))
+            layers.append((G[2 * b + 1], act[2 * b + 1], g_max[2 * b + 1:2 * b + 2], act_max[2 * b + 1:2 * b + 2], True))
+        for b in range(nz):
+            gi = 2 * b - 1 if b > 0 else 2 * nb
+            layers.append((Gz[b], lat_feat, g_max[gi:gi + 1], lat_max, False))
+        layers.append((G[2 * nb], zf, g_max[2 * nb:2 * nb + 1], zf_max, True))
+        # lin_out (4 outputs): d out through sigmoid / relu (torch: g * (1 - y) * y, g * (y > 0))
+        y = out.reshape(Mt, 4)
+        go = grad_out.reshape(Mt, 4)
+        d4 = torch.cat([go[:, :3] * ((1.0 - y[:, :3]) * y[:, :3]), go[:, 3:] * (y[:, 3:] > 0)], -1).contiguous()
+        layers.append((d4, act[2 * nb], _max_bits(d4), act_max[2 * nb:2 * nb + 1], True))
+        res = weight_grads(layers, Mt)
+        grads = {"lin_out.weight": res[-1][0], "lin_out.bias": res[-1][1]}
+        res = res[:-1]
+        for b in range(nb):
+            grads[f"blocks.{b}.fc_0.weight"], grads[f"blocks.{b}.fc_0.bias"] = res[2 * b]
+            grads[f"blocks.{b}.fc_1.weight"], grads[f"blocks.{b}.fc_1.bias"] = res[2 * b + 1]
+        for b in range(nz):
+            grads[f"lin_z.{b}.weight"] = res[2 * nb + b][0]
+            # lin_z[b]'s output gradient is the gradient at block b's input
+            grads[f"lin_z.{b}.bias"] = res[2 * b - 1][1] if b > 0 else res[-1][1]
+        w_in, b_in = res[-1]
+        grads["lin_in.weight"], grads["lin_in.bias"] = w_in[:, :d_in].contiguous(), b_in
         d_latent = None
-        if dZ is not None:
+        if want_latent:
+            dZ = sum(Gz[b] @ P[f"lin_z.{b}.weight"].detach() for b in range(nz))
             with torch.enable_grad():
                 lat = latent.detach().requires_grad_(True)
                 feat, _ = net.mlp_inputs(xyz.detach(), viewdirs.detach(), latent=lat)

@@ -299,13 +299,20 @@ class NewPixelNeRFNet(nn.Module):
         """(latent features (SB*B, d_latent), z_feature (SB*B, d_in)) at the
         points: the MLP input halves of models.py:753-823 (forward_torch's code;
         `latent` overrides the encoder's map, for its gradient)."""
-        return self._inputs(xyz, viewdirs, latent)[:2]
+        return self._inputs(xyz, viewdirs, latent, batched_rot=True)[:2]
 
-    def _inputs(self, xyz, viewdirs, latent_map=None):
+    def _inputs(self, xyz, viewdirs, latent_map=None, batched_rot=False):
         SB, B, _ = xyz.shape
         NS = self.num_views_per_obj
         xyz = repeat_interleave(xyz, NS)
-        xyz_rot = torch.matmul(self.poses[:, None, :3, :3], xyz.unsqueeze(-1))[..., 0]
+        rot = self.poses[:, :3, :3]
+
+        def rotate(v):   # R v per point: the reference's per-point (3x3)(3x1) matmul, or one bmm per scene
+            if batched_rot and NS == 1 and rot.shape[0] == v.shape[0]:
+                return torch.bmm(v, rot.transpose(1, 2))
+            return torch.matmul(rot[:, None], v.unsqueeze(-1))[..., 0]
+
+        xyz_rot = rotate(xyz)
         xyz = xyz_rot + self.poses[:, None, :3, 3]
         z_feature = latent = None
         if self.d_in > 0:
@@ -316,8 +323,8 @@ class NewPixelNeRFNet(nn.Module):
             if self.use_code and not self.use_code_viewdirs:
                 z_feature = self.code(z_feature)
             if self.use_viewdirs:
-                vd = repeat_interleave(viewdirs.reshape(SB, B, 3, 1), NS)
-                vd = torch.matmul(self.poses[:, None, :3, :3], vd).reshape(-1, 3)
+                vd = repeat_interleave(viewdirs.reshape(SB, B, 3), NS)
+                vd = rotate(vd).reshape(-1, 3)
                 z_feature = torch.cat((z_feature, vd), dim=1)
             if self.use_code and self.use_code_viewdirs:
                 z_feature = self.code(z_feature)

@@ -255,3 +255,59 @@ def raymarch(view, gate_table, lstm, out_layer, ro, rd, init_dist, steps, trace=
     call("avr_raymarch", ctypes.byref(view), *[ptr(t) for t in ps], ptr(ro), ptr(rd), ptr(d0), R, int(steps),
          ptr(world), ptr(fd), ptr(tr), stream_of(ro))
     return (world, fd, tr) if trace else (world, fd)
+
+
+def _max_bits(t):
+    """max |t| as a one-element int32 device tensor of float bits (avr_weight_grads' scale input)."""
+    return t.detach().abs().amax().reshape(1).to(torch.float32).view(torch.int32)
+
+
+def _wgrad_splits(tiles, n_rows, dev):
+    """K-split of avr_weight_grads: the grid (tiles x splits workgroups, two per
+    CU) should end in full rounds, with K-ranges of at least 2048 rows."""
+    slots = 2 * torch.cuda.get_device_properties(dev).multi_processor_count
+    best, best_eff = 1, 0.0
+    for n in range(1, 65):
+        if n > 1 and n_rows < 2048 * n:
+            break
+        w = n * tiles
+        eff = w / (-(-w // slots) * slots) * min(1.0, w / slots)
+        if eff >= 0.95:
+            return n      # the fewest splits (partials) that fill the rounds
+        if eff > best_eff + 1e-3:
+            best, best_eff = n, eff
+    return best
+
+
+def weight_grads(layers, n_rows, n_split=None):
+    """dW = G^T X and db = colsum(G) for each (grad, input, grad_max, input_max, want_bias)
+    of `layers` (avr_weight_grads: split-K x3 MFMA). grad (n_rows, out) / input
+    (n_rows, in) fp32 row-major (row strides may exceed the widths); *_max: int32
+    (1,) float bits of max |.|. Returns [(dW (out, in), db (out,) or None)]."""
+    if not layers:
+        return []
+    dev = layers[0][0].device
+    if n_rows == 0:
+        return [(torch.zeros(g.shape[1], x.shape[1], device=dev), torch.zeros(g.shape[1], device=dev) if wb else None)
+                for g, x, _, _, wb in layers]
+    tiles = sum(-(-g.shape[1] // 128) * -(-x.shape[1] // 128) for g, x, *_ in layers)
+    if n_split is None:
+        n_split = _wgrad_splits(tiles, n_rows, dev)
+    out = []
+    for base in range(0, len(layers), _lib.AVR_WGRAD_MAX_LAYERS):
+        chunk = layers[base:base + _lib.AVR_WGRAD_MAX_LAYERS]
+        arr = (_lib.WGradLayer * len(chunk))()
+        keep = []
+        for k, (g, x, gmax, xmax, want_bias) in enumerate(chunk):
+            O, I = g.shape[1], x.shape[1]
+            for t in (g, x):
+                if t.dtype != torch.float32 or t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+                    raise _lib.AVRError("weight_grads: operands must be fp32 rows, 16-B aligned, unit column stride")
+            part = torch.empty(n_split, O, I, device=dev, dtype=torch.float32)
+            bpart = torch.empty(n_split, O, device=dev, dtype=torch.float32) if want_bias else None
+            arr[k] = _lib.WGradLayer(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), O, I, gmax.data_ptr(),
+                                     xmax.data_ptr(), part.data_ptr(), 0 if bpart is None else bpart.data_ptr())
+            keep.append((part, bpart))
+        call("avr_weight_grads", arr, len(chunk), n_rows, n_split, stream_of(layers[0][0]))
+        out += [(p.sum(0), None if b is None else b.sum(0)) for p, b in keep]
+    return out

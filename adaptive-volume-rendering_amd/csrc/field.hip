@@ -491,25 +491,29 @@ extern "C" int avr_field_train_sizes(const avr_field_dims* dims, int64_t n_point
 
 extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
                                           const float* table, const float* xyz, const float* viewdirs,
-                                          int64_t n_points, float* out, float* act, uint32_t* mask, void* stream) {
+                                          int64_t n_points, float* out, float* act, int64_t act_rows,
+                                          uint32_t* mask, uint32_t* act_max, void* stream) {
   FieldArgs a{};
   int rc = field_common(dims, view, packed, table, &a);
   if (rc) return rc;
   AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_fwd_points_train: the training path is x3 only");
   AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points_train: bad size");
   AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && out && act && mask), "avr_field_fwd_points_train: null pointer");
+  AVR_REQUIRE(act_rows >= n_points, "avr_field_fwd_points_train: act_rows < n_points");
   a.xyz = xyz; a.vd = viewdirs; a.n_samples = 1;
   a.M = n_points;
   a.out = reinterpret_cast<float4*>(out);
   a.act = act;
+  a.act_stride = act_rows * dims->d_hidden;
   a.mask = mask;
+  a.act_max = act_max;
   if (a.M == 0) return AVR_OK;
   return dispatch_field_x3(dims->d_hidden, a, as_stream(stream));
 }
 
 extern "C" int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd,
                              const float* out, const float* grad_out, const uint32_t* mask, int64_t n_points,
-                             float* grads, void* stream) {
+                             float* grads, int64_t grads_rows, uint32_t* grads_max, void* stream) {
   BwdArgs a{};
   int rc = make_layout(dims, &a.L);
   if (rc) return rc;
@@ -517,6 +521,7 @@ extern "C" int avr_field_bwd(const avr_field_dims* dims, const float* packed, co
   AVR_REQUIRE(n_points >= 0, "avr_field_bwd: bad size");
   if (n_points == 0) return AVR_OK;
   AVR_REQUIRE(packed && packed_bwd && out && grad_out && mask && grads, "avr_field_bwd: null pointer");
+  AVR_REQUIRE(grads_rows >= n_points, "avr_field_bwd: grads_rows < n_points");
   make_bwd_layout(dims, &a.LB);
   a.packed = packed;
   a.packed_bwd = packed_bwd;
@@ -526,6 +531,8 @@ extern "C" int avr_field_bwd(const avr_field_dims* dims, const float* packed, co
   a.grad_out = reinterpret_cast<const float4*>(grad_out);
   a.mask = mask;
   a.G = grads;
+  a.g_stride = grads_rows * dims->d_hidden;
+  a.g_max = grads_max;
   return dispatch_field_bwd_x3(dims->d_hidden, a, as_stream(stream));
 }
 

@@ -55,6 +55,14 @@ __device__ __forceinline__ void store_rows(float* G, const floatx4 (&v)[FT][4], 
     }
 }
 
+// layer l's rows + its running max |G| (mx: the wave's max |v|)
+template <int FT, int NW>
+__device__ __forceinline__ void store_layer(const BwdArgs& a, int layer, const floatx4 (&v)[FT][4], float mx,
+                                            int64_t base, int wid, int g, int j, int lane) {
+  store_rows<FT, NW>(a.G + layer * a.g_stride, v, base, a.M, wid, g, j);
+  if (a.g_max && lane == 0) atomicMax(a.g_max + layer, __float_as_uint(mx));
+}
+
 template <int FT>
 __device__ __forceinline__ float absmax(const floatx4 (&v)[FT][4]) {
   float mx = 0.f;
@@ -84,7 +92,6 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, j = lane & 15;
   const int64_t base = (int64_t)blockIdx.x * kX3Samples;
-  const int64_t HM = a.M * HID;
   const int nb = a.n_blocks;
   const uint4* PB = reinterpret_cast<const uint4*>(a.packed_bwd);
 
@@ -121,10 +128,11 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   FragX3 A0[FT];
   for (int b = nb - 1; b >= 0; --b) {
     // ---- fc_1^T
-    store_rows<FT, NW>(a.G + (2 * b + 1) * HM, dx, base, a.M, wid, g, j);
+    float mx = absmax<FT>(dx);
+    store_layer<FT, NW>(a, 2 * b + 1, dx, mx, base, wid, g, j, lane);
     const uint4* W1 = PB + a.LB.fc1t[b] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W1, lane);
-    float s_x = publish<FT, NW>(X16, dx, absmax<FT>(dx), red, wid, lane, g, j);
+    float s_x = publish<FT, NW>(X16, dx, mx, red, wid, lane, g, j);
     load_mask<FT, NW>(mb, a.mask, 2 * b + 1, lane, wid);
     gemm_x3<FT, true, false>(t, A0, W1, KC, 64 * NTT, X16, lane);
     float inv = 1.0f / (bwd_scale(a.packed_bwd, 3 + 2 * b) * s_x);
@@ -132,11 +140,12 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
       for (int sg = 0; sg < 4; ++sg) t[ft][sg] = masked<FT>(t[ft][sg] * inv, mb, ft, sg);
-    store_rows<FT, NW>(a.G + 2 * b * HM, t, base, a.M, wid, g, j);
+    mx = absmax<FT>(t);
+    store_layer<FT, NW>(a, 2 * b, t, mx, base, wid, g, j, lane);
     // ---- fc_0^T
     const uint4* W0 = PB + a.LB.fc0t[b] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W0, lane);
-    s_x = publish<FT, NW>(X16, t, absmax<FT>(t), red, wid, lane, g, j);
+    s_x = publish<FT, NW>(X16, t, mx, red, wid, lane, g, j);
     load_mask<FT, NW>(mb, a.mask, 2 * b, lane, wid);
     gemm_x3<FT, true, false>(t, A0, W0, KC, 64 * NTT, X16, lane);
     inv = 1.0f / (bwd_scale(a.packed_bwd, 2 + 2 * b) * s_x);
@@ -145,7 +154,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
 #pragma unroll
       for (int sg = 0; sg < 4; ++sg) dx[ft][sg] += masked<FT>(t[ft][sg] * inv, mb, ft, sg);
   }
-  store_rows<FT, NW>(a.G + 2 * nb * HM, dx, base, a.M, wid, g, j);
+  store_layer<FT, NW>(a, 2 * nb, dx, absmax<FT>(dx), base, wid, g, j, lane);
 }
 
 template <int FT, int NW>

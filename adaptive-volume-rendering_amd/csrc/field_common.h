@@ -78,8 +78,10 @@ struct FieldArgs {
   const float* xyz; const float* vd;
   int64_t M;
   float4* out;
-  float* act;                  // training forward: GEMM inputs, (2 n_blocks + 1, M, d_hidden) fp32, or null
-  unsigned* mask;              //   and their relu masks (see mask_words)
+  float* act;                  // training forward: GEMM inputs, layer l at act + l * act_stride, (M, d_hidden)
+  int64_t act_stride;          //   floats between layers
+  unsigned* mask;              //   their relu masks (see mask_words)
+  unsigned* act_max;           //   per-layer max |act| as float bits (atomicMax), or null
   unsigned long long* stamps;  // diagnostic builds (-DAVR_STAMPS) only: per-block phase clocks (waves 0, 4)
   int debug;                   // diagnostic builds only: experiment flags (1: every fc layer uses block 0's weights)
 };
@@ -238,7 +240,9 @@ struct BwdArgs {
   const float4* out;        // field output (sigmoid rgb, relu sigma)
   const float4* grad_out;
   const unsigned* mask;
-  float* G;                 // (2 n_blocks + 1, M, d_hidden) layer-output gradients
+  float* G;                 // layer-output gradients, layer l at G + l * g_stride, (M, d_hidden)
+  int64_t g_stride;
+  unsigned* g_max;          // per-layer max |G| as float bits (atomicMax), or null
 };
 
 int dispatch_field_bwd_x3(int d_hidden, const BwdArgs& a, hipStream_t s);

@@ -180,11 +180,14 @@ struct LdsPlan {
 
 // Training forward: GEMM input `layer` (relu'd, true scale) -> act rows and
 // its relu mask bits -> mask (both consumed by the backward pass).
+// mx: the wave's max of v (v >= 0), folded into the layer's max for the
+// weight-gradient split scales.
 template <int FT, int NW>
-__device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const floatx4 (&v)[FT][4], int64_t base,
-                                           int wid, int g, int j, int lane) {
+__device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const floatx4 (&v)[FT][4], float mx,
+                                           int64_t base, int wid, int g, int j, int lane) {
   constexpr int HID = 16 * FT * NW, MW = mask_words(FT);
-  float* act = a.act + (int64_t)layer * a.M * HID;
+  float* act = a.act + (int64_t)layer * a.act_stride;
+  if (a.act_max && lane == 0) atomicMax(a.act_max + layer, __float_as_uint(mx));
   unsigned bits[MW];
 #pragma unroll
   for (int q = 0; q < MW; ++q) bits[q] = 0u;
@@ -351,7 +354,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
     }
     AVR_STAMP(5 + 5 * (b & 3));
-    if (SAVE) save_layer<FT, NW>(a, 2 * b, v, base, wid, g, j, lane);
+    if (SAVE) save_layer<FT, NW>(a, 2 * b, v, mx, base, wid, g, j, lane);
     const uint4* W0 = P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W0, lane);
     s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
@@ -362,7 +365,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     AVR_STAMP(7 + 5 * (b & 3));
     // fc_1 input relu(t + b0)
     mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
-    if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, base, wid, g, j, lane);
+    if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, mx, base, wid, g, j, lane);
     const uint4* W1 = P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W1, lane);
     s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
@@ -395,7 +398,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     for (int c = 0; c < KC / 4; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
   }
   mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
-  if (SAVE) save_layer<FT, NW>(a, 2 * a.n_blocks, v, base, wid, g, j, lane);
+  if (SAVE) save_layer<FT, NW>(a, 2 * a.n_blocks, v, mx, base, wid, g, j, lane);
   s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
   if (wid < 4) {
 #pragma unroll

@@ -1,0 +1,234 @@
+// Weight gradients of the field's linear layers (the dW = G^T X, db = sum G
+// half of autograd through nn.Linear, models.py:541-592) as one batched
+// split-K GEMM on split-fp16 MFMA. For every layer l and K-range k of the
+// samples:
+//   partial[l][k][o][i]   = sum_{m in k} G_l[m][o] * X_l[m][i]
+//   bias_partial[l][k][o] = sum_{m in k} G_l[m][o]
+// G (gradient at the layer output) and X (the layer input) are fp32 rows, one
+// per sample, as the training forward / backward kernels write them.
+//
+// The contraction runs over the ROW index of both operands, so the MFMA
+// operands are k-strided in memory: each workgroup stages 32-sample chunks of
+// its 128-column G and X slices in LDS as row-major fp16 hi/lo images
+// (XOR-swizzled 256-B rows) and reads the A and B fragments of
+// v_mfma_f32_16x16x32_f16 with gfx950's transposing ds_read_b64_tr_b16.
+// Products are W-split x3 (Gh.Xh + Gh.Xl + Gl.Xh, fp32 accumulate) under
+// per-layer power-of-two scales from the max |G| / |X| the producing kernels
+// tracked, the same arithmetic as the forward's GEMMs.
+//
+// Work split: workgroup = one 128 x 128 output tile of one layer over one
+// K-range; 4 waves of 64 x 64 (4 x 4 MFMA tiles). Consecutive workgroups on
+// one XCD take the tiles of the same K-range, so the G / X rows they share are
+// read from that XCD's L2.
+#include "x3_gemm.h"
+
+namespace avr {
+
+constexpr int kDwTile = 128;
+constexpr int kDwK = 32;
+constexpr int kDwImg = kDwK * kDwTile * 2;   // bytes of one fp16 image (32 rows x 256 B)
+constexpr int kDwStage = 4 * kDwImg;         // G hi, G lo, X hi, X lo
+
+struct DwLayerDev {
+  const float* g;
+  const float* x;
+  int64_t ldg, ldx;
+  int O, I, nIt, tile0;
+  const unsigned* gmax;
+  const unsigned* xmax;
+  float* part;
+  float* bpart;
+};
+
+struct DwArgs {
+  DwLayerDev L[AVR_WGRAD_MAX_LAYERS];
+  int n_layers, tiles, ksplit;
+  int64_t M, kper;
+};
+
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+typedef __attribute__((address_space(3))) char lds_char;
+
+// byte offset of 16-B chunk ch (0..15) of row r in a 256-B-row image (XOR swizzle:
+// conflict-free transposed reads, cdna_hip_programming.md T10 image (b))
+__device__ __forceinline__ int img_off(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+
+// MFMA operand fragment of 16 columns col0 .. col0+15 of an image: lane l
+// (g = l >> 4, i = l & 15) gets column col0 + i, rows 8g .. 8g+7 (element j =
+// row 8g + j, the natural k order of v_mfma_f32_16x16x32_f16 for A and B).
+__device__ __forceinline__ half8 tr_frag(const lds_char* img, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int ch = (col0 >> 3) + (p >> 1), sub = 8 * (p & 1);
+  typedef __attribute__((address_space(3))) short4_t lds_short4;
+  const short4_t r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(img + img_off(8 * g + q, ch) + sub));
+  const short4_t r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(img + img_off(8 * g + 4 + q, ch) + sub));
+  const short4_t both[2] = {r0, r1};
+  return __builtin_bit_cast(half8, both);
+}
+
+__global__ void __launch_bounds__(256, 2) weight_grad_kernel(DwArgs a) {
+  extern __shared__ float lds_f[];
+  lds_char* lds = (lds_char*)lds_f;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // XCD-aware order: blocks b = x, x+8, ... run on XCD x; give them consecutive logical indices
+  const int nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
+  const int lg = x * per + (x < rem ? x : rem) + (b >> 3);
+  const int krange = lg / a.tiles, tile = lg - krange * a.tiles;
+  int l = 0;
+  while (l + 1 < a.n_layers && tile >= a.L[l + 1].tile0) ++l;
+  const DwLayerDev D = a.L[l];   // one copy in SGPRs (the fields are read in the loop)
+  const int local = tile - D.tile0, ot = local / D.nIt, it = local - ot * D.nIt;
+  const int o0 = ot * kDwTile, i0 = it * kDwTile;
+  const int64_t k0 = (int64_t)krange * a.kper;
+  const int64_t k1 = k0 + a.kper < a.M ? k0 + a.kper : a.M;
+  const int nch = k1 > k0 ? (int)((k1 - k0 + kDwK - 1) / kDwK) : 0;
+  const float sG = pow2_scale_for(__uint_as_float(*D.gmax)), sX = pow2_scale_for(__uint_as_float(*D.xmax));
+  const bool bias = D.bpart && it == 0;
+
+  // staging: thread -> 4-column group cc, rows rb + 8u
+  const int cc = threadIdx.x & 31, rb = threadIdx.x >> 5;
+  const bool gcol = o0 + 4 * cc < D.O, xcol = i0 + 4 * cc < D.I;
+  const float* gp = D.g + o0 + 4 * cc;
+  const float* xp = D.x + i0 + 4 * cc;
+  floatx4 bsum = {0.f, 0.f, 0.f, 0.f};
+  const auto load = [&](int c, floatx4 (&gv)[4], floatx4 (&xv)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t m = k0 + (int64_t)kDwK * c + rb + 8 * u;
+      const bool ok = m < k1;
+      gv[u] = ok && gcol ? *reinterpret_cast<const floatx4*>(gp + m * D.ldg) : floatx4{0.f, 0.f, 0.f, 0.f};
+      xv[u] = ok && xcol ? *reinterpret_cast<const floatx4*>(xp + m * D.ldx) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  const int wo = wid >> 1, wi = wid & 1;
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[t][u] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // One chunk: its registers -> LDS stage c & 1 (split), barrier, the loads of
+  // chunk c + 2 into the same registers (two chunks of MFMAs to land), MFMAs.
+  // Stage c & 1 was last read in chunk c - 2, which every wave finished before
+  // the barrier of chunk c - 1.
+  const auto step = [&](int c, floatx4 (&gv)[4], floatx4 (&xv)[4]) {
+    lds_char* st = lds + (c & 1) * kDwStage;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = rb + 8 * u, off = img_off(r, cc >> 1) + 8 * (cc & 1);
+      uint2 hi, lo;
+      split4(gv[u], sG, hi, lo);
+      *(lds_u32x2*)(st + off) = u32x2{hi.x, hi.y};
+      *(lds_u32x2*)(st + kDwImg + off) = u32x2{lo.x, lo.y};
+      split4(xv[u], sX, hi, lo);
+      *(lds_u32x2*)(st + 2 * kDwImg + off) = u32x2{hi.x, hi.y};
+      *(lds_u32x2*)(st + 3 * kDwImg + off) = u32x2{lo.x, lo.y};
+      if (bias) bsum += gv[u];
+    }
+    __syncthreads();
+    if (c + 2 < nch) load(c + 2, gv, xv);
+    half8 bh[4], bl[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      bh[u] = tr_frag(st + 2 * kDwImg, 64 * wi + 16 * u, lane);
+      bl[u] = tr_frag(st + 3 * kDwImg, 64 * wi + 16 * u, lane);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      // A fragments one row tile at a time (register pressure: two chunks of loads are in flight)
+      const half8 ah = tr_frag(st, 64 * wo + 16 * t, lane);
+      const half8 al = tr_frag(st + kDwImg, 64 * wo + 16 * t, lane);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[t][u] = mfma32h(ah, bh[u], acc[t][u]);
+        acc[t][u] = mfma32h(ah, bl[u], acc[t][u]);
+        acc[t][u] = mfma32h(al, bh[u], acc[t][u]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  floatx4 g0[4], x0[4], g1[4], x1[4];
+  if (nch > 0) load(0, g0, x0);
+  if (nch > 1) load(1, g1, x1);
+  for (int c = 0; c < nch; c += 2) {
+    step(c, g0, x0);
+    if (c + 1 < nch) step(c + 1, g1, x1);
+  }
+
+  // ---- partial dW: lane holds rows 4 (lane >> 4) + r, column lane & 15 of each 16 x 16 tile
+  const float inv = (1.0f / sG) * (1.0f / sX);
+  float* part = D.part + (int64_t)krange * D.O * D.I;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 64 * wi + 16 * u + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + 64 * wo + 16 * t + 4 * (lane >> 4) + r;
+        if (o < D.O && i < D.I) part[(int64_t)o * D.I + i] = acc[t][u][r] * inv;
+      }
+    }
+  // ---- partial db: the 8 row groups' column sums through LDS
+  if (bias) {
+    __syncthreads();
+    float* red = lds_f;   // [8][128]
+    *reinterpret_cast<floatx4*>(red + rb * kDwTile + 4 * cc) = bsum;
+    __syncthreads();
+    if (threadIdx.x < kDwTile && o0 + (int)threadIdx.x < D.O) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += red[q * kDwTile + threadIdx.x];
+      D.bpart[(int64_t)krange * D.O + o0 + threadIdx.x] = s;
+    }
+  }
+}
+
+}  // namespace avr
+
+using namespace avr;
+
+extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int64_t n_rows, int n_split,
+                                void* stream) {
+  AVR_REQUIRE(layers && n_layers >= 1 && n_layers <= AVR_WGRAD_MAX_LAYERS, "avr_weight_grads: bad layer list");
+  AVR_REQUIRE(n_rows >= 0 && n_split >= 1, "avr_weight_grads: bad sizes");
+  DwArgs a{};
+  a.n_layers = n_layers;
+  a.M = n_rows;
+  a.ksplit = n_split;
+  const int64_t per = (n_rows + n_split - 1) / n_split;
+  a.kper = ((per + kDwK - 1) / kDwK) * kDwK;
+  if (a.kper == 0) a.kper = kDwK;
+  int tiles = 0;
+  for (int l = 0; l < n_layers; ++l) {
+    const avr_wgrad_layer& s = layers[l];
+    AVR_REQUIRE(s.grad && s.input && s.partial && s.grad_max && s.input_max, "avr_weight_grads: null pointer (layer %d)", l);
+    AVR_REQUIRE(s.out_dim > 0 && s.in_dim > 0 && s.out_dim % 4 == 0 && s.in_dim % 4 == 0 && s.ld_grad >= s.out_dim &&
+                    s.ld_input >= s.in_dim && s.ld_grad % 4 == 0 && s.ld_input % 4 == 0,
+                "avr_weight_grads: layer %d dims must be multiples of 4 within their row strides", l);
+    DwLayerDev& D = a.L[l];
+    D.g = s.grad; D.x = s.input; D.ldg = s.ld_grad; D.ldx = s.ld_input;
+    D.O = s.out_dim; D.I = s.in_dim;
+    D.nIt = (s.in_dim + kDwTile - 1) / kDwTile;
+    D.tile0 = tiles;
+    D.gmax = s.grad_max; D.xmax = s.input_max;
+    D.part = s.partial; D.bpart = s.bias_partial;
+    tiles += ((s.out_dim + kDwTile - 1) / kDwTile) * D.nIt;
+  }
+  a.tiles = tiles;
+  const int64_t blocks = (int64_t)tiles * n_split;
+  AVR_REQUIRE(blocks < (1ll << 31), "avr_weight_grads: too many tiles");
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess)
+      return fail(AVR_E_HIP, "weight_grad_kernel: cannot set dynamic LDS");
+    attr = true;
+  }
+  weight_grad_kernel<<<(unsigned)blocks, 256, 2 * kDwStage, as_stream(stream)>>>(a);
+  return check_launch("weight_grad_kernel");
+}

@@ -132,6 +132,74 @@ def cpu_baseline(rays_cap=4096, budget_s=12.0):
                       f"{threads} threads), {t_total:.1f} s, host {os.cpu_count()} logical CPUs"}
 
 
+def run_train(args, device):
+    """--mode train: one train.py step (train.py:50-114) per step — SB = 4
+    scenes x 512 rays (train.py defaults batch_size 4, ray_batch_size 512),
+    the conf/default.conf renderer (64 coarse + 32 fine of which 16 depth
+    samples) and field, MSE on rgb coarse + fine, backward, Adam (lr 1e-4).
+    The latent maps are fixed inputs (the ResNet34 encoder is out of scope).
+    Timed twice: autograd through the HIP field (x3 training forward + HIP
+    backward chain + hipBLASLt weight-gradient GEMMs) and PyTorch autograd of
+    the same module (forward_torch; the rest of the step is identical)."""
+    from avr.conf import default_conf
+    from avr.renderers import VolumeRenderer
+    SB, R = 4, 512
+    net = build_scene(device)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    net.encoder.set_latent(torch.randn(SB, net.d_latent, 64, 64, generator=g).to(device))
+    net.num_objs = SB
+    net.poses = net.poses.repeat(SB, 1, 1)
+    net.poses[:, 0, 3] += 0.05 * torch.arange(SB, device=device, dtype=torch.float32)
+    net.focal, net.c = net.focal.repeat(SB, 1), net.c.repeat(SB, 1)
+    net.train()
+    for p in net.parameters():
+        p.requires_grad_(True)
+    rend = VolumeRenderer.from_conf(default_conf()["normal_renderer"]).to(device)
+    rend.seed = 99
+    x_pix = torch.rand(SB, R, 2, generator=g).to(device)
+    c2w = torch.stack([orbit_c2w(0.3 + 0.9 * b) for b in range(SB)]).to(device)
+    c2w = c2w.reshape(SB, 1, 4, 4).expand(SB, R, 4, 4)
+    K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]] * SB, device=device)
+    gt = torch.rand(SB, R, 3, generator=g).to(device)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+
+    def step():
+        rgb_c, rgb_f, _, _ = rend(c2w, K, x_pix, net)
+        loss = ((rgb_c - gt) ** 2).mean() + ((rgb_f - gt) ** 2).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return loss
+
+    res = {}
+    for mode in args.train_modes.split(","):
+        net.hip_backward = mode == "hip"
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss = step()
+        torch.cuda.synchronize()
+        res[mode] = (time.perf_counter() - t0) / args.steps
+        assert bool(torch.isfinite(loss))
+    spr = rend.n_coarse + rend.n_coarse + rend.n_fine
+    line = {
+        "metric": "training rays/s (train.py step: forward + loss.backward() + Adam through VolumeRenderer)",
+        "value": round(SB * R / res["hip"], 1), "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(res["hip"] * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (field products as 3 fp16 MFMA terms)",
+        "data": "synthetic: random-init default.conf field, 4 random 512x64x64 latents, random pixels/targets",
+        "config": {"workload": f"train.py defaults: {SB} scenes x {R} rays, {rend.n_coarse} coarse + "
+                               f"{rend.n_fine} fine ({rend.n_fine_depth} depth) samples, Adam lr 1e-4",
+                   "field_samples_per_step": SB * R * spr},
+    }
+    if "torch" in res:
+        line["torch_autograd"] = {"value": round(SB * R / res["torch"], 1), "ms_per_step": round(res["torch"] * 1e3, 3)}
+        line["speedup_vs_torch_autograd"] = round(res["torch"] / res["hip"], 3)
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,6 +216,9 @@ def main():
                          "with fine-pass early termination at T_stop 1e-5")
     ap.add_argument("--sigma-bias", type=float, default=0.0,
                     help="density bias of the synthetic field (config 4: opacity of the scene)")
+    ap.add_argument("--mode", choices=["render", "train"], default="render",
+                    help="render: the headline inference metric; train: one train.py step per step (1 GPU)")
+    ap.add_argument("--train-modes", default="hip,torch", help="--mode train: which autograd paths to time")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -163,6 +234,8 @@ def main():
     import avr
     from avr.renderers import VolumeRenderer
     avr.load_library()
+    if args.mode == "train":
+        return run_train(args, device)
 
     net = build_scene(device, sigma_bias=args.sigma_bias)
     net.field_precision = args.precision

@@ -196,12 +196,17 @@ int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, 
  * path (dims->precision must be AVR_FIELD_X3).
  *
  * Forward: avr_field_fwd_points_train = avr_field_fwd_points that also writes
- *   act  (2 n_blocks + 1, n_points, d_hidden) fp32: the relu'd input of every
+ *   act  (2 n_blocks + 1) layers of (n_points, d_hidden) fp32, layer l at
+ *        act + l * act_rows * d_hidden (act_rows >= n_points, so calls for
+ *        several scenes can fill one buffer): the relu'd input of every
  *        hidden GEMM, act[2b] = relu(x) into fc_0 of block b, act[2b+1] =
  *        relu(fc_0 out) into fc_1, act[2 n_blocks] = relu(x) into lin_out;
- *   mask (mask_words) their relu masks (opaque, read by avr_field_bwd).
+ *   mask (mask_words) their relu masks (opaque, read by avr_field_bwd);
+ *   act_max (2 n_blocks + 1) or NULL: atomicMax of max |act[l]| (float bits;
+ *        zero it first), the split scales of avr_weight_grads.
  * Backward: avr_field_bwd, given the forward's out and d loss / d out
- * (n_points, 4), writes grads (2 n_blocks + 1, n_points, d_hidden):
+ * (n_points, 4), writes grads (layer l at grads + l * grads_rows * d_hidden,
+ * grads_max as act_max):
  *   grads[2b]   = d loss / d fc_0[b] output (pre-relu),
  *   grads[2b+1] = d loss / d fc_1[b] output,
  *   grads[2 n_blocks] = d loss / d lin_in output.
@@ -215,9 +220,32 @@ int avr_field_bwd_packed_floats(const avr_field_dims* dims, int64_t* n_floats);
 int avr_field_pack_bwd(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed_bwd, void* stream);
 int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
                                const float* table, const float* xyz, const float* viewdirs, int64_t n_points,
-                               float* out, float* act, uint32_t* mask, void* stream);
+                               float* out, float* act, int64_t act_rows, uint32_t* mask, uint32_t* act_max,
+                               void* stream);
 int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd, const float* out,
-                  const float* grad_out, const uint32_t* mask, int64_t n_points, float* grads, void* stream);
+                  const float* grad_out, const uint32_t* mask, int64_t n_points, float* grads, int64_t grads_rows,
+                  uint32_t* grads_max, void* stream);
+
+/* Weight gradients of linear layers, dW = G^T X and db = sum_rows G (the
+ * parameter half of nn.Linear's autograd, models.py:541-592), for up to
+ * AVR_WGRAD_MAX_LAYERS layers in one launch: split-K over the rows (n_split
+ * ranges), split-fp16 MFMA (3 products, fp32 accumulate) under power-of-two
+ * scales from grad_max / input_max (max |.| as float bits, device; the
+ * training kernels above accumulate them with atomicMax). The caller sums
+ * the partials over the split: dW = sum_k partial[k], db = sum_k bias_partial[k]. */
+#define AVR_WGRAD_MAX_LAYERS 16
+typedef struct {
+  const float* grad;        /* (n_rows, ld_grad): d loss / d layer output, columns [0, out_dim) */
+  int64_t ld_grad;
+  const float* input;       /* (n_rows, ld_input): the layer input, columns [0, in_dim) */
+  int64_t ld_input;
+  int out_dim, in_dim;      /* multiples of 4 */
+  const uint32_t* grad_max;
+  const uint32_t* input_max;
+  float* partial;           /* (n_split, out_dim, in_dim) */
+  float* bias_partial;      /* (n_split, out_dim) or NULL */
+} avr_wgrad_layer;
+int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int64_t n_rows, int n_split, void* stream);
 
 /* --------------------------------------------------------- LSTM ray marcher
  * Raymarcher / AdaptiveVolumeRenderer march (renderers.py:313-351, :380-432):

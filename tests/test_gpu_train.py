@@ -137,3 +137,27 @@ def test_volume_renderer_training_step_hip_vs_torch():
     assert abs(res[True][0] - res[False][0]) < 1e-5
     _compare(res[True][1], res[False][1], 5e-3)
     del ops
+
+
+@pytest.mark.parametrize("M,O,I,ld", [(1000, 512, 512, 512), (77, 64, 44, 48), (4096, 4, 512, 512), (0, 128, 64, 64),
+                                      (5000, 512, 64, 64)])
+def test_weight_grads_kernel_vs_fp64(M, O, I, ld):
+    """avr_weight_grads (split-K x3 MFMA, transposed LDS reads) against an fp64
+    G^T X, with ragged row counts, narrow layers and row strides wider than the
+    layer, in a batch of two layers."""
+    from avr import ops
+    g = torch.Generator(device="cpu").manual_seed(M + O + I)
+    G = (torch.randn(M, O, generator=g) * 1e-3 * (torch.rand(M, 1, generator=g) < 0.7)).to(DEV)
+    Xb = torch.relu(torch.randn(M, ld, generator=g)).to(DEV)
+    X = Xb[:, :I]
+    G2 = (torch.randn(M, O, generator=g) * 5.0).to(DEV)
+    mb = ops._max_bits if M else (lambda t: torch.zeros(1, dtype=torch.int32, device=DEV))
+    res = ops.weight_grads([(G, X, mb(G), mb(X), True), (G2, X, mb(G2), mb(X), False)], M)
+    for (dW, db), GG in zip(res, (G, G2)):
+        ref = (GG.double().t() @ X.double()).float().cpu().numpy()
+        got = dW.cpu().numpy()
+        scale = max(float(np.abs(ref).max()), 1e-30)
+        assert float(np.abs(got - ref).max()) <= 2e-6 * scale + 1e-30, float(np.abs(got - ref).max()) / scale
+    bref = G.double().sum(0).float().cpu().numpy()
+    np.testing.assert_allclose(res[0][1].cpu().numpy(), bref, rtol=0, atol=2e-6 * float(np.abs(bref).max(initial=0)) + 1e-30)
+    assert res[1][1] is None
