@@ -87,19 +87,34 @@ __global__ void __launch_bounds__(256, 2) weight_grad_kernel(DwArgs a) {
   const float sG = pow2_scale_for(__uint_as_float(*D.gmax)), sX = pow2_scale_for(__uint_as_float(*D.xmax));
   const bool bias = D.bpart && it == 0;
 
-  // staging: thread -> 4-column group cc, rows rb + 8u
+  // staging: thread -> 4-column group cc, rows rb + 8u of each 32-row chunk.
+  // Columns past O / I read column 0 instead (finite values whose products
+  // land in output rows / columns that are never stored), so every load is
+  // unconditional: a uniform chunk base (SGPRs) plus a 32-bit lane offset.
   const int cc = threadIdx.x & 31, rb = threadIdx.x >> 5;
-  const bool gcol = o0 + 4 * cc < D.O, xcol = i0 + 4 * cc < D.I;
-  const float* gp = D.g + o0 + 4 * cc;
-  const float* xp = D.x + i0 + 4 * cc;
+  const int ldg = (int)D.ldg, ldx = (int)D.ldx;
+  const int gcol = o0 + 4 * cc < D.O ? o0 + 4 * cc : 0;
+  const int xcol = i0 + 4 * cc < D.I ? i0 + 4 * cc : 0;
   floatx4 bsum = {0.f, 0.f, 0.f, 0.f};
   const auto load = [&](int c, floatx4 (&gv)[4], floatx4 (&xv)[4]) {
+    const int64_t row0 = k0 + (int64_t)kDwK * c;
+    const float* gb = D.g + row0 * D.ldg;
+    const float* xb = D.x + row0 * D.ldx;
+    if (row0 + kDwK <= k1) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t m = k0 + (int64_t)kDwK * c + rb + 8 * u;
-      const bool ok = m < k1;
-      gv[u] = ok && gcol ? *reinterpret_cast<const floatx4*>(gp + m * D.ldg) : floatx4{0.f, 0.f, 0.f, 0.f};
-      xv[u] = ok && xcol ? *reinterpret_cast<const floatx4*>(xp + m * D.ldx) : floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < 4; ++u) {
+        gv[u] = *reinterpret_cast<const floatx4*>(gb + (unsigned)((rb + 8 * u) * ldg + gcol));
+        xv[u] = *reinterpret_cast<const floatx4*>(xb + (unsigned)((rb + 8 * u) * ldx + xcol));
+      }
+    } else {   // the K-range's ragged last chunk: rows past k1 read row k1 - 1, G zeroed
+      const int last = (int)(k1 - 1 - row0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + 8 * u < last ? rb + 8 * u : last;
+        gv[u] = *reinterpret_cast<const floatx4*>(gb + (unsigned)(r * ldg + gcol));
+        xv[u] = *reinterpret_cast<const floatx4*>(xb + (unsigned)(r * ldx + xcol));
+        if (rb + 8 * u > last) gv[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   };
 
@@ -110,26 +125,27 @@ __global__ void __launch_bounds__(256, 2) weight_grad_kernel(DwArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[t][u] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // One chunk: its registers -> LDS stage c & 1 (split), barrier, the loads of
-  // chunk c + 2 into the same registers (two chunks of MFMAs to land), MFMAs.
-  // Stage c & 1 was last read in chunk c - 2, which every wave finished before
-  // the barrier of chunk c - 1.
-  const auto step = [&](int c, floatx4 (&gv)[4], floatx4 (&xv)[4]) {
+  // Row group u of chunk c (registers gv / xv) -> LDS stage c & 1, split into fp16 hi / lo.
+  const auto put = [&](int c, const floatx4 (&gv)[4], const floatx4 (&xv)[4], int u) {
     lds_char* st = lds + (c & 1) * kDwStage;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int r = rb + 8 * u, off = img_off(r, cc >> 1) + 8 * (cc & 1);
-      uint2 hi, lo;
-      split4(gv[u], sG, hi, lo);
-      *(lds_u32x2*)(st + off) = u32x2{hi.x, hi.y};
-      *(lds_u32x2*)(st + kDwImg + off) = u32x2{lo.x, lo.y};
-      split4(xv[u], sX, hi, lo);
-      *(lds_u32x2*)(st + 2 * kDwImg + off) = u32x2{hi.x, hi.y};
-      *(lds_u32x2*)(st + 3 * kDwImg + off) = u32x2{lo.x, lo.y};
-      if (bias) bsum += gv[u];
-    }
-    __syncthreads();
-    if (c + 2 < nch) load(c + 2, gv, xv);
+    const int r = rb + 8 * u, off = img_off(r, cc >> 1) + 8 * (cc & 1);
+    uint2 hi, lo;
+    split4(gv[u], sG, hi, lo);
+    *(lds_u32x2*)(st + off) = u32x2{hi.x, hi.y};
+    *(lds_u32x2*)(st + kDwImg + off) = u32x2{lo.x, lo.y};
+    split4(xv[u], sX, hi, lo);
+    *(lds_u32x2*)(st + 2 * kDwImg + off) = u32x2{hi.x, hi.y};
+    *(lds_u32x2*)(st + 3 * kDwImg + off) = u32x2{lo.x, lo.y};
+    if (bias) bsum += gv[u];
+  };
+
+  // Chunk c: MFMAs on stage c & 1, with chunk c + 1 (registers gn / xn, loaded
+  // two chunks ago) split into stage (c + 1) & 1 between them, then gn / xn
+  // reloaded with chunk c + 3; one barrier. Stage (c + 1) & 1 was last read in
+  // chunk c - 1, which every wave finished before that chunk's barrier.
+  const auto step = [&](int c, floatx4 (&gn)[4], floatx4 (&xn)[4]) {
+    const lds_char* st = lds + (c & 1) * kDwStage;
+    const bool next = c + 1 < nch;
     half8 bh[4], bl[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -138,7 +154,6 @@ __global__ void __launch_bounds__(256, 2) weight_grad_kernel(DwArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      // A fragments one row tile at a time (register pressure: two chunks of loads are in flight)
       const half8 ah = tr_frag(st, 64 * wo + 16 * t, lane);
       const half8 al = tr_frag(st + kDwImg, 64 * wo + 16 * t, lane);
 #pragma unroll
@@ -147,16 +162,25 @@ __global__ void __launch_bounds__(256, 2) weight_grad_kernel(DwArgs a) {
         acc[t][u] = mfma32h(ah, bl[u], acc[t][u]);
         acc[t][u] = mfma32h(al, bh[u], acc[t][u]);
       }
+      if (next) put(c + 1, gn, xn, t);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (c + 3 < nch) load(c + 3, gn, xn);
+    __syncthreads();
   };
 
   floatx4 g0[4], x0[4], g1[4], x1[4];
-  if (nch > 0) load(0, g0, x0);
-  if (nch > 1) load(1, g1, x1);
+  if (nch > 0) {
+    load(0, g0, x0);
+    if (nch > 1) load(1, g1, x1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) put(0, g0, x0, u);
+    if (nch > 2) load(2, g0, x0);
+    __syncthreads();
+  }
   for (int c = 0; c < nch; c += 2) {
-    step(c, g0, x0);
-    if (c + 1 < nch) step(c + 1, g1, x1);
+    step(c, g1, x1);
+    if (c + 1 < nch) step(c + 1, g0, x0);
   }
 
   // ---- partial dW: lane holds rows 4 (lane >> 4) + r, column lane & 15 of each 16 x 16 tile
