@@ -262,10 +262,13 @@ def _max_bits(t):
     return t.detach().abs().amax().reshape(1).to(torch.float32).view(torch.int32)
 
 
+_DW_TILE = 256        # avr_weight_grads output tile (weight_grad.hip kDwTile), one workgroup per CU
+
+
 def _wgrad_splits(tiles, n_rows, dev):
-    """K-split of avr_weight_grads: the grid (tiles x splits workgroups, two per
+    """K-split of avr_weight_grads: the grid (tiles x splits workgroups, one per
     CU) should end in full rounds, with K-ranges of at least 2048 rows."""
-    slots = 2 * torch.cuda.get_device_properties(dev).multi_processor_count
+    slots = torch.cuda.get_device_properties(dev).multi_processor_count
     best, best_eff = 1, 0.0
     for n in range(1, 65):
         if n > 1 and n_rows < 2048 * n:
@@ -290,7 +293,7 @@ def weight_grads(layers, n_rows, n_split=None):
     if n_rows == 0:
         return [(torch.zeros(g.shape[1], x.shape[1], device=dev), torch.zeros(g.shape[1], device=dev) if wb else None)
                 for g, x, _, _, wb in layers]
-    tiles = sum(-(-g.shape[1] // 128) * -(-x.shape[1] // 128) for g, x, *_ in layers)
+    tiles = sum(-(-g.shape[1] // _DW_TILE) * -(-x.shape[1] // _DW_TILE) for g, x, *_ in layers)
     if n_split is None:
         n_split = _wgrad_splits(tiles, n_rows, dev)
     out = []

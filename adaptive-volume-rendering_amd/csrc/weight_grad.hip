@@ -24,9 +24,11 @@
 
 namespace avr {
 
-constexpr int kDwTile = 128;
+constexpr int kDwTile = 256;                 // output tile (o x i) per workgroup
+constexpr int kDwWT = 8;                     // 16 x 16 MFMA tiles per wave and dimension (128 x 128 per wave)
 constexpr int kDwK = 32;
-constexpr int kDwImg = kDwK * kDwTile * 2;   // bytes of one fp16 image (32 rows x 256 B)
+constexpr int kDwHalf = kDwK * 256;          // bytes of one 128-column half image (32 rows x 256 B)
+constexpr int kDwImg = 2 * kDwHalf;          // one fp16 image of 256 columns
 constexpr int kDwStage = 4 * kDwImg;         // G hi, G lo, X hi, X lo
 
 struct DwLayerDev {
@@ -52,13 +54,17 @@ typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
 typedef __attribute__((address_space(3))) char lds_char;
 
 // byte offset of 16-B chunk ch (0..15) of row r in a 256-B-row image (XOR swizzle:
-// conflict-free transposed reads, cdna_hip_programming.md T10 image (b))
+// conflict-free transposed reads, cdna_hip_programming.md T10 image (b)); a
+// 256-column image is two such 128-column halves
 __device__ __forceinline__ int img_off(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+__device__ __forceinline__ int img_off_col(int r, int col) { return kDwHalf * (col >> 7) + img_off(r, (col & 127) >> 3); }
 
 // MFMA operand fragment of 16 columns col0 .. col0+15 of an image: lane l
 // (g = l >> 4, i = l & 15) gets column col0 + i, rows 8g .. 8g+7 (element j =
 // row 8g + j, the natural k order of v_mfma_f32_16x16x32_f16 for A and B).
-__device__ __forceinline__ half8 tr_frag(const lds_char* img, int col0, int lane) {
+__device__ __forceinline__ half8 tr_frag(const lds_char* img_full, int col0_full, int lane) {
+  const lds_char* img = img_full + kDwHalf * (col0_full >> 7);
+  const int col0 = col0_full & 127;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const int ch = (col0 >> 3) + (p >> 1), sub = 8 * (p & 1);
   typedef __attribute__((address_space(3))) short4_t lds_short4;
@@ -68,7 +74,7 @@ __device__ __forceinline__ half8 tr_frag(const lds_char* img, int col0, int lane
   return __builtin_bit_cast(half8, both);
 }
 
-__global__ void __launch_bounds__(256, 2) weight_grad_kernel(DwArgs a) {
+__global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
   extern __shared__ float lds_f[];
   lds_char* lds = (lds_char*)lds_f;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -87,48 +93,49 @@ __global__ void __launch_bounds__(256, 2) weight_grad_kernel(DwArgs a) {
   const float sG = pow2_scale_for(__uint_as_float(*D.gmax)), sX = pow2_scale_for(__uint_as_float(*D.xmax));
   const bool bias = D.bpart && it == 0;
 
-  // staging: thread -> 4-column group cc, rows rb + 8u of each 32-row chunk.
+  // staging: thread -> 4-column group cc, rows rb + 4u of each 32-row chunk.
   // Columns past O / I read column 0 instead (finite values whose products
   // land in output rows / columns that are never stored), so every load is
   // unconditional: a uniform chunk base (SGPRs) plus a 32-bit lane offset.
-  const int cc = threadIdx.x & 31, rb = threadIdx.x >> 5;
+  const int cc = threadIdx.x & 63, rb = threadIdx.x >> 6;
   const int ldg = (int)D.ldg, ldx = (int)D.ldx;
   const int gcol = o0 + 4 * cc < D.O ? o0 + 4 * cc : 0;
   const int xcol = i0 + 4 * cc < D.I ? i0 + 4 * cc : 0;
   floatx4 bsum = {0.f, 0.f, 0.f, 0.f};
-  const auto load = [&](int c, floatx4 (&gv)[4], floatx4 (&xv)[4]) {
+  constexpr int NU = kDwK / 4;   // rows per thread and chunk
+  const auto load = [&](int c, floatx4 (&gv)[NU], floatx4 (&xv)[NU]) {
     const int64_t row0 = k0 + (int64_t)kDwK * c;
     const float* gb = D.g + row0 * D.ldg;
     const float* xb = D.x + row0 * D.ldx;
     if (row0 + kDwK <= k1) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        gv[u] = *reinterpret_cast<const floatx4*>(gb + (unsigned)((rb + 8 * u) * ldg + gcol));
-        xv[u] = *reinterpret_cast<const floatx4*>(xb + (unsigned)((rb + 8 * u) * ldx + xcol));
+      for (int u = 0; u < NU; ++u) {
+        gv[u] = *reinterpret_cast<const floatx4*>(gb + (unsigned)((rb + 4 * u) * ldg + gcol));
+        xv[u] = *reinterpret_cast<const floatx4*>(xb + (unsigned)((rb + 4 * u) * ldx + xcol));
       }
     } else {   // the K-range's ragged last chunk: rows past k1 read row k1 - 1, G zeroed
       const int last = (int)(k1 - 1 - row0);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = rb + 8 * u < last ? rb + 8 * u : last;
+      for (int u = 0; u < NU; ++u) {
+        const int r = rb + 4 * u < last ? rb + 4 * u : last;
         gv[u] = *reinterpret_cast<const floatx4*>(gb + (unsigned)(r * ldg + gcol));
         xv[u] = *reinterpret_cast<const floatx4*>(xb + (unsigned)(r * ldx + xcol));
-        if (rb + 8 * u > last) gv[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (rb + 4 * u > last) gv[u] = floatx4{0.f, 0.f, 0.f, 0.f};
       }
     }
   };
 
   const int wo = wid >> 1, wi = wid & 1;
-  floatx4 acc[4][4];
+  floatx4 acc[kDwWT][kDwWT];
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < kDwWT; ++t)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[t][u] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < kDwWT; ++u) acc[t][u] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // Row group u of chunk c (registers gv / xv) -> LDS stage c & 1, split into fp16 hi / lo.
-  const auto put = [&](int c, const floatx4 (&gv)[4], const floatx4 (&xv)[4], int u) {
+  const auto put = [&](int c, const floatx4 (&gv)[NU], const floatx4 (&xv)[NU], int u) {
     lds_char* st = lds + (c & 1) * kDwStage;
-    const int r = rb + 8 * u, off = img_off(r, cc >> 1) + 8 * (cc & 1);
+    const int r = rb + 4 * u, off = img_off_col(r, 4 * cc) + 8 * (cc & 1);
     uint2 hi, lo;
     split4(gv[u], sG, hi, lo);
     *(lds_u32x2*)(st + off) = u32x2{hi.x, hi.y};
@@ -140,73 +147,81 @@ __global__ void __launch_bounds__(256, 2) weight_grad_kernel(DwArgs a) {
   };
 
   // Chunk c: MFMAs on stage c & 1, with chunk c + 1 (registers gn / xn, loaded
-  // two chunks ago) split into stage (c + 1) & 1 between them, then gn / xn
-  // reloaded with chunk c + 3; one barrier. Stage (c + 1) & 1 was last read in
+  // during chunk c - 1) split into stage (c + 1) & 1 between them, then gn / xn
+  // reloaded with chunk c + 2; one barrier. Stage (c + 1) & 1 was last read in
   // chunk c - 1, which every wave finished before that chunk's barrier.
-  const auto step = [&](int c, floatx4 (&gn)[4], floatx4 (&xn)[4]) {
+  floatx4 gn[NU], xn[NU];
+  const auto step = [&](int c) {
     const lds_char* st = lds + (c & 1) * kDwStage;
     const bool next = c + 1 < nch;
-    half8 bh[4], bl[4];
+    half8 bh[kDwWT], bl[kDwWT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      bh[u] = tr_frag(st + 2 * kDwImg, 64 * wi + 16 * u, lane);
-      bl[u] = tr_frag(st + 3 * kDwImg, 64 * wi + 16 * u, lane);
+    for (int u = 0; u < kDwWT; ++u) {
+      bh[u] = tr_frag(st + 2 * kDwImg, 128 * wi + 16 * u, lane);
+      bl[u] = tr_frag(st + 3 * kDwImg, 128 * wi + 16 * u, lane);
     }
+    // A fragments one row tile ahead: row tile t + 1's transposed reads are in
+    // flight while row tile t's 24 MFMAs issue
+    half8 ah = tr_frag(st, 128 * wo, lane), al = tr_frag(st + kDwImg, 128 * wo, lane);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const half8 ah = tr_frag(st, 64 * wo + 16 * t, lane);
-      const half8 al = tr_frag(st + kDwImg, 64 * wo + 16 * t, lane);
+    for (int t = 0; t < kDwWT; ++t) {
+      half8 ahn = ah, aln = al;
+      if (t + 1 < kDwWT) {
+        ahn = tr_frag(st, 128 * wo + 16 * (t + 1), lane);
+        aln = tr_frag(st + kDwImg, 128 * wo + 16 * (t + 1), lane);
+      }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kDwWT; ++u) {
         acc[t][u] = mfma32h(ah, bh[u], acc[t][u]);
         acc[t][u] = mfma32h(ah, bl[u], acc[t][u]);
         acc[t][u] = mfma32h(al, bh[u], acc[t][u]);
       }
-      if (next) put(c + 1, gn, xn, t);
-      __builtin_amdgcn_sched_barrier(0);
+      // chunk c + 1's loads were issued at the end of chunk c - 1: split them in
+      // the second half of the MFMAs, when they have landed
+      if (next && t >= kDwWT / 2) {
+        put(c + 1, gn, xn, 2 * (t - kDwWT / 2));
+        put(c + 1, gn, xn, 2 * (t - kDwWT / 2) + 1);
+      }
+      ah = ahn;
+      al = aln;
     }
-    if (c + 3 < nch) load(c + 3, gn, xn);
+    if (c + 2 < nch) load(c + 2, gn, xn);
     __syncthreads();
   };
 
-  floatx4 g0[4], x0[4], g1[4], x1[4];
   if (nch > 0) {
-    load(0, g0, x0);
-    if (nch > 1) load(1, g1, x1);
+    load(0, gn, xn);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) put(0, g0, x0, u);
-    if (nch > 2) load(2, g0, x0);
+    for (int u = 0; u < NU; ++u) put(0, gn, xn, u);
+    if (nch > 1) load(1, gn, xn);
     __syncthreads();
   }
-  for (int c = 0; c < nch; c += 2) {
-    step(c, g1, x1);
-    if (c + 1 < nch) step(c + 1, g0, x0);
-  }
+  for (int c = 0; c < nch; ++c) step(c);
 
   // ---- partial dW: lane holds rows 4 (lane >> 4) + r, column lane & 15 of each 16 x 16 tile
   const float inv = (1.0f / sG) * (1.0f / sX);
   float* part = D.part + (int64_t)krange * D.O * D.I;
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < kDwWT; ++t)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + 64 * wi + 16 * u + (lane & 15);
+    for (int u = 0; u < kDwWT; ++u) {
+      const int i = i0 + 128 * wi + 16 * u + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int o = o0 + 64 * wo + 16 * t + 4 * (lane >> 4) + r;
+        const int o = o0 + 128 * wo + 16 * t + 4 * (lane >> 4) + r;
         if (o < D.O && i < D.I) part[(int64_t)o * D.I + i] = acc[t][u][r] * inv;
       }
     }
   // ---- partial db: the 8 row groups' column sums through LDS
   if (bias) {
     __syncthreads();
-    float* red = lds_f;   // [8][128]
+    float* red = lds_f;   // [4][256]
     *reinterpret_cast<floatx4*>(red + rb * kDwTile + 4 * cc) = bsum;
     __syncthreads();
     if (threadIdx.x < kDwTile && o0 + (int)threadIdx.x < D.O) {
       float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) s += red[q * kDwTile + threadIdx.x];
+      for (int q = 0; q < 4; ++q) s += red[q * kDwTile + threadIdx.x];
       D.bpart[(int64_t)krange * D.O + o0 + threadIdx.x] = s;
     }
   }
