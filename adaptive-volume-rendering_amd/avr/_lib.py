@@ -88,6 +88,7 @@ _SIGS = {
     "avr_field_bwd": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p,
                       i64, c_void_p, c_void_p],
     "avr_weight_grads": [ctypes.POINTER(WGradLayer), c_int, i64, c_int, c_void_p],
+    "avr_latent_features": [ctypes.POINTER(ViewDesc), c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
 }
 EXPORTED = ("avr_version", "avr_last_error_string", "avr_device_count") + tuple(_SIGS)
 

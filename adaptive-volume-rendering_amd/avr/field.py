@@ -280,7 +280,7 @@ class _FieldTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
-        from .ops import _max_bits, weight_grads
+        from .ops import _max_bits, latent_features, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         fused, entry, names = ctx.fused, ctx.entry, ctx.names
         net = fused.net
@@ -305,12 +305,16 @@ class _FieldTrain(torch.autograd.Function):
         entry.dims.precision = PRECISIONS[fused.precision]
         act, act_max = ctx.act, ctx.act_max
         ctx.act = ctx.act_max = ctx.masks = None
-        # MLP inputs the lin_z / lin_in gradients contract against (forward_torch's code)
+        # MLP inputs the lin_z / lin_in gradients contract against: the latent
+        # features (avr_latent_features, row-major) and z_feature (forward_torch's code)
         with torch.no_grad():
-            lat_feat, z_feature = net.mlp_inputs(xyz.detach(), viewdirs.detach())
+            z_feature = net.z_features(xyz.detach(), viewdirs.detach())
             d_in = z_feature.shape[1]
             zf = torch.nn.functional.pad(z_feature.to(F32), (0, (-d_in) % 4)).contiguous()
-            lat_feat = lat_feat.to(F32).contiguous()
+            lat_feat = torch.empty(Mt, net.d_latent, device=dev, dtype=F32)
+            for sb in range(SB):
+                latent_features(fused.view(sb), latent[min(sb, latent.shape[0] - 1)], xyz[sb],
+                                out=lat_feat[sb * B:(sb + 1) * B])
         lat_max = _max_bits(latent)          # |interpolated latent| <= max |latent| (convex blend)
         zf_max = _max_bits(zf)
         Gz = [G[2 * b - 1] if b > 0 else G[2 * nb] for b in range(nz)]

@@ -301,7 +301,11 @@ class NewPixelNeRFNet(nn.Module):
         `latent` overrides the encoder's map, for its gradient)."""
         return self._inputs(xyz, viewdirs, latent, batched_rot=True)[:2]
 
-    def _inputs(self, xyz, viewdirs, latent_map=None, batched_rot=False):
+    def z_features(self, xyz, viewdirs):
+        """z_feature (SB*B, d_in) alone: the positional-encoded MLP input half."""
+        return self._inputs(xyz, viewdirs, batched_rot=True, want_latent=False)[1]
+
+    def _inputs(self, xyz, viewdirs, latent_map=None, batched_rot=False, want_latent=True):
         SB, B, _ = xyz.shape
         NS = self.num_views_per_obj
         xyz = repeat_interleave(xyz, NS)
@@ -328,7 +332,7 @@ class NewPixelNeRFNet(nn.Module):
                 z_feature = torch.cat((z_feature, vd), dim=1)
             if self.use_code and self.use_code_viewdirs:
                 z_feature = self.code(z_feature)
-        if self.use_encoder:
+        if self.use_encoder and want_latent:
             uv = -xyz[:, :, :2] / xyz[:, :, 2:]
             uv = uv * repeat_interleave(self.focal.unsqueeze(1), NS if self.focal.shape[0] > 1 else 1)
             uv = uv + repeat_interleave(self.c.unsqueeze(1), NS if self.c.shape[0] > 1 else 1)

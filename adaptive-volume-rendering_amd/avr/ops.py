@@ -314,3 +314,18 @@ def weight_grads(layers, n_rows, n_split=None):
         call("avr_weight_grads", arr, len(chunk), n_rows, n_split, stream_of(layers[0][0]))
         out += [(p.sum(0), None if b is None else b.sum(0)) for p, b in keep]
     return out
+
+
+def latent_features(view, latent_chw, xyz, out=None):
+    """SpatialEncoder.index at world points (models.py:245-274, 753-810):
+    latent (C, H, W) of one source view (avr.field.FusedField.view gives the
+    ViewDesc), xyz (N, 3) -> (N, C) row-major (avr_latent_features)."""
+    C, H, W = latent_chw.shape
+    lat = latent_chw.detach().to(F32).reshape(C, H * W).t().contiguous()
+    xyz = _f32c(xyz.reshape(-1, 3))
+    n = xyz.shape[0]
+    if out is None:
+        out = torch.empty(n, C, device=xyz.device, dtype=F32)
+    require_device(lat, xyz, out)
+    call("avr_latent_features", ctypes.byref(view), ptr(lat), C, ptr(xyz), n, ptr(out), stream_of(xyz))
+    return out

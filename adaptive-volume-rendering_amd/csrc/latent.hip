@@ -1,0 +1,53 @@
+// Pixel-aligned latent features at points: SpatialEncoder.index
+// (models.py:245-274: project into the source view, uv * scale - 1, grid_sample
+// bilinear / border / align_corners=True) as NewPixelNeRFNet.forward calls it
+// (models.py:753-810) — the `latent` half of the MLP input, which the lin_z
+// weight gradients contract against, and phi(..., return_features=True).
+//
+// The map is read channels-last, (H*W, C): one wave per point, each lane
+// blends 8 channels of the 4 corner rows (2 x 16-B loads per corner, the rows
+// of neighbouring points mostly L2 hits) and writes them with two 16-B stores,
+// so a point costs one 2 KB row out (C = 512) and the output is row-major
+// (n_points, C) with no transpose pass.
+#include "field_common.h"
+
+namespace avr {
+
+__global__ void __launch_bounds__(256) latent_features_kernel(View v, const float* __restrict__ lat_hwc, int C,
+                                                              const float* __restrict__ xyz, int64_t n_points,
+                                                              float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= n_points) return;
+  const Bilinear bl = bilinear_at(v, xyz[3 * m], xyz[3 * m + 1], xyz[3 * m + 2]);
+  for (int c = 4 * lane; c < C; c += 256) {
+    float4 acc;
+    const float4 a = *reinterpret_cast<const float4*>(lat_hwc + (int64_t)bl.tex[0] * C + c);
+    const float4 b = *reinterpret_cast<const float4*>(lat_hwc + (int64_t)bl.tex[1] * C + c);
+    const float4 d = *reinterpret_cast<const float4*>(lat_hwc + (int64_t)bl.tex[2] * C + c);
+    const float4 e = *reinterpret_cast<const float4*>(lat_hwc + (int64_t)bl.tex[3] * C + c);
+    // grid_sample's order: nw, ne, sw, se
+    acc.x = fadd(fadd(fadd(fmul(a.x, bl.w[0]), fmul(b.x, bl.w[1])), fmul(d.x, bl.w[2])), fmul(e.x, bl.w[3]));
+    acc.y = fadd(fadd(fadd(fmul(a.y, bl.w[0]), fmul(b.y, bl.w[1])), fmul(d.y, bl.w[2])), fmul(e.y, bl.w[3]));
+    acc.z = fadd(fadd(fadd(fmul(a.z, bl.w[0]), fmul(b.z, bl.w[1])), fmul(d.z, bl.w[2])), fmul(e.z, bl.w[3]));
+    acc.w = fadd(fadd(fadd(fmul(a.w, bl.w[0]), fmul(b.w, bl.w[1])), fmul(d.w, bl.w[2])), fmul(e.w, bl.w[3]));
+    *reinterpret_cast<float4*>(out + m * C + c) = acc;
+  }
+}
+
+}  // namespace avr
+
+using namespace avr;
+
+extern "C" int avr_latent_features(const avr_view_desc* view, const float* latent_hwc, int channels,
+                                   const float* xyz, int64_t n_points, float* out, void* stream) {
+  AVR_REQUIRE(n_points >= 0 && channels > 0 && channels % 4 == 0, "avr_latent_features: bad sizes");
+  if (n_points == 0) return AVR_OK;
+  AVR_REQUIRE(view && latent_hwc && xyz && out, "avr_latent_features: null pointer");
+  AVR_REQUIRE(view->latent_h > 0 && view->latent_w > 0, "avr_latent_features: bad latent size");
+  View v;
+  view_from_desc(view, &v);
+  latent_features_kernel<<<(unsigned)((n_points + 3) / 4), 256, 0, as_stream(stream)>>>(v, latent_hwc, channels, xyz,
+                                                                                      n_points, out);
+  return check_launch("latent_features_kernel");
+}

@@ -247,6 +247,14 @@ typedef struct {
 } avr_wgrad_layer;
 int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int64_t n_rows, int n_split, void* stream);
 
+/* Latent features at points — SpatialEncoder.index (models.py:245-274) as
+ * NewPixelNeRFNet.forward uses it (models.py:753-810): bilinear / border /
+ * align_corners=True lookup of latent_hwc (H*W, channels), the source view's
+ * map channels-last, at world points xyz (n_points, 3) -> out (n_points,
+ * channels). channels multiple of 4.                                           */
+int avr_latent_features(const avr_view_desc* view, const float* latent_hwc, int channels, const float* xyz,
+                        int64_t n_points, float* out, void* stream);
+
 /* --------------------------------------------------------- LSTM ray marcher
  * Raymarcher / AdaptiveVolumeRenderer march (renderers.py:313-351, :380-432):
  * x = ro + rd * init_dist, then `steps` x { v = latent features at x

@@ -161,3 +161,18 @@ def test_weight_grads_kernel_vs_fp64(M, O, I, ld):
     bref = G.double().sum(0).float().cpu().numpy()
     np.testing.assert_allclose(res[0][1].cpu().numpy(), bref, rtol=0, atol=2e-6 * float(np.abs(bref).max(initial=0)) + 1e-30)
     assert res[1][1] is None
+
+
+def test_latent_features_kernel_vs_grid_sample():
+    """avr_latent_features (row-major pixel-aligned lookup) against the module's
+    SpatialEncoder.index (torch grid_sample), two scenes, points inside and
+    outside the source image (border padding)."""
+    from avr import ops
+    net = _net(64, 2, 64, (8, 8), sb=2)
+    xyz, vd, _ = _points(2, 333, seed=9)
+    xyz = xyz * 3.0   # some points project outside the source view
+    ref, _ = net.mlp_inputs(xyz, vd)
+    fused = net.fused()
+    for sb in range(2):
+        got = ops.latent_features(fused.view(sb), net.encoder.latent[sb], xyz[sb])
+        np.testing.assert_allclose(got.cpu().numpy(), ref[sb * 333:(sb + 1) * 333].cpu().numpy(), atol=2e-6, rtol=1e-5)
