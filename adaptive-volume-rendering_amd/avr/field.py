@@ -292,7 +292,8 @@ class _FieldTrain(torch.autograd.Function):
         want_latent = ctx.needs_input_grad[5] and not net.stop_encoder_grad
         if B == 0:
             zeros = tuple(torch.zeros_like(p) if ctx.needs_input_grad[6 + i] else None for i, p in enumerate(params))
-            return (None, None, None, None, None, torch.zeros_like(latent) if want_latent else None) + zeros
+            return (None, None, None, torch.zeros_like(xyz) if ctx.needs_input_grad[3] else None, None,
+                    torch.zeros_like(latent) if want_latent else None) + zeros
         dev = xyz.device
         dims.precision = _lib.FIELD_X3
         bwd = fused.packed_bwd(ctx.coarse, entry)
@@ -343,12 +344,28 @@ class _FieldTrain(torch.autograd.Function):
             grads[f"lin_z.{b}.bias"] = res[2 * b - 1][1] if b > 0 else res[-1][1]
         w_in, b_in = res[-1]
         grads["lin_in.weight"], grads["lin_in.bias"] = w_in[:, :d_in].contiguous(), b_in
-        d_latent = None
-        if want_latent:
-            dZ = sum(Gz[b] @ P[f"lin_z.{b}.weight"].detach() for b in range(nz))
+        # the gradient at the MLP inputs, sent through the (cheap) torch input
+        # functions: the latent map via the grid_sample adjoint, the points via
+        # PE / rotation / projection (the adaptive renderer's band points)
+        d_latent = d_xyz = None
+        want_xyz = ctx.needs_input_grad[3]
+        if want_latent or want_xyz:
             with torch.enable_grad():
-                lat = latent.detach().requires_grad_(True)
-                feat, _ = net.mlp_inputs(xyz.detach(), viewdirs.detach(), latent=lat)
-                (d_latent,) = torch.autograd.grad(feat, lat, dZ)
-        return (None, None, None, None, None, d_latent) + tuple(
+                lat = latent.detach().requires_grad_(want_latent)
+                x = xyz.detach().requires_grad_(want_xyz)
+                feat, zft = net.mlp_inputs(x, viewdirs.detach(), latent=lat)
+                outs, grads_out = [], []
+                if nz > 0:
+                    outs.append(feat)
+                    grads_out.append(sum(Gz[b] @ P[f"lin_z.{b}.weight"].detach() for b in range(nz)))
+                if want_xyz:
+                    outs.append(zft)
+                    grads_out.append(G[2 * nb] @ P["lin_in.weight"].detach())
+                wrt = ([lat] if want_latent else []) + ([x] if want_xyz else [])
+                res_in = torch.autograd.grad(outs, wrt, grads_out, allow_unused=True)
+            if want_latent:
+                d_latent = res_in[0] if res_in[0] is not None else torch.zeros_like(latent)
+            if want_xyz:
+                d_xyz = res_in[-1] if res_in[-1] is not None else torch.zeros_like(xyz)
+        return (None, None, None, d_xyz, None, d_latent) + tuple(
             grads[n] if ctx.needs_input_grad[6 + i] else None for i, n in enumerate(names))

@@ -280,13 +280,12 @@ class NewPixelNeRFNet(nn.Module):
         return any(p.requires_grad for p in self.parameters()) or self.encoder.latent.requires_grad
 
     def can_train_fused(self, xyz, viewdirs):
-        """Autograd on the HIP path: parameters / latent need gradients, the
-        points do not (VolumeRenderer training; the adaptive renderer's band
-        points carry a gradient and take forward_torch)."""
+        """Autograd on the HIP path (avr.field._FieldTrain): parameters, the
+        latent or the points need gradients (VolumeRenderer training; the
+        adaptive renderer's band points); view directions must not."""
         from .field import fused_eligible
         return (self.use_fused and self.hip_backward and xyz.is_cuda and torch.is_grad_enabled()
-                and not xyz.requires_grad and viewdirs is not None and not viewdirs.requires_grad
-                and fused_eligible(self))
+                and viewdirs is not None and not viewdirs.requires_grad and fused_eligible(self))
 
     def forward(self, xyz, coarse=True, viewdirs=None, far=False, return_features=False):
         if not return_features and self.can_fuse(xyz):

@@ -176,3 +176,22 @@ def test_latent_features_kernel_vs_grid_sample():
     for sb in range(2):
         got = ops.latent_features(fused.view(sb), net.encoder.latent[sb], xyz[sb])
         np.testing.assert_allclose(got.cpu().numpy(), ref[sb * 333:(sb + 1) * 333].cpu().numpy(), atol=2e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("d_hidden,latent_grad", [(64, False), (512, True)])
+def test_field_train_point_gradient(d_hidden, latent_grad):
+    """Points that carry a gradient (the adaptive renderer's band samples,
+    renderers.py:492-508): d loss / d xyz through PE, rotation, projection and
+    the bilinear latent lookup, with the parameter gradients, vs PyTorch autograd."""
+    d_latent = 512 if d_hidden == 512 else 64
+    net = _net(d_hidden, 3, d_latent, (16, 16) if d_hidden == 512 else (8, 8))
+    xyz0, vd, w = _points(1, 500, seed=17)
+    res = {}
+    for hip in (True, False):
+        xyz = xyz0.clone().requires_grad_(True)
+        _, g, l = _grads(net, xyz, vd, w, True, hip=hip, latent_grad=latent_grad)
+        res[hip] = (g, l, xyz.grad.detach().clone())
+    _compare(res[True][0], res[False][0], 2e-3)
+    _compare({"xyz": res[True][2]}, {"xyz": res[False][2]}, 2e-3)
+    if latent_grad:
+        _compare({"latent": res[True][1]}, {"latent": res[False][1]}, 2e-3)
