@@ -12,6 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
+AVR_MAX_SCENES = 16
 ABI_VERSION = 3
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -80,13 +81,13 @@ _SIGS = {
                            c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p],
     "avr_field_fwd_points": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
                              c_void_p, i64, c_void_p, c_void_p],
-    "avr_field_train_sizes": [ctypes.POINTER(FieldDims), i64, ctypes.POINTER(i64), ctypes.POINTER(i64)],
+    "avr_field_train_sizes": [ctypes.POINTER(FieldDims), c_int, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)],
     "avr_field_bwd_packed_floats": [ctypes.POINTER(FieldDims), ctypes.POINTER(i64)],
     "avr_field_pack_bwd": [ctypes.POINTER(FieldDims), ctypes.POINTER(ResnetFCWeights), c_void_p, c_void_p],
-    "avr_field_fwd_points_train": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
-                                   c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, c_void_p, c_void_p],
-    "avr_field_bwd": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p,
-                      i64, c_void_p, c_void_p],
+    "avr_field_fwd_points_train": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, c_void_p, c_void_p],
+    "avr_field_bwd": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_int, i64, c_void_p, c_void_p, c_void_p,
+                      c_void_p, i64, c_void_p, c_void_p],
     "avr_weight_grads": [ctypes.POINTER(WGradLayer), c_int, i64, c_int, c_void_p],
     "avr_latent_features": [ctypes.POINTER(ViewDesc), c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
 }

@@ -160,6 +160,25 @@ class FusedField:
         entry.tables[sb] = (key, table, lat)  # holding `lat` keeps its address from being reused
         return table
 
+    def tables_batch(self, coarse, n_scenes):
+        """The lin_z tables of scenes 0 .. n_scenes-1 back to back, (n_scenes,
+        max(n_lin_z, 1), H*W, d_hidden): one buffer for the training launches."""
+        entry = self.packed(coarse)
+        lat = self.net.encoder.latent
+        key = (n_scenes, lat.data_ptr(), lat._version, tuple(lat.shape))
+        hit = getattr(entry, "batch_tables", None)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        dims = entry.dims
+        L, H, W = lat.shape[1:]
+        out = torch.empty(n_scenes, max(dims.n_lin_z, 1), H * W, dims.d_hidden, device=lat.device, dtype=F32)
+        for sb in range(n_scenes):
+            latent = lat[min(sb, lat.shape[0] - 1)].detach().to(F32).contiguous()
+            call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W, ptr(out[sb]),
+                 stream_of(out))
+        entry.batch_tables = (key, out, lat)
+        return out
+
     def view(self, sb=0):
         net = self.net
         srcs = [net.poses, net.focal, net.c, net.image_shape, net.encoder.latent_scaling]
@@ -254,24 +273,26 @@ class _FieldTrain(torch.autograd.Function):
         dims.precision = _lib.FIELD_X3
         H, nb = dims.d_hidden, dims.n_blocks
         n_l, Mt = 2 * nb + 1, SB * B
-        act_n, mask_n = ctypes.c_int64(0), ctypes.c_int64(0)
-        _lib.check(_lib.load().avr_field_train_sizes(ctypes.byref(dims), B, ctypes.byref(act_n), ctypes.byref(mask_n)),
-                   "avr_field_train_sizes")
         dev = xyz.device
         out = torch.empty(SB, B, 4, device=dev, dtype=F32)
         act = torch.empty(n_l, Mt, H, device=dev, dtype=F32)
         act_max = torch.zeros(n_l, device=dev, dtype=torch.int32)
+        p = xyz.detach().to(F32).contiguous()
+        v = viewdirs.reshape(SB, B, 3).detach().to(F32).contiguous()
+        require_device(p, v)
+        tables = fused.tables_batch(coarse, SB)
         masks = []
-        vd = viewdirs.reshape(SB, B, 3)
-        for sb in range(SB):
-            p = xyz[sb].detach().to(F32).contiguous()
-            v = vd[sb].detach().to(F32).contiguous()
-            require_device(p, v)
+        for g0 in range(0, SB, _lib.AVR_MAX_SCENES):     # one launch per group of scenes
+            n = min(_lib.AVR_MAX_SCENES, SB - g0)
+            act_n, mask_n = ctypes.c_int64(0), ctypes.c_int64(0)
+            _lib.check(_lib.load().avr_field_train_sizes(ctypes.byref(dims), n, B, ctypes.byref(act_n),
+                                                         ctypes.byref(mask_n)), "avr_field_train_sizes")
+            views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
             mask = torch.empty(max(mask_n.value, 1), device=dev, dtype=torch.int32)
-            call("avr_field_fwd_points_train", ctypes.byref(dims), ctypes.byref(fused.view(sb)), ptr(entry.packed),
-                 ptr(fused.table(coarse, sb)), ptr(p), ptr(v), B, ptr(out[sb]),
-                 ctypes.c_void_p(act.data_ptr() + sb * B * H * 4), Mt, ptr(mask), ptr(act_max), stream_of(p))
-            masks.append(mask)
+            call("avr_field_fwd_points_train", ctypes.byref(dims), views, n, ptr(entry.packed), ptr(tables[g0]),
+                 ptr(p[g0]), ptr(v[g0]), B, ptr(out[g0]), ctypes.c_void_p(act.data_ptr() + g0 * B * H * 4), Mt,
+                 ptr(mask), ptr(act_max), stream_of(p))
+            masks.append((g0, n, mask))
         entry.dims.precision = PRECISIONS[fused.precision]
         ctx.fused, ctx.coarse, ctx.names, ctx.entry = fused, coarse, names, entry
         ctx.act, ctx.act_max, ctx.masks = act, act_max, masks
@@ -300,9 +321,10 @@ class _FieldTrain(torch.autograd.Function):
         grad_out = grad_out.to(F32).contiguous()
         G = torch.empty(n_l, Mt, H, device=dev, dtype=F32)
         g_max = torch.zeros(n_l, device=dev, dtype=torch.int32)
-        for sb in range(SB):
-            call("avr_field_bwd", ctypes.byref(dims), ptr(entry.packed), ptr(bwd), ptr(out[sb]), ptr(grad_out[sb]),
-                 ptr(ctx.masks[sb]), B, ctypes.c_void_p(G.data_ptr() + sb * B * H * 4), Mt, ptr(g_max), stream_of(G))
+        for g0, n, mask in ctx.masks:
+            call("avr_field_bwd", ctypes.byref(dims), ptr(entry.packed), ptr(bwd), n, B, ptr(out[g0]),
+                 ptr(grad_out[g0]), ptr(mask), ctypes.c_void_p(G.data_ptr() + g0 * B * H * 4), Mt, ptr(g_max),
+                 stream_of(G))
         entry.dims.precision = PRECISIONS[fused.precision]
         act, act_max = ctx.act, ctx.act_max
         ctx.act = ctx.act_max = ctx.masks = None

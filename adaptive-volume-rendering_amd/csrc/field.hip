@@ -476,30 +476,37 @@ extern "C" int avr_field_pack_bwd(const avr_field_dims* dims, const avr_resnetfc
   return AVR_OK;
 }
 
-extern "C" int avr_field_train_sizes(const avr_field_dims* dims, int64_t n_points, int64_t* act_floats,
+extern "C" int avr_field_train_sizes(const avr_field_dims* dims, int n_scenes, int64_t n_points, int64_t* act_floats,
                                      int64_t* mask_words_out) {
   Layout L;
   const int rc = make_layout(dims, &L);
   if (rc) return rc;
-  AVR_REQUIRE(n_points >= 0 && act_floats && mask_words_out, "avr_field_train_sizes: bad argument");
+  AVR_REQUIRE(n_scenes >= 1 && n_points >= 0 && act_floats && mask_words_out, "avr_field_train_sizes: bad argument");
   const int64_t layers = 2 * dims->n_blocks + 1;
-  const int64_t blocks = (n_points + kX3Samples - 1) / kX3Samples;
-  *act_floats = layers * n_points * dims->d_hidden;
+  const int64_t blocks = n_scenes * ((n_points + kX3Samples - 1) / kX3Samples);
+  *act_floats = layers * n_scenes * n_points * dims->d_hidden;
   *mask_words_out = layers * blocks * 4 * mask_words(dims->d_hidden / 64) * 64;
   return AVR_OK;
 }
 
-extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
-                                          const float* table, const float* xyz, const float* viewdirs,
-                                          int64_t n_points, float* out, float* act, int64_t act_rows,
-                                          uint32_t* mask, uint32_t* act_max, void* stream) {
+extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
+                                          const float* packed, const float* tables, const float* xyz,
+                                          const float* viewdirs, int64_t n_points, float* out, float* act,
+                                          int64_t act_rows, uint32_t* mask, uint32_t* act_max, void* stream) {
   FieldArgs a{};
-  int rc = field_common(dims, view, packed, table, &a);
+  AVR_REQUIRE(views && n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES,
+              "avr_field_fwd_points_train: 1..%d scenes per call", AVR_MAX_SCENES);
+  int rc = field_common(dims, views, packed, tables, &a);
   if (rc) return rc;
   AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_fwd_points_train: the training path is x3 only");
   AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points_train: bad size");
   AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && out && act && mask), "avr_field_fwd_points_train: null pointer");
-  AVR_REQUIRE(act_rows >= n_points, "avr_field_fwd_points_train: act_rows < n_points");
+  AVR_REQUIRE(act_rows >= n_scenes * n_points, "avr_field_fwd_points_train: act_rows < n_scenes * n_points");
+  for (int s = 0; s < n_scenes; ++s) {
+    AVR_REQUIRE(views[s].latent_h == views[0].latent_h && views[s].latent_w == views[0].latent_w,
+                "avr_field_fwd_points_train: scenes need latent maps of one size");
+    view_from_desc(&views[s], &a.views[s]);
+  }
   a.xyz = xyz; a.vd = viewdirs; a.n_samples = 1;
   a.M = n_points;
   a.out = reinterpret_cast<float4*>(out);
@@ -507,26 +514,31 @@ extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_
   a.act_stride = act_rows * dims->d_hidden;
   a.mask = mask;
   a.act_max = act_max;
+  a.n_scenes = n_scenes;
+  a.blocks_per_scene = (n_points + kX3Samples - 1) / kX3Samples;
+  a.table_scene_stride = (int64_t)(dims->n_lin_z > 0 ? dims->n_lin_z : 1) * a.table_stride;
   if (a.M == 0) return AVR_OK;
   return dispatch_field_x3(dims->d_hidden, a, as_stream(stream));
 }
 
-extern "C" int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd,
-                             const float* out, const float* grad_out, const uint32_t* mask, int64_t n_points,
+extern "C" int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd, int n_scenes,
+                             int64_t n_points, const float* out, const float* grad_out, const uint32_t* mask,
                              float* grads, int64_t grads_rows, uint32_t* grads_max, void* stream) {
   BwdArgs a{};
   int rc = make_layout(dims, &a.L);
   if (rc) return rc;
   AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_bwd: the training path is x3 only");
-  AVR_REQUIRE(n_points >= 0, "avr_field_bwd: bad size");
+  AVR_REQUIRE(n_points >= 0 && n_scenes >= 1, "avr_field_bwd: bad size");
   if (n_points == 0) return AVR_OK;
   AVR_REQUIRE(packed && packed_bwd && out && grad_out && mask && grads, "avr_field_bwd: null pointer");
-  AVR_REQUIRE(grads_rows >= n_points, "avr_field_bwd: grads_rows < n_points");
+  AVR_REQUIRE(grads_rows >= n_scenes * n_points, "avr_field_bwd: grads_rows < n_scenes * n_points");
   make_bwd_layout(dims, &a.LB);
   a.packed = packed;
   a.packed_bwd = packed_bwd;
   a.n_blocks = dims->n_blocks;
   a.M = n_points;
+  a.n_scenes = n_scenes;
+  a.blocks_per_scene = (n_points + kX3Samples - 1) / kX3Samples;
   a.out = reinterpret_cast<const float4*>(out);
   a.grad_out = reinterpret_cast<const float4*>(grad_out);
   a.mask = mask;

@@ -58,8 +58,8 @@ __device__ __forceinline__ void store_rows(float* G, const floatx4 (&v)[FT][4], 
 // layer l's rows + its running max |G| (mx: the wave's max |v|)
 template <int FT, int NW>
 __device__ __forceinline__ void store_layer(const BwdArgs& a, int layer, const floatx4 (&v)[FT][4], float mx,
-                                            int64_t base, int wid, int g, int j, int lane) {
-  store_rows<FT, NW>(a.G + layer * a.g_stride, v, base, a.M, wid, g, j);
+                                            int64_t base, int64_t roff, int wid, int g, int j, int lane) {
+  store_rows<FT, NW>(a.G + layer * a.g_stride + roff * (16 * FT * NW), v, base, a.M, wid, g, j);
   if (a.g_max && lane == 0) atomicMax(a.g_max + layer, __float_as_uint(mx));
 }
 
@@ -91,7 +91,9 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   float* red = lds + KC * 2048;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, j = lane & 15;
-  const int64_t base = (int64_t)blockIdx.x * kX3Samples;
+  const int scene = (int)(blockIdx.x / a.blocks_per_scene);   // the forward's workgroup -> scene map
+  const int64_t base = (int64_t)(blockIdx.x - (int64_t)scene * a.blocks_per_scene) * kX3Samples;
+  const int64_t roff = (int64_t)scene * a.M;
   const int nb = a.n_blocks;
   const uint4* PB = reinterpret_cast<const uint4*>(a.packed_bwd);
 
@@ -103,7 +105,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   for (int sg = 0; sg < 4; ++sg) {
     const int64_t m = base + 16 * sg + j;
     const bool ok = m < a.M;
-    const float4 o = a.out[ok ? m : a.M - 1], go = a.grad_out[ok ? m : a.M - 1];
+    const float4 o = a.out[roff + (ok ? m : a.M - 1)], go = a.grad_out[roff + (ok ? m : a.M - 1)];
     d4[sg][0] = ok ? go.x * ((1.f - o.x) * o.x) : 0.f;
     d4[sg][1] = ok ? go.y * ((1.f - o.y) * o.y) : 0.f;
     d4[sg][2] = ok ? go.z * ((1.f - o.z) * o.z) : 0.f;
@@ -129,7 +131,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   for (int b = nb - 1; b >= 0; --b) {
     // ---- fc_1^T
     float mx = absmax<FT>(dx);
-    store_layer<FT, NW>(a, 2 * b + 1, dx, mx, base, wid, g, j, lane);
+    store_layer<FT, NW>(a, 2 * b + 1, dx, mx, base, roff, wid, g, j, lane);
     const uint4* W1 = PB + a.LB.fc1t[b] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W1, lane);
     float s_x = publish<FT, NW>(X16, dx, mx, red, wid, lane, g, j);
@@ -141,7 +143,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
 #pragma unroll
       for (int sg = 0; sg < 4; ++sg) t[ft][sg] = masked<FT>(t[ft][sg] * inv, mb, ft, sg);
     mx = absmax<FT>(t);
-    store_layer<FT, NW>(a, 2 * b, t, mx, base, wid, g, j, lane);
+    store_layer<FT, NW>(a, 2 * b, t, mx, base, roff, wid, g, j, lane);
     // ---- fc_0^T
     const uint4* W0 = PB + a.LB.fc0t[b] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W0, lane);
@@ -154,7 +156,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
 #pragma unroll
       for (int sg = 0; sg < 4; ++sg) dx[ft][sg] += masked<FT>(t[ft][sg] * inv, mb, ft, sg);
   }
-  store_layer<FT, NW>(a, 2 * nb, dx, absmax<FT>(dx), base, wid, g, j, lane);
+  store_layer<FT, NW>(a, 2 * nb, dx, absmax<FT>(dx), base, roff, wid, g, j, lane);
 }
 
 template <int FT, int NW>
@@ -168,7 +170,7 @@ static int launch_bwd(const BwdArgs& a, hipStream_t s) {
       return fail(AVR_E_HIP, "field_bwd_x3_kernel: cannot set dynamic LDS to %zu", shm);
     attr = true;
   }
-  const int64_t blocks = (a.M + kX3Samples - 1) / kX3Samples;
+  const int64_t blocks = a.blocks_per_scene * a.n_scenes;
   AVR_REQUIRE(blocks < (1ll << 31), "field backward: too many points");
   field_bwd_x3_kernel<FT, NW><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("field_bwd_x3_kernel");

@@ -82,6 +82,13 @@ struct FieldArgs {
   int64_t act_stride;          //   floats between layers
   unsigned* mask;              //   their relu masks (see mask_words)
   unsigned* act_max;           //   per-layer max |act| as float bits (atomicMax), or null
+  // training forward over several scenes in one launch: workgroup b works on
+  // scene b / blocks_per_scene (M points each, rows scene * M + m), with that
+  // scene's view and lin_z tables (table + scene * table_scene_stride)
+  int n_scenes;
+  int64_t blocks_per_scene;
+  int64_t table_scene_stride;
+  View views[AVR_MAX_SCENES];
   unsigned long long* stamps;  // diagnostic builds (-DAVR_STAMPS) only: per-block phase clocks (waves 0, 4)
   int debug;                   // diagnostic builds only: experiment flags (1: every fc layer uses block 0's weights)
 };
@@ -151,6 +158,17 @@ __device__ __forceinline__ Bilinear bilinear_from_rot(const View& v, const float
   bl.tex[2] = Y1 * v.W + X0; bl.w[2] = fmul(wx0, wy1);
   bl.tex[3] = Y1 * v.W + X1; bl.w[3] = fmul(wx1, wy1);
   return bl;
+}
+
+// Explicit points: xyz / viewdir of point mm under view v.
+__device__ __forceinline__ SampleGeom sample_geom_pts(const View& v, const float* xyz, const float* vd, int64_t mm) {
+  const float x0 = xyz[3 * mm], x1 = xyz[3 * mm + 1], x2 = xyz[3 * mm + 2];
+  const float d0 = vd[3 * mm], d1 = vd[3 * mm + 1], d2 = vd[3 * mm + 2];
+  SampleGeom s;
+  s.xr[0] = dot3(v.R + 0, x0, x1, x2); s.xr[1] = dot3(v.R + 3, x0, x1, x2); s.xr[2] = dot3(v.R + 6, x0, x1, x2);
+  s.vr[0] = dot3(v.R + 0, d0, d1, d2); s.vr[1] = dot3(v.R + 3, d0, d1, d2); s.vr[2] = dot3(v.R + 6, d0, d1, d2);
+  s.bl = bilinear_from_rot(v, s.xr);
+  return s;
 }
 
 __device__ __forceinline__ SampleGeom sample_geom(const FieldArgs& a, int64_t mm) {
@@ -243,6 +261,8 @@ struct BwdArgs {
   float* G;                 // layer-output gradients, layer l at G + l * g_stride, (M, d_hidden)
   int64_t g_stride;
   unsigned* g_max;          // per-layer max |G| as float bits (atomicMax), or null
+  int n_scenes;             // M points per scene, rows scene * M + m
+  int64_t blocks_per_scene; // workgroup b: scene b / blocks_per_scene (the forward's map)
 };
 
 int dispatch_field_bwd_x3(int d_hidden, const BwdArgs& a, hipStream_t s);

@@ -184,9 +184,9 @@ struct LdsPlan {
 // weight-gradient split scales.
 template <int FT, int NW>
 __device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const floatx4 (&v)[FT][4], float mx,
-                                           int64_t base, int wid, int g, int j, int lane) {
+                                           int64_t base, int64_t roff, int wid, int g, int j, int lane) {
   constexpr int HID = 16 * FT * NW, MW = mask_words(FT);
-  float* act = a.act + (int64_t)layer * a.act_stride;
+  float* act = a.act + (int64_t)layer * a.act_stride + roff * HID;
   if (a.act_max && lane == 0) atomicMax(a.act_max + layer, __float_as_uint(mx));
   unsigned bits[MW];
 #pragma unroll
@@ -226,7 +226,15 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, j = lane & 15;
   const int gg = g + 4 * (wid >> 2);               // prologue: sub-lane of sample 16 (wid & 3) + j
-  const int64_t base = (int64_t)blockIdx.x * kX3Samples;
+  // SAVE: one training launch covers every scene of the batch (scene of this workgroup, its rows)
+  int scene = 0;
+  int64_t lblk = blockIdx.x;
+  if (SAVE) {
+    scene = (int)(blockIdx.x / a.blocks_per_scene);
+    lblk = blockIdx.x - (int64_t)scene * a.blocks_per_scene;
+  }
+  const int64_t base = lblk * kX3Samples;
+  const int64_t roff = SAVE ? (int64_t)scene * a.M : 0;
   const Layout& L = a.L;
   const uint4* P16 = reinterpret_cast<const uint4*>(a.packed);  // 16-B units
 
@@ -245,7 +253,9 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   {
     const int s = 16 * (wid & 3) + j;
     const int64_t m = base + s;
-    const SampleGeom geo = sample_geom(a, m < a.M ? m : a.M - 1);
+    const int64_t mm = m < a.M ? m : a.M - 1;
+    const SampleGeom geo = SAVE ? sample_geom_pts(a.views[scene], a.xyz + 3 * roff, a.vd + 3 * roff, mm)
+                                : sample_geom(a, mm);
     if (g == 0 && wid < 4) {
       *reinterpret_cast<int4*>(tail->tex + 4 * s) = make_int4(geo.bl.tex[0], geo.bl.tex[1], geo.bl.tex[2], geo.bl.tex[3]);
       *reinterpret_cast<float4*>(tail->w + 4 * s) = make_float4(geo.bl.w[0], geo.bl.w[1], geo.bl.w[2], geo.bl.w[3]);
@@ -332,7 +342,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     // + lin_z[b](interp latent) (models.py ResnetFC: x = x + lin_z[b](z) before block b)
     // (fused with the fc_0 input prep: v = relu(h), mx)
     if (b < a.n_lin_z) lds_barrier();  // every wave is done reading X (the stage aliases it)
-    const float* table = a.table + b * a.table_stride;
+    const float* table = a.table + b * a.table_stride + (SAVE ? scene * a.table_scene_stride : 0);
     if (b < a.n_lin_z && D <= P::CAP) {
       stage_rows<HID, NW>(stage, table, tail, 0, D, P::RS, lane, wid);
       AVR_STAMP(29);
@@ -354,7 +364,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
     }
     AVR_STAMP(5 + 5 * (b & 3));
-    if (SAVE) save_layer<FT, NW>(a, 2 * b, v, mx, base, wid, g, j, lane);
+    if (SAVE) save_layer<FT, NW>(a, 2 * b, v, mx, base, roff, wid, g, j, lane);
     const uint4* W0 = P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W0, lane);
     s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
@@ -365,7 +375,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     AVR_STAMP(7 + 5 * (b & 3));
     // fc_1 input relu(t + b0)
     mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
-    if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, mx, base, wid, g, j, lane);
+    if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, mx, base, roff, wid, g, j, lane);
     const uint4* W1 = P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W1, lane);
     s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
@@ -398,7 +408,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     for (int c = 0; c < KC / 4; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
   }
   mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
-  if (SAVE) save_layer<FT, NW>(a, 2 * a.n_blocks, v, mx, base, wid, g, j, lane);
+  if (SAVE) save_layer<FT, NW>(a, 2 * a.n_blocks, v, mx, base, roff, wid, g, j, lane);
   s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
   if (wid < 4) {
 #pragma unroll
@@ -422,7 +432,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   o *= 1.0f / S;
   AVR_STAMP(26);
   const int64_t m = base + 16 * wid + j;
-  if (g == 0 && m < a.M) a.out[m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
+  if (g == 0 && m < a.M)
+    a.out[roff + m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
 }
 
 template <int FT, int NW, bool SAVE>
@@ -435,7 +446,7 @@ static int launch_x3(const FieldArgs& a, hipStream_t s) {
       return fail(AVR_E_HIP, "field_x3_kernel: cannot set dynamic LDS to %zu", shm);
     attr = true;
   }
-  const int64_t blocks = (a.M + kX3Samples - 1) / kX3Samples;
+  const int64_t blocks = SAVE ? a.blocks_per_scene * a.n_scenes : (a.M + kX3Samples - 1) / kX3Samples;
   AVR_REQUIRE(blocks < (1ll << 31), "field: too many points");
   field_x3_kernel<FT, NW, SAVE><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("field_x3_kernel");

@@ -26,6 +26,7 @@ extern "C" {
 
 #define AVR_ABI_VERSION 3
 #define AVR_MAX_BLOCKS 8
+#define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
 enum {
   AVR_OK = 0,
@@ -195,10 +196,14 @@ int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, 
  * through the ResnetFC: models.py:541-592, :454-470, :856-862), on the x3
  * path (dims->precision must be AVR_FIELD_X3).
  *
+ * Both take a batch of n_scenes (<= AVR_MAX_SCENES) scenes of n_points points
+ * each in one launch: views[n_scenes] (host array), tables = the scenes'
+ * avr_field_latent_table outputs back to back, xyz / viewdirs (n_scenes,
+ * n_points, 3), out (n_scenes * n_points, 4); rows r = scene * n_points + m.
  * Forward: avr_field_fwd_points_train = avr_field_fwd_points that also writes
- *   act  (2 n_blocks + 1) layers of (n_points, d_hidden) fp32, layer l at
- *        act + l * act_rows * d_hidden (act_rows >= n_points, so calls for
- *        several scenes can fill one buffer): the relu'd input of every
+ *   act  (2 n_blocks + 1) layers of (rows, d_hidden) fp32, layer l at
+ *        act + l * act_rows * d_hidden (act_rows >= n_scenes * n_points, so
+ *        calls for more scenes can fill one buffer): the relu'd input of every
  *        hidden GEMM, act[2b] = relu(x) into fc_0 of block b, act[2b+1] =
  *        relu(fc_0 out) into fc_1, act[2 n_blocks] = relu(x) into lin_out;
  *   mask (mask_words) their relu masks (opaque, read by avr_field_bwd);
@@ -215,16 +220,17 @@ int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, 
  * grads[2b-1] (b >= 1) or grads[2 n_blocks] (b = 0), the gradient at block
  * b's input). packed_bwd: avr_field_bwd_packed_floats floats, filled by
  * avr_field_pack_bwd (fc_0 / fc_1 transposed, x3 fragments).                    */
-int avr_field_train_sizes(const avr_field_dims* dims, int64_t n_points, int64_t* act_floats, int64_t* mask_words);
+int avr_field_train_sizes(const avr_field_dims* dims, int n_scenes, int64_t n_points, int64_t* act_floats,
+                          int64_t* mask_words);
 int avr_field_bwd_packed_floats(const avr_field_dims* dims, int64_t* n_floats);
 int avr_field_pack_bwd(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed_bwd, void* stream);
-int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
-                               const float* table, const float* xyz, const float* viewdirs, int64_t n_points,
-                               float* out, float* act, int64_t act_rows, uint32_t* mask, uint32_t* act_max,
-                               void* stream);
-int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd, const float* out,
-                  const float* grad_out, const uint32_t* mask, int64_t n_points, float* grads, int64_t grads_rows,
-                  uint32_t* grads_max, void* stream);
+int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
+                               const float* packed, const float* tables, const float* xyz, const float* viewdirs,
+                               int64_t n_points, float* out, float* act, int64_t act_rows, uint32_t* mask,
+                               uint32_t* act_max, void* stream);
+int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd, int n_scenes,
+                  int64_t n_points, const float* out, const float* grad_out, const uint32_t* mask, float* grads,
+                  int64_t grads_rows, uint32_t* grads_max, void* stream);
 
 /* Weight gradients of linear layers, dW = G^T X and db = sum_rows G (the
  * parameter half of nn.Linear's autograd, models.py:541-592), for up to
