@@ -158,11 +158,12 @@ class _Composite(torch.autograd.Function):
         return gz, gfield if ctx.needs_input_grad[1] else None, None, None
 
 
-def composite(z, field, white_back=True, infinity=1.8):
-    """Differentiable volume_integral on (R,N) z and (R,N,4) field."""
+def composite(z, field, white_back=True, infinity=1.8, want_weights=True):
+    """Differentiable volume_integral on (R,N) z and (R,N,4) field. Without
+    autograd, want_weights=False skips the (R,N) weights store (returns None)."""
     if torch.is_grad_enabled() and (field.requires_grad or z.requires_grad):
         return _Composite.apply(z, field, white_back, infinity)
-    return composite_fwd(z, field, white_back, infinity)
+    return composite_fwd(z, field, white_back, infinity, want_weights=want_weights)
 
 
 def points(ro, rd, z):

@@ -190,7 +190,8 @@ class VolumeRenderer(nn.Module):
             rgb_f, dist_f = self._fine_early_termination(ro, rd, z_sorted, radiance_field, fuse, SB, R)
         else:
             ff = field(z_sorted, False)
-            rgb_f, dist_f, _ = ops.composite(z_sorted, ff, self.white_back)
+            # the fine weights are not returned (renderers.py:264-277): no store without autograd
+            rgb_f, dist_f, _ = ops.composite(z_sorted, ff, self.white_back, want_weights=False)
             self.last_fine_samples = z_sorted.numel()
         depth = ops.depth_from_world(ro, rd, dist_f.reshape(SB, R), c2w_info)
         assert z_sorted.shape[-1] == Nt

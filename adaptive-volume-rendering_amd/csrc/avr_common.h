@@ -99,4 +99,55 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const unsigned long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// ---- DPP wave64 scans (no LDS traffic, unlike __shfl's ds_bpermute).
+// dpp_d: the double of the lane named by CTRL (row_shr:n, row_bcast:15/31,
+// wave_shr:1); lanes without a source (or outside ROW_MASK) get `ident`.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v, double ident) {
+  const unsigned long long b = __double_as_longlong(v), e = __double_as_longlong(ident);
+  const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)e, (int)(unsigned)b, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(unsigned)(e >> 32), (int)(unsigned)(b >> 32), CTRL, ROW_MASK, 0xf,
+                                             false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
+constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShr1 = 0x138;
+
+// Inclusive scan (Hillis-Steele in rows of 16, then row broadcasts); OP(a, b).
+template <typename OP>
+__device__ __forceinline__ double wave_incl_scan_dpp(double v, double ident, OP op) {
+  v = op(v, dpp_d<kDppRowShr1>(v, ident));
+  v = op(v, dpp_d<kDppRowShr2>(v, ident));
+  v = op(v, dpp_d<kDppRowShr4>(v, ident));
+  v = op(v, dpp_d<kDppRowShr8>(v, ident));
+  v = op(v, dpp_d<kDppRowBcast15, 0xa>(v, ident));
+  v = op(v, dpp_d<kDppRowBcast31, 0xc>(v, ident));
+  return v;
+}
+
+// Exclusive product scan of doubles (lane 0 gets 1) and the wave total.
+__device__ __forceinline__ double wave_excl_prod_dpp(double v, double& total) {
+  const double incl = wave_incl_scan_dpp(v, 1.0, [](double a, double b) { return a * b; });
+  total = readlane_d(incl, 63);
+  return dpp_d<kDppWaveShr1>(incl, 1.0);
+}
+
+// Exclusive sum scan of doubles (lane 0 gets 0).
+__device__ __forceinline__ double wave_excl_sum_dpp(double v) {
+  const double incl = wave_incl_scan_dpp(v, 0.0, [](double a, double b) { return a + b; });
+  return dpp_d<kDppWaveShr1>(incl, 0.0);
+}
+
+__device__ __forceinline__ double wave_total_sum_dpp(double v) {
+  return readlane_d(wave_incl_scan_dpp(v, 0.0, [](double a, double b) { return a + b; }), 63);
+}
+
 }  // namespace avr

@@ -58,6 +58,13 @@ __device__ __forceinline__ SampleTerms sample_terms(const float* __restrict__ zr
   return s;
 }
 
+// Forward: lane l owns the K consecutive samples [K l, K l + K) of its ray
+// (K = ceil(N / 64)), so the transmittance needs ONE wave scan: a sequential
+// fp64 product over the lane's own samples, a DPP exclusive product scan of
+// the lane totals, and the lane-local expansion. rgb / dist are fp64 lane sums
+// reduced by a DPP scan; the white-background sum reads w back from LDS in the
+// torch-CPU cascade order. No block barriers: every ray is one wave.
+template <int K>
 __global__ void __launch_bounds__(256) composite_fwd_kernel(const float* __restrict__ z,
                                                             const float4* __restrict__ field, int64_t n_rays, int N,
                                                             int white_back, float infinity, float* __restrict__ rgb,
@@ -70,31 +77,52 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(const float* __restr
   float* scratch = wbuf + N;
   const float* zr = z + ray * N;
   const float4* fr = field + ray * N;
-  double carry = 1.0, r = 0.0, g = 0.0, b = 0.0, dd = 0.0;
-  for (int base = 0; base < N; base += 64) {
-    const int n = base + lane;
+  const int n0 = K * lane;
+  float4 f[K];
+  float zv[K + 1];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int n = n0 + k;
+    f[k] = n < N ? fr[n] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k <= K; ++k) zv[k] = n0 + k < N ? zr[n0 + k] : 0.f;
+  float alpha[K], zz[K];
+  double P[K + 1];     // P[k] = prod of t over the lane's samples before k (sequential fp64)
+  P[0] = 1.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int n = n0 + k;
     const bool ok = n < N;
-    float4 f = ok ? fr[n] : make_float4(0.f, 0.f, 0.f, 0.f);
-    SampleTerms s = ok ? sample_terms(zr, n, N, f.w, infinity) : SampleTerms{0.f, 1.f, 0.f, 1.f, 0.f};
-    const double incl = wave_incl_scan_mul((double)s.t, lane) * carry;
-    double excl = __shfl_up(incl, 1, 64);
-    if (lane == 0) excl = carry;
-    carry = __shfl(incl, 63, 64);
-    const float T = (float)excl;
-    const float w = fmul(s.alpha, T);
-    if (ok) {
+    const bool last = (n == N - 1);
+    const float d = last ? 1e10f : fsub(zv[k + 1], zv[k]);
+    zz[k] = last ? infinity : zv[k + 1];
+    const float e = expf(-fmul(f[k].w, d));
+    alpha[k] = ok ? fsub(1.0f, e) : 0.f;
+    const float t = ok ? fadd(fsub(1.0f, alpha[k]), 1e-10f) : 1.f;
+    P[k + 1] = P[k] * (double)t;
+  }
+  double total;
+  const double excl = wave_excl_prod_dpp(P[K], total);
+  double r = 0.0, g = 0.0, b = 0.0, dd = 0.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int n = n0 + k;
+    const float T = (float)(excl * P[k]);
+    const float w = fmul(alpha[k], T);
+    if (n < N) {
       wbuf[n] = w;
       if (w_out) w_out[ray * N + n] = w;
-      r += (double)w * f.x;
-      g += (double)w * f.y;
-      b += (double)w * f.z;
-      dd += (double)w * s.zz;
+      r += (double)w * f[k].x;
+      g += (double)w * f[k].y;
+      b += (double)w * f[k].z;
+      dd += (double)w * zz[k];
     }
   }
-  r = wave_sum_d(r);
-  g = wave_sum_d(g);
-  b = wave_sum_d(b);
-  dd = wave_sum_d(dd);
+  r = wave_total_sum_dpp(r);
+  g = wave_total_sum_dpp(g);
+  b = wave_total_sum_dpp(b);
+  dd = wave_total_sum_dpp(dd);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   float acc = 0.f;
@@ -205,8 +233,19 @@ extern "C" int avr_composite_fwd(const float* z, const float* field, int64_t n_r
   AVR_REQUIRE(z && field && rgb && dist, "avr_composite_fwd: null pointer");
   const size_t shm = (size_t)kCompWaves * (n_samples + 64) * sizeof(float);
   const unsigned grid = (unsigned)((n_rays + kCompWaves - 1) / kCompWaves);
-  composite_fwd_kernel<<<grid, 64 * kCompWaves, shm, as_stream(stream)>>>(
-      z, reinterpret_cast<const float4*>(field), n_rays, n_samples, white_back, infinity, rgb, dist, weights);
+  const float4* f4 = reinterpret_cast<const float4*>(field);
+  hipStream_t st = as_stream(stream);
+#define AVR_COMP_K(KK)                                                                                          \
+  case KK:                                                                                                      \
+    composite_fwd_kernel<KK><<<grid, 64 * kCompWaves, shm, st>>>(z, f4, n_rays, n_samples, white_back, infinity, \
+                                                                 rgb, dist, weights);                           \
+    break;
+  switch ((n_samples + 63) / 64) {
+    AVR_COMP_K(1) AVR_COMP_K(2) AVR_COMP_K(3) AVR_COMP_K(4) AVR_COMP_K(5) AVR_COMP_K(6) AVR_COMP_K(7) AVR_COMP_K(8)
+    AVR_COMP_K(9) AVR_COMP_K(10) AVR_COMP_K(11) AVR_COMP_K(12) AVR_COMP_K(13) AVR_COMP_K(14) AVR_COMP_K(15)
+    AVR_COMP_K(16)
+  }
+#undef AVR_COMP_K
   return check_launch("composite_fwd_kernel");
 }
 

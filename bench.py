@@ -97,6 +97,66 @@ class FieldTimer:
         return sum(s.elapsed_time(e) for s, e in self.events)
 
 
+class HbmKernelTimer:
+    """The renderer's HBM-bound launches (avr.ops wrappers; each enqueues one
+    kernel on torch's current stream), measured in isolation: the arguments of
+    their first call inside the timed steps are kept and every launch is then
+    replayed `reps` times back to back between two HIP events, so the average
+    is kernel time without host launch gaps. Bytes are ALGORITHMIC per launch
+    (SURVEY §8d): compulsory reads + writes, fp32, Philox noise (no noise bytes)."""
+
+    def __init__(self, ops):
+        self.ops = ops
+        self.calls = {}    # label -> (fn, args, kwargs, bytes)
+        self.on = False
+
+    def _wrap(self, name, kernel, nbytes):
+        orig = getattr(self.ops, name)
+
+        def timed(*a, **k):
+            out = orig(*a, **k)
+            if self.on:
+                nb, what = nbytes(a, k, out)
+                label = f"{kernel} ({what})" if what else kernel
+                self.calls.setdefault(label, (orig, a, k, nb))
+            return out
+
+        setattr(self.ops, name, timed)
+
+    def install(self):
+        def composite_bytes(a, k, out):
+            R, N = a[0].shape
+            ww = out[2] is not None
+            return R * (N * (4 + 16 + (4 if ww else 0)) + 16), f"N={N}, weights {'stored' if ww else 'not stored'}"
+
+        def sample_fine_bytes(a, k, out):
+            w, zc = a[0], a[1]
+            return w.numel() * 4 + zc.numel() * 4 + out[0].numel() * 4, f"Nc={zc.shape[1]}, out {out[0].shape[1]}"
+
+        self._wrap("world_rays", "world_rays_kernel", lambda a, k, out: (a[0].shape[0] * a[0].shape[1] * 32, ""))
+        self._wrap("sample_coarse", "sample_coarse_kernel", lambda a, k, out: (out.numel() * 4, f"N={out.shape[1]}"))
+        self._wrap("composite_fwd", "composite_fwd_kernel", composite_bytes)
+        self._wrap("sample_fine", "sample_fine_kernel", sample_fine_bytes)
+        self._wrap("depth_from_world_fwd", "depth_kernel", lambda a, k, out: (a[0].shape[0] * a[0].shape[1] * 32, ""))
+
+    def report(self, reps=20):
+        res = []
+        for label, (fn, a, k, nb) in self.calls.items():
+            fn(*a, **k)
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                fn(*a, **k)
+            e.record()
+            e.synchronize()
+            us = s.elapsed_time(e) * 1e3 / reps
+            gbs = nb / (us * 1e-6) / 1e9
+            res.append({"kernel": label, "avg_us": round(us, 2), "bytes_per_launch": int(nb),
+                        "achieved_GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)})
+        return res
+
+
 def cpu_baseline(rays_cap=4096, budget_s=12.0):
     """The oracle (numpy restatement of the reference path, 'port') on this
     host's cores, on a bounded sample of the same workload: 128-ray chunks of
@@ -242,6 +302,8 @@ def main():
     fused = net.fused()
     timer = FieldTimer()
     timer.wrap(fused)
+    hbm = HbmKernelTimer(avr.ops)
+    hbm.install()
     rend = VolumeRenderer(0.8, 1.8, args.n_coarse, args.n_fine, 0, 0.01, True)
     rend.seed = 1234 + rank
     if args.config == 4:
@@ -276,6 +338,7 @@ def main():
     assert rend.last_path == "fused", "bench must run the fused HIP field"
     torch.cuda.synchronize()
     timer.reset()
+    hbm.on = True
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -347,6 +410,8 @@ def main():
             "field_share_of_step": round(field_ms / (elapsed * 1e3), 4),
         },
     }
+    # the renderer's HBM-bound kernels (the metric's "achieved HBM GB/s vs roofline"), HIP events per launch
+    line["hbm_kernels"] = hbm.report()
     pmc = os.path.join(REPO, "profiles", "field_pmc.json")
     if os.path.exists(pmc):
         with open(pmc) as f:

@@ -173,12 +173,15 @@ def positional_encoding(x, num_freqs=6, freq_factor=1.5, include_input=True):
     return np.concatenate([x, emb], -1) if include_input else emb
 
 
-def grid_sample_bilinear_border(latent, uv, latent_scaling, image_shape):
+def grid_sample_bilinear_border(latent, uv, latent_scaling, image_shape, rows=None):
     """SpatialEncoder.index (models.py:245-274): uv*scale - 1, then
     F.grid_sample(bilinear, padding=border, align_corners=True).
-    latent (L,H,W), uv (B,2) -> (B,L)."""
+    latent (L,H,W), uv (B,2) -> (B,L). `rows` is the same latent as (H*W, L)
+    texel rows (a layout cache: the gathers then read contiguous rows)."""
     latent = np.asarray(latent, F32)
     L, H, W = latent.shape
+    if rows is None:
+        rows = np.ascontiguousarray(latent.reshape(L, H * W).T)
     scale = (np.asarray(latent_scaling, F32) / np.asarray(image_shape, F32)).astype(F32)
     g = (np.asarray(uv, F32) * scale - F32(1.0)).astype(F32)
     ix = ((g[:, 0] + F32(1)) / F32(2)) * F32(W - 1)
@@ -195,13 +198,13 @@ def grid_sample_bilinear_border(latent, uv, latent_scaling, image_shape):
         ok = (xx <= W - 1) & (yy <= H - 1)
         xi = np.minimum(xx, W - 1).astype(np.int64)
         yi = np.minimum(yy, H - 1).astype(np.int64)
-        vals = latent[:, yi, xi].T.astype(np.float64)                  # (B,L)
-        out += np.where(ok, ww, 0).astype(np.float64)[:, None] * vals
+        out += np.where(ok, ww, 0).astype(np.float64)[:, None] * rows[yi * W + xi]   # fp64 accumulate
     return out.astype(F32)
 
 
 def _linear(x, W, b):
-    return (x @ np.asarray(W, F32).T + np.asarray(b, F32)).astype(F32)
+    y = np.asarray(x, F32) @ np.asarray(W, F32).T
+    return np.add(y, np.asarray(b, F32), out=y)
 
 
 def resnetfc_forward(zx, p, d_latent, n_blocks, combine_layer):
@@ -228,6 +231,8 @@ class PixelNeRFField:
                  n_blocks=3, combine_layer=1000, num_freqs=6, freq_factor=1.5):
         self.pc, self.pf = params_coarse, params_fine
         self.latent = np.asarray(latent, F32).reshape(np.asarray(latent).shape[-3:])
+        L_, H_, W_ = self.latent.shape
+        self.latent_rows = np.ascontiguousarray(self.latent.reshape(L_, H_ * W_).T)   # (H*W, L) texel rows
         self.poses = np.asarray(poses, F32).reshape(3, 4)
         self.focal = np.asarray(focal, F32).reshape(2)
         self.c = np.asarray(c, F32).reshape(2)
@@ -248,7 +253,7 @@ class PixelNeRFField:
         zf = np.concatenate([zf, vd], -1)
         uv = -xyz_c[:, :2] / xyz_c[:, 2:]
         uv = uv * self.focal + self.c
-        lat = grid_sample_bilinear_border(self.latent, uv, self.latent_scaling, self.image_shape)
+        lat = grid_sample_bilinear_border(self.latent, uv, self.latent_scaling, self.image_shape, self.latent_rows)
         return lat, zf
 
     def __call__(self, xyz, viewdirs, coarse=True):

@@ -64,6 +64,27 @@ def test_composite_bwd_golden(golden, N, wb):
     np.testing.assert_allclose(got / scale, ref / scale, atol=1e-4, rtol=0)
 
 
+@pytest.mark.parametrize("N", [1, 5, 63, 65, 100, 333, 1024])
+def test_composite_fwd_lane_segments(N):
+    """Every lane-segment width K = ceil(N/64) (1..16), ragged last lanes,
+    weights stored or not, against the oracle."""
+    from avr import ops
+    R = 97
+    rng = np.random.default_rng(N)
+    z = np.sort(rng.uniform(0.8, 1.8, (R, N)).astype(np.float32), -1)
+    sig = np.maximum(rng.normal(0, 30, (R, N, 1)), 0).astype(np.float32)
+    sig[::5] = 0.0
+    rad = rng.random((R, N, 3), dtype=np.float32)
+    field = T(np.concatenate([rad, sig], -1))
+    orgb, odep, ow = O.volume_integral(z[None], sig[None], rad[None], True)
+    rgb, dist, w = ops.composite_fwd(T(z), field, True)
+    np.testing.assert_allclose(to_np(w), ow[0, ..., 0], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(to_np(rgb), orgb[0], atol=2e-6, rtol=0)
+    np.testing.assert_allclose(to_np(dist), odep[0, :, 0], atol=2e-6, rtol=0)
+    rgb2, dist2, w2 = ops.composite_fwd(T(z), field, True, want_weights=False)
+    assert w2 is None and torch.equal(rgb2, rgb) and torch.equal(dist2, dist)
+
+
 def test_composite_edge_cases():
     from avr import ops
     # one sample per ray, a ray of all zeros, a huge sigma
@@ -128,6 +149,43 @@ def test_sample_coarse_bit_exact():
     z = ops.sample_coarse(0.8, 1.8, R, N, DEV, noise=T(noise))
     ref = O.sample_coarse(np.full((1, R), 0.8, np.float32), np.full((1, R), 1.8, np.float32), N, noise[None])[0]
     np.testing.assert_array_equal(to_np(z), ref)
+
+
+@pytest.mark.parametrize("N", [1, 6, 37, 64])
+def test_sample_coarse_ragged_bit_exact(N):
+    """N not a multiple of the kernel's 4-sample blocks: explicit noise bit-exact;
+    in-kernel noise equal to the one-uniform-at-a-time draw (block k of ray r holds
+    samples 4k..4k+3), i.e. a prefix of the N=64 draw."""
+    from avr import ops
+    R = 301
+    noise = np.random.default_rng(N).random((R, N), dtype=np.float32)
+    z = ops.sample_coarse(0.8, 1.8, R, N, DEV, noise=T(noise))
+    ref = O.sample_coarse(np.full((1, R), 0.8, np.float32), np.full((1, R), 1.8, np.float32), N, noise[None])[0]
+    np.testing.assert_array_equal(to_np(z), ref)
+    zp = ops.sample_coarse(0.8, 1.8, R, N, DEV, seed=11, offset=5)
+    z64 = ops.sample_coarse(0.8, 1.8, R, 64, DEV, seed=11, offset=5)
+    u_n = (zp - (0.8 + torch.arange(N, device=DEV) / N)) * N
+    u_64 = (z64 - (0.8 + torch.arange(64, device=DEV) / 64)) * 64
+    torch.testing.assert_close(u_n, u_64[:, :N], atol=2e-5, rtol=0)
+
+
+def test_sample_fine_unsorted_coarse_fallback():
+    """z_coarse given out of order (the reference sorts cat(z_c, z_f) whatever
+    z_c holds): the wave-local bitonic path must equal numpy's sort."""
+    from avr import ops
+    R, Nc, Nf, Nd = 300, 64, 32, 8
+    rng = np.random.default_rng(5)
+    zc = rng.uniform(0.8, 1.8, (R, Nc)).astype(np.float32)
+    zc[: R // 2] = np.sort(zc[: R // 2], -1)          # half sorted (fast path), half not (fallback)
+    zc[::7, 3] = zc[::7, 4]                            # ties
+    w = rng.random((R, Nc), dtype=np.float32)
+    u, u2 = rng.random((R, Nf), dtype=np.float32), rng.random((R, Nf), dtype=np.float32)
+    nd = rng.normal(0, 1, (R, Nd)).astype(np.float32)
+    zs, idx, zf = ops.sample_fine(T(w), T(zc), 0.8, 1.8, Nf, Nd, 0.01, u=T(u), u2=T(u2), noise_depth=T(nd),
+                                  want_idx=True, want_fine=True)
+    od = np.clip(O.sample_depth(np.zeros((1, R, 1), np.float32), Nd, 0.01, nd[None]), np.float32(0.8),
+                 np.float32(1.8))[0]
+    np.testing.assert_array_equal(to_np(zs), np.sort(np.concatenate([zc, to_np(zf), od], -1), -1))
 
 
 def test_philox_noise_properties():
@@ -310,7 +368,7 @@ def test_volume_renderer_module_path_and_backward(golden):
     import avr.ops as ops
     orig = ops.composite
 
-    def torch_composite(z, field, white_back=True, infinity=1.8):
+    def torch_composite(z, field, white_back=True, infinity=1.8, want_weights=True):
         rgb, dist, w = vi_torch(z, field[..., 3:], field[..., :3])
         return rgb, dist[..., 0], w
 
