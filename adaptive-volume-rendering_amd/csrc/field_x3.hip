@@ -21,6 +21,8 @@
 // Accumulators stay in their scaled domain between layers (no unscale pass),
 // and the bilinear lin_z gather for block b+1 streams in during block b's fc_0
 // MFMAs (issued one K-chunk ahead, added into the residual).
+#include <stdlib.h>
+
 #include "x3_gemm.h"
 
 namespace avr {
@@ -94,7 +96,7 @@ __device__ __forceinline__ int dedup_texels(ZTail* tail, int lane, int wid) {
 // compiler wait for the earlier DMA to land.
 template <int HID, int NW>
 __device__ __forceinline__ void stage_rows(char* stage, const float* __restrict__ table, const ZTail* tail, int lo,
-                                           int n, int RS, int lane, int wid) {
+                                           int n, int RS, int lane, int wid, int dst0 = 0) {
   constexpr int ROWB = 4 * HID;                                  // bytes per row
   constexpr int PPR = ROWB >= 1024 ? ROWB / 1024 : 1;            // pieces per row
   constexpr int LANES = ROWB >= 1024 ? 64 : ROWB / 16;           // active lanes per piece
@@ -110,17 +112,26 @@ __device__ __forceinline__ void stage_rows(char* stage, const float* __restrict_
     const int r = pc / PPR, q = pc - r * PPR;
     const int row = __builtin_amdgcn_readlane(rowv, i);
     const char* src = reinterpret_cast<const char*>(table + (int64_t)row * HID) + 1024 * q + 16 * lane;
-    auto* dst = (__attribute__((address_space(3))) void*)(stage + r * RS + 1024 * q);
+    auto* dst = (__attribute__((address_space(3))) void*)(stage + (dst0 + r) * RS + 1024 * q);
     if (lane < LANES) __builtin_amdgcn_global_load_lds((const void*)src, dst, 16, 0, 0);
   }
 }
 
 typedef __attribute__((address_space(3))) char lds_char;
 
+template <int FT, bool ZERO, bool TWO, int SYNCP>
+__device__ __forceinline__ void gemm(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W, int KC,
+                                     int cstride, const uint4* X16, int lane) {
+  if constexpr (TWO)
+    gemm_x3_sg<FT, ZERO, SYNCP>(acc, A0, W, KC, cstride, X16, lane);
+  else
+    gemm_x3<FT, ZERO, false>(acc, A0, W, KC, cstride, X16, lane);
+}
+
 // h += S * sum_c w_c * row(slot_c) over the corners whose slot is in [lo, lo+n).
 // PREP: also v = relu(h * f) and the running max for the next publish (the
 // fc_0 input of the block), from the same register read of h.
-template <int FT, bool PREP>
+template <int FT, bool PREP, bool STOREV = true>
 __device__ __forceinline__ void blend_stage(floatx4 (&h)[FT][4], floatx4 (&v)[FT][4], float& mx, const char* stage_g,
                                             const ZTail* tail, int lo, int n, int RS, float S, float f, int wid, int g,
                                             int j) {
@@ -148,7 +159,7 @@ __device__ __forceinline__ void blend_stage(floatx4 (&h)[FT][4], floatx4 (&v)[FT
       if (PREP) {
         floatx4 x = hn * f;
         x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
-        v[ft][sg] = x;
+        if (STOREV) v[ft][sg] = x;
         mx = fmaxf(fmaxf(mx, x.x), fmaxf(fmaxf(x.y, x.z), x.w));
       }
       if (ft & 1) __builtin_amdgcn_sched_barrier(0);  // bound the LDS reads in flight (register pressure)
@@ -168,6 +179,7 @@ struct LdsPlan {
   static constexpr int WANT = (XB > 96 * RS ? XB : 96 * RS) + TAIL;
   static constexpr int BYTES = WANT < 160 * 1024 ? WANT : 160 * 1024;
   static constexpr int CAP = (BYTES - TAIL) / RS;
+  static constexpr int IN_ROWS0 = (kX3InChunks * 8192 + RS - 1) / RS;   // first row clear of lin_in's X
   static_assert(XB + TAIL <= BYTES, "X and tail must fit");
   static_assert(CAP * (4 * HID >= 1024 ? HID / 256 : 1) <= 4 * 64, "stage_rows: one lane per piece");
 };
@@ -211,13 +223,30 @@ __device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const 
 // VALU issue rate of the epilogues and hides one wave's stalls behind the
 // other); wave w owns the FT 16-row feature tiles FT*w .. FT*w + FT-1.
 // SAVE (training forward): also write every GEMM input and its relu mask.
-template <int FT, int NW, bool SAVE>
+// VAR (8-wave layout experiments): bits 0-1 GEMM sync period (see gemm_x3_sg:
+// 0 -> every chunk pair, 1 -> every second pair, 2 -> none); bit 2: waves 4-7 at
+// s_setprio 1; bit 3: waves 0-3 at s_setprio 1; bit 4: block 0's lin_z stage rows
+// past lin_in's X issued before the lin_in GEMM. (Issuing the next block's first
+// stage rows in the middle of fc_1 measured 1.4 % slower: every later weight
+// load then waits for the LDS-DMA in the in-order vmcnt.)
+template <int FT, int NW, bool SAVE, int VAR = 0>
 __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
+  constexpr int SYNCP = (VAR & 3) == 0 ? 1 : ((VAR & 3) == 1 ? 2 : 0);
   constexpr int HID = 16 * FT * NW;
   using P = LdsPlan<HID>;
   constexpr int KC = P::KC;
   constexpr int NTT = FT * NW;                     // feature tiles of a hidden layer
   constexpr int PES = (6 * 7 + NW - 1) / NW;       // PE slots per lane (6 * num_freqs <= 42)
+  // 8 waves (256 registers each): two-pass epilogues instead of a materialised layer input v
+  constexpr bool TWO = NW > 4;
+  static_assert(!(SAVE && TWO), "the training forward keeps the 4-wave layout");
+  const floatx4 bz[FT] = {};
+  if constexpr ((VAR & 4) != 0) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
+  if constexpr ((VAR & 8) != 0) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 256) __builtin_amdgcn_s_setprio(1);
+  }
   extern __shared__ float lds[];
   uint4* X16 = reinterpret_cast<uint4*>(lds);      // KCX * 512 slots of 16 B
   char* stage = reinterpret_cast<char*>(lds);
@@ -335,7 +364,16 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     for (int sg = 0; sg < 4; ++sg) h[ft][sg] = b * S_h;
   }
   AVR_STAMP(3);
-  gemm_x3<FT, false, (NW > 4)>(h, A0, Win, kX3InChunks, 64 * NTT, X16, lane);
+  // 8 waves: stage rows of the next lin_z table that are already in flight
+  // ([p0, p1), issued while the preceding GEMM still read other parts of X)
+  int p0 = 0, p1 = 0;
+  constexpr bool PRE0 = TWO && (VAR & 16);
+  if (PRE0 && a.n_lin_z > 0 && D <= P::CAP && D > P::IN_ROWS0) {
+    stage_rows<HID, NW>(stage, a.table, tail, P::IN_ROWS0, D - P::IN_ROWS0, P::RS, lane, wid, P::IN_ROWS0);
+    p0 = P::IN_ROWS0;
+    p1 = D;
+  }
+  gemm<FT, false, TWO, SYNCP>(h, A0, Win, kX3InChunks, 64 * NTT, X16, lane);
   AVR_STAMP(4);
 
   for (int b = 0; b < a.n_blocks; ++b) {
@@ -344,13 +382,15 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     if (b < a.n_lin_z) lds_barrier();  // every wave is done reading X (the stage aliases it)
     const float* table = a.table + b * a.table_stride + (SAVE ? scene * a.table_scene_stride : 0);
     if (b < a.n_lin_z && D <= P::CAP) {
-      stage_rows<HID, NW>(stage, table, tail, 0, D, P::RS, lane, wid);
+      if (p0 > 0) stage_rows<HID, NW>(stage, table, tail, 0, p0, P::RS, lane, wid, 0);
+      if (p1 < D) stage_rows<HID, NW>(stage, table, tail, p1, D - p1, P::RS, lane, wid, p1);
+      p0 = p1 = 0;
       AVR_STAMP(29);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       AVR_STAMP(30);
       mx = 0.f;
-      blend_stage<FT, true>(h, v, mx, stage, tail, 0, D, P::RS, S_h, 1.0f / S_h, wid, g, j);
+      blend_stage<FT, true, !TWO>(h, v, mx, stage, tail, 0, D, P::RS, S_h, 1.0f / S_h, wid, g, j);
       mx = wave_max(mx);
     } else {
       for (int lo = 0; b < a.n_lin_z && lo < D; lo += P::CAP) {   // more distinct texels than the stage holds
@@ -361,24 +401,35 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
         __syncthreads();
         blend_stage<FT, false>(h, v, mx, stage, tail, lo, n, P::RS, S_h, 1.0f / S_h, wid, g, j);
       }
-      mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
+      mx = TWO ? max_relu_affine<FT, false>(h, 1.0f / S_h, bz) : prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
     }
     AVR_STAMP(5 + 5 * (b & 3));
     if (SAVE) save_layer<FT, NW>(a, 2 * b, v, mx, base, roff, wid, g, j, lane);
     const uint4* W0 = P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W0, lane);
-    s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+    if constexpr (TWO)
+      s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
+    else
+      s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
     AVR_STAMP(6 + 5 * (b & 3));
     // fc_0 (from zero)
     const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
-    gemm_x3<FT, true, (NW > 4)>(t, A0, W0, KC, 64 * NTT, X16, lane);
+    gemm<FT, true, TWO, SYNCP>(t, A0, W0, KC, 64 * NTT, X16, lane);
     AVR_STAMP(7 + 5 * (b & 3));
     // fc_1 input relu(t + b0)
-    mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
-    if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, mx, base, roff, wid, g, j, lane);
     const uint4* W1 = P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
-    prefetch_a<FT>(A0, W1, lane);
-    s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+    if constexpr (TWO) {
+      floatx4 bv[FT];
+      load_bias<FT, true>(bv, a.packed + L.b_fc0[b], wid, g);
+      mx = max_relu_affine<FT, true>(t, 1.0f / S_t, bv);
+      prefetch_a<FT>(A0, W1, lane);
+      s_x = publish_affine<FT, NW, true>(X16, t, 1.0f / S_t, bv, mx, red, wid, lane, g, j);
+    } else {
+      mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
+      if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, mx, base, roff, wid, g, j, lane);
+      prefetch_a<FT>(A0, W1, lane);
+      s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+    }
     AVR_STAMP(8 + 5 * (b & 3));
     // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
     const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
@@ -395,7 +446,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
         for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb[ft];
     }
     S_h = S1;
-    gemm_x3<FT, false, (NW > 4)>(h, A0, W1, KC, 64 * NTT, X16, lane);
+    gemm<FT, false, TWO, SYNCP>(h, A0, W1, KC, 64 * NTT, X16, lane);
     AVR_STAMP(9 + 5 * (b & 3));
   }
 
@@ -407,9 +458,14 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
 #pragma unroll
     for (int c = 0; c < KC / 4; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
   }
-  mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
-  if (SAVE) save_layer<FT, NW>(a, 2 * a.n_blocks, v, mx, base, roff, wid, g, j, lane);
-  s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+  if constexpr (TWO) {
+    mx = max_relu_affine<FT, false>(h, 1.0f / S_h, bz);
+    s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
+  } else {
+    mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
+    if (SAVE) save_layer<FT, NW>(a, 2 * a.n_blocks, v, mx, base, roff, wid, g, j, lane);
+    s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+  }
   if (wid < 4) {
 #pragma unroll
     for (int c = KC / 4; c < KC; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
@@ -436,23 +492,43 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     a.out[roff + m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
 }
 
-template <int FT, int NW, bool SAVE>
+template <int FT, int NW, bool SAVE, int VAR = 0>
 static int launch_x3(const FieldArgs& a, hipStream_t s) {
   const size_t shm = LdsPlan<16 * FT * NW>::BYTES;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT, NW, SAVE>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT, NW, SAVE, VAR>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
       return fail(AVR_E_HIP, "field_x3_kernel: cannot set dynamic LDS to %zu", shm);
     attr = true;
   }
   const int64_t blocks = SAVE ? a.blocks_per_scene * a.n_scenes : (a.M + kX3Samples - 1) / kX3Samples;
   AVR_REQUIRE(blocks < (1ll << 31), "field: too many points");
-  field_x3_kernel<FT, NW, SAVE><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
+  field_x3_kernel<FT, NW, SAVE, VAR><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("field_x3_kernel");
 }
 
+static int x3_waves() {
+  static int w = -1;
+  if (w < 0) {
+    const char* e = getenv("AVR_X3_WAVES");
+    w = (e && atoi(e) == 4) ? 4 : 8;
+  }
+  return w;
+}
+
 int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s) {
+  // inference at d_hidden 512: 8 waves x 4 tiles, no GEMM-loop barriers, waves 0-3 at priority 1, block 0's
+  // stage rows issued ahead (VAR 26; +2.7-3.1 % over the 4-wave layout on the same box); AVR_X3_WAVES=4 selects
+  // the 4-wave layout, AVR_X3_VAR another 8-wave variant (diagnostics)
+  if (d_hidden == 512 && !a.act && x3_waves() == 8) {
+    const char* e = getenv("AVR_X3_VAR");
+    switch (e ? atoi(e) : 26) {
+      case 10: return launch_x3<4, 8, false, 10>(a, s);
+      case 2: return launch_x3<4, 8, false, 2>(a, s);
+      default: return launch_x3<4, 8, false, 26>(a, s);
+    }
+  }
   switch (d_hidden) {
     case 64: return a.act ? launch_x3<1, 4, true>(a, s) : launch_x3<1, 4, false>(a, s);
     case 128: return a.act ? launch_x3<2, 4, true>(a, s) : launch_x3<2, 4, false>(a, s);

@@ -143,6 +143,59 @@ __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT],
   }
 }
 
+// 8-wave variant of the K-chunk loop (256 registers per wave): sample groups
+// outermost, so only the current and the next B fragment pair are resident
+// (16 registers instead of 32); the next chunk's A fragment of tile sg loads
+// during sample group sg (FT == 4: one tile per group).
+template <int FT, bool ZERO>
+__device__ __forceinline__ void chunk_step_sg(floatx4 (&acc)[FT][4], const FragX3 (&A)[FT], FragX3 (&An)[FT],
+                                              const uint4* wn, BPair& B, const uint4* X16, int c, int cn, int g,
+                                              int j) {
+  static_assert(FT == 4, "one next-chunk tile per sample group");
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg) {
+    const BPair Bn = sg < 3 ? read_b(X16, c, sg + 1, g, j) : read_b(X16, cn, 0, g, j);
+    An[sg] = load_frag(wn + 2 * 64 * sg);
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      acc[ft][sg] = mfma32h(A[ft].hi, B.hi, ZERO ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[ft][sg]);
+      acc[ft][sg] = mfma32h(A[ft].hi, B.lo, acc[ft][sg]);
+      acc[ft][sg] = mfma32h(A[ft].lo, B.hi, acc[ft][sg]);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    B = Bn;
+  }
+}
+
+// SYNCP: s_barrier after every chunk pair (1), every second pair (2), never (0).
+template <int FT, bool ZERO, int SYNCP>
+__device__ __forceinline__ void gemm_x3_sg(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W,
+                                           int KC, int cstride, const uint4* X16, int lane) {
+  const int g = lane >> 4, j = lane & 15;
+  const uint4* wl = W + 2 * lane;
+  FragX3 A1[FT];
+#pragma unroll
+  for (int ft = kPrefetch; ft < FT; ++ft) A0[ft] = load_frag(wl + 2 * 64 * ft);
+  BPair B = read_b(X16, 0, 0, g, j);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int c = 0; c < KC; c += 2) {
+    const int c2 = c + 2 < KC ? c + 2 : c + 1;
+    const uint4* w1 = wl + (int64_t)2 * (c + 1) * cstride;
+    const uint4* w2 = wl + (int64_t)2 * c2 * cstride;
+    if (ZERO && c == 0)
+      chunk_step_sg<FT, true>(acc, A0, A1, w1, B, X16, c, c + 1, g, j);
+    else
+      chunk_step_sg<FT, false>(acc, A0, A1, w1, B, X16, c, c + 1, g, j);
+    chunk_step_sg<FT, false>(acc, A1, A0, w2, B, X16, c + 1, c2, g, j);
+    if (SYNCP == 1 || (SYNCP == 2 && (c & 2))) __builtin_amdgcn_s_barrier();
+  }
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not
 // for its outstanding global loads (the next layer's weight prefetch stays in
 // flight; __syncthreads would drain it).
@@ -196,6 +249,55 @@ __device__ __forceinline__ void store_split(uint4* X16, const floatx4 (&v)[FT][4
   }
 }
 
+// ---- Two-pass epilogue (8-wave workgroups, 256 registers per wave: no room
+// for a materialised copy v of the layer input). Pass 1 reduces the max of
+// relu(acc * f + b); pass 2 recomputes each value and writes its split.
+template <int FT, bool BIAS>
+__device__ __forceinline__ void load_bias(floatx4 (&bv)[FT], const float* __restrict__ bias, int wid, int g) {
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+    bv[ft] = BIAS ? *reinterpret_cast<const floatx4*>(bias + 16 * (FT * wid + ft) + 4 * g) : floatx4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <bool BIAS>
+__device__ __forceinline__ floatx4 relu_affine(const floatx4& a, float f, const floatx4& b) {
+  floatx4 x = BIAS ? a * f + b : a * f;
+  x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
+  return x;
+}
+
+template <int FT, bool BIAS>
+__device__ __forceinline__ float max_relu_affine(const floatx4 (&acc)[FT][4], float f, const floatx4 (&bv)[FT]) {
+  float mx = 0.f;
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      const floatx4 x = relu_affine<BIAS>(acc[ft][sg], f, bv[ft]);
+      mx = fmaxf(fmaxf(mx, x.x), fmaxf(fmaxf(x.y, x.z), x.w));
+    }
+  return wave_max(mx);
+}
+
+// X <- split(relu(acc * f + b) * s_x) for this wave's feature tiles
+template <int FT, bool BIAS>
+__device__ __forceinline__ void store_split_affine(uint4* X16, const floatx4 (&acc)[FT][4], float f,
+                                                   const floatx4 (&bv)[FT], float s_x, int wid, int g, int j) {
+  char* base = reinterpret_cast<char*>(X16);
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    const int ftg = FT * wid + ft;
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      uint2 hi, lo;
+      split4(relu_affine<BIAS>(acc[ft][sg], f, bv[ft]), s_x, hi, lo);
+      const int s = 16 * sg + j;
+      *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 0, g, s) * 16 + (ftg & 1) * 8) = hi;
+      *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 1, g, s) * 16 + (ftg & 1) * 8) = lo;
+    }
+  }
+}
+
 __device__ __forceinline__ float layer_scale(const float* packed, const Layout& L, int layer) {
   return pow2_scale_for(__uint_as_float(reinterpret_cast<const unsigned*>(packed + L.x3_hdr)[layer]));
 }
@@ -217,6 +319,19 @@ __device__ __forceinline__ float publish(uint4* X16, const floatx4 (&v)[FT][4], 
   lds_barrier();
   const float s_x = pow2_scale_for(red_max<NW>(red));
   store_split<FT>(X16, v, s_x, wid, g, j);
+  lds_barrier();
+  return s_x;
+}
+
+// Two-pass publish of relu(acc * f + b) (mx from max_relu_affine); returns s_x
+template <int FT, int NW, bool BIAS>
+__device__ __forceinline__ float publish_affine(uint4* X16, const floatx4 (&acc)[FT][4], float f,
+                                                const floatx4 (&bv)[FT], float mx, float* red, int wid, int lane,
+                                                int g, int j) {
+  if (lane == 0) red[wid] = mx;
+  lds_barrier();
+  const float s_x = pow2_scale_for(red_max<NW>(red));
+  store_split_affine<FT, BIAS>(X16, acc, f, bv, s_x, wid, g, j);
   lds_barrier();
   return s_x;
 }
