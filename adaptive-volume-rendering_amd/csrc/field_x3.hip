@@ -158,9 +158,13 @@ __device__ __forceinline__ void blend_stage(floatx4 (&h)[FT][4], floatx4 (&v)[FT
       h[ft][sg] = hn;
       if (PREP) {
         floatx4 x = hn * f;
-        x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
-        if (STOREV) v[ft][sg] = x;
-        mx = fmaxf(fmaxf(mx, x.x), fmaxf(fmaxf(x.y, x.z), x.w));
+        if (STOREV) {
+          x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
+          v[ft][sg] = x;
+        }
+        // mx starts at 0: max relu(x_i) = max(0, max x_i)
+        mx = fmaxf(mx, fmaxf(x.x, x.y));
+        mx = fmaxf(mx, fmaxf(x.z, x.w));
       }
       if (ft & 1) __builtin_amdgcn_sched_barrier(0);  // bound the LDS reads in flight (register pressure)
     }
@@ -252,7 +256,9 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   char* stage = reinterpret_cast<char*>(lds);
   ZTail* tail = reinterpret_cast<ZTail*>(reinterpret_cast<char*>(lds) + (P::BYTES - P::TAIL));
   float* red = tail->red;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wid through readfirstlane: the compiler then knows it is wave-uniform and keeps
+  // wid-derived addresses (weight fragments, bias rows) in SGPRs
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, j = lane & 15;
   const int gg = g + 4 * (wid >> 2);               // prologue: sub-lane of sample 16 (wid & 3) + j
   // SAVE: one training launch covers every scene of the batch (scene of this workgroup, its rows)
@@ -453,10 +459,11 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   // ---- lin_out(relu(h)): waves 0-3 compute the 16-row output tile for samples 16w + j.
   // (a quarter of lin_out's A fragments are loaded ahead of the publish, the rest after)
   FragX3 Ao[KC];
-  const uint4* wo = P16 + L.x3_out / 4 + 2 * lane;
+  const uint4* wo = P16 + L.x3_out / 4;
+  const unsigned wlo = 2 * lane;
   if (wid < 4) {
 #pragma unroll
-    for (int c = 0; c < KC / 4; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
+    for (int c = 0; c < KC / 4; ++c) Ao[c] = load_frag(wo + (wlo + 2 * 64 * c));
   }
   if constexpr (TWO) {
     mx = max_relu_affine<FT, false>(h, 1.0f / S_h, bz);
@@ -468,7 +475,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   }
   if (wid < 4) {
 #pragma unroll
-    for (int c = KC / 4; c < KC; ++c) Ao[c] = load_frag(wo + (int64_t)2 * 64 * c);
+    for (int c = KC / 4; c < KC; ++c) Ao[c] = load_frag(wo + (wlo + 2 * 64 * c));
   }
   AVR_STAMP(25);
   if (wid >= 4) return;

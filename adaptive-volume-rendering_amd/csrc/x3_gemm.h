@@ -110,7 +110,7 @@ constexpr int kPrefetch = 2;
 template <int FT>
 __device__ __forceinline__ void prefetch_a(FragX3 (&A0)[FT], const uint4* __restrict__ W, int lane) {
 #pragma unroll
-  for (int ft = 0; ft < (FT < kPrefetch ? FT : kPrefetch); ++ft) A0[ft] = load_frag(W + 2 * lane + 2 * 64 * ft);
+  for (int ft = 0; ft < (FT < kPrefetch ? FT : kPrefetch); ++ft) A0[ft] = load_frag(W + (unsigned)(2 * lane + 2 * 64 * ft));
 }
 
 // A0 holds chunk 0 (prefetch_a).
@@ -149,13 +149,13 @@ __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT],
 // during sample group sg (FT == 4: one tile per group).
 template <int FT, bool ZERO>
 __device__ __forceinline__ void chunk_step_sg(floatx4 (&acc)[FT][4], const FragX3 (&A)[FT], FragX3 (&An)[FT],
-                                              const uint4* wn, BPair& B, const uint4* X16, int c, int cn, int g,
-                                              int j) {
+                                              const uint4* __restrict__ wn, unsigned lo, BPair& B, const uint4* X16,
+                                              int c, int cn, int g, int j) {
   static_assert(FT == 4, "one next-chunk tile per sample group");
 #pragma unroll
   for (int sg = 0; sg < 4; ++sg) {
     const BPair Bn = sg < 3 ? read_b(X16, c, sg + 1, g, j) : read_b(X16, cn, 0, g, j);
-    An[sg] = load_frag(wn + 2 * 64 * sg);
+    An[sg] = load_frag(wn + (lo + 2 * 64 * sg));   // wave-uniform base + 32-bit lane offset
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft) {
       acc[ft][sg] = mfma32h(A[ft].hi, B.hi, ZERO ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[ft][sg]);
@@ -177,21 +177,21 @@ template <int FT, bool ZERO, int SYNCP>
 __device__ __forceinline__ void gemm_x3_sg(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W,
                                            int KC, int cstride, const uint4* X16, int lane) {
   const int g = lane >> 4, j = lane & 15;
-  const uint4* wl = W + 2 * lane;
+  const unsigned lo = 2 * lane;      // W (wave-uniform) + lo: this lane's fragment
   FragX3 A1[FT];
 #pragma unroll
-  for (int ft = kPrefetch; ft < FT; ++ft) A0[ft] = load_frag(wl + 2 * 64 * ft);
+  for (int ft = kPrefetch; ft < FT; ++ft) A0[ft] = load_frag(W + (lo + 2 * 64 * ft));
   BPair B = read_b(X16, 0, 0, g, j);
   __builtin_amdgcn_sched_barrier(0);
   for (int c = 0; c < KC; c += 2) {
     const int c2 = c + 2 < KC ? c + 2 : c + 1;
-    const uint4* w1 = wl + (int64_t)2 * (c + 1) * cstride;
-    const uint4* w2 = wl + (int64_t)2 * c2 * cstride;
+    const uint4* w1 = W + (int64_t)2 * (c + 1) * cstride;
+    const uint4* w2 = W + (int64_t)2 * c2 * cstride;
     if (ZERO && c == 0)
-      chunk_step_sg<FT, true>(acc, A0, A1, w1, B, X16, c, c + 1, g, j);
+      chunk_step_sg<FT, true>(acc, A0, A1, w1, lo, B, X16, c, c + 1, g, j);
     else
-      chunk_step_sg<FT, false>(acc, A0, A1, w1, B, X16, c, c + 1, g, j);
-    chunk_step_sg<FT, false>(acc, A1, A0, w2, B, X16, c + 1, c2, g, j);
+      chunk_step_sg<FT, false>(acc, A0, A1, w1, lo, B, X16, c, c + 1, g, j);
+    chunk_step_sg<FT, false>(acc, A1, A0, w2, lo, B, X16, c + 1, c2, g, j);
     if (SYNCP == 1 || (SYNCP == 2 && (c & 2))) __builtin_amdgcn_s_barrier();
   }
 }
@@ -266,6 +266,7 @@ __device__ __forceinline__ floatx4 relu_affine(const floatx4& a, float f, const 
   return x;
 }
 
+// max relu(x_i) = max(0, max x_i): no per-value relu (mx starts at 0)
 template <int FT, bool BIAS>
 __device__ __forceinline__ float max_relu_affine(const floatx4 (&acc)[FT][4], float f, const floatx4 (&bv)[FT]) {
   float mx = 0.f;
@@ -273,8 +274,9 @@ __device__ __forceinline__ float max_relu_affine(const floatx4 (&acc)[FT][4], fl
   for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) {
-      const floatx4 x = relu_affine<BIAS>(acc[ft][sg], f, bv[ft]);
-      mx = fmaxf(fmaxf(mx, x.x), fmaxf(fmaxf(x.y, x.z), x.w));
+      const floatx4 x = BIAS ? acc[ft][sg] * f + bv[ft] : acc[ft][sg] * f;
+      mx = fmaxf(mx, fmaxf(x.x, x.y));
+      mx = fmaxf(mx, fmaxf(x.z, x.w));
     }
   return wave_max(mx);
 }

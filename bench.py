@@ -368,7 +368,7 @@ def main():
     achieved_tflops = timer.samples * fps / (field_ms * 1e-3) / 1e12
     if args.precision == "x3":
         # each fp32-equivalent MAC is 3 fp16 MFMA MACs: the attainable fp32-equivalent peak is fp16 / 3
-        peak, kname = FP16_MFMA_PEAK_TFLOPS / 3.0, ("field_x3_kernel<8,4> (fused PE + lin_z interpolation + ResnetFC on "
+        peak, kname = FP16_MFMA_PEAK_TFLOPS / 3.0, ("field_x3_kernel<4,8> (8 waves; fused PE + lin_z interpolation + ResnetFC on "
                                                     "split-fp16 v_mfma_f32_16x16x32_f16 x3, fp32 accumulate)")
     else:
         peak, kname = FP32_MFMA_PEAK_TFLOPS, ("field_fwd_kernel<32> (fused PE + latent lookup + ResnetFC on "

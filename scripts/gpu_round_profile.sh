@@ -34,7 +34,7 @@ res = {k: sum(v) / len(v) for k, v in vals.items()}
 fetch = res.get("FETCH_SIZE")   # KB per dispatch
 write = res.get("WRITE_SIZE")
 hit, miss = res.get("TCC_HIT_sum"), res.get("TCC_MISS_sum")
-j = {"kernel": "field_x3_kernel<8,4>", "source": f"rocprofv3 --pmc over bench.py --steps 1 --warmup 1 ({out})",
+j = {"kernel": "field_x3_kernel<4,8> (8 waves)", "source": f"rocprofv3 --pmc over bench.py --steps 1 --warmup 1 ({out})",
      "dispatches_averaged": len(vals.get("FETCH_SIZE", [])),
      "fetch_size_kb_per_launch_raw": fetch, "write_size_kb_per_launch": write,
      "hbm_bytes_per_launch": None if fetch is None else int(2 * fetch * 1024 + (write or 0) * 1024),
