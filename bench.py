@@ -102,7 +102,8 @@ class HbmKernelTimer:
     kernel on torch's current stream), measured in isolation: the arguments of
     their first call inside the timed steps are kept and every launch is then
     replayed `reps` times back to back between two HIP events, so the average
-    is kernel time without host launch gaps. Bytes are ALGORITHMIC per launch
+    is kernel time without host launch gaps (one HIP graph of `reps` launches).
+    Bytes are ALGORITHMIC per launch
     (SURVEY §8d): compulsory reads + writes, fp32, Philox noise (no noise bytes)."""
 
     def __init__(self, ops):
@@ -139,18 +140,42 @@ class HbmKernelTimer:
         self._wrap("sample_fine", "sample_fine_kernel", sample_fine_bytes)
         self._wrap("depth_from_world_fwd", "depth_kernel", lambda a, k, out: (a[0].shape[0] * a[0].shape[1] * 32, ""))
 
-    def report(self, reps=20):
-        res = []
-        for label, (fn, a, k, nb) in self.calls.items():
-            fn(*a, **k)
-            s = torch.cuda.Event(enable_timing=True)
-            e = torch.cuda.Event(enable_timing=True)
+    @staticmethod
+    def _replay_us(fn, a, k, reps):
+        """Average launch duration: `reps` launches captured in one HIP graph
+        (no host launch gaps between them), or plain back-to-back launches if
+        capture is refused."""
+        fn(*a, **k)
+        torch.cuda.synchronize()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        try:
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    for _ in range(reps):
+                        fn(*a, **k)
+            torch.cuda.current_stream().wait_stream(side)
+            g.replay()
+            torch.cuda.synchronize()
+            s.record()
+            g.replay()
+            e.record()
+        except Exception:  # noqa: BLE001 -- capture refused: time plain launches
+            torch.cuda.synchronize()
             s.record()
             for _ in range(reps):
                 fn(*a, **k)
             e.record()
-            e.synchronize()
-            us = s.elapsed_time(e) * 1e3 / reps
+        e.synchronize()
+        return s.elapsed_time(e) * 1e3 / reps
+
+    def report(self, reps=20):
+        res = []
+        for label, (fn, a, k, nb) in self.calls.items():
+            us = self._replay_us(fn, a, k, reps)
             gbs = nb / (us * 1e-6) / 1e9
             res.append({"kernel": label, "avg_us": round(us, 2), "bytes_per_launch": int(nb),
                         "achieved_GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)})
