@@ -123,7 +123,7 @@ template <int FT, bool ZERO, bool TWO, int SYNCP>
 __device__ __forceinline__ void gemm(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W, int KC,
                                      int cstride, const uint4* X16, int lane) {
   if constexpr (TWO)
-    gemm_x3_sg<FT, ZERO, SYNCP>(acc, A0, W, KC, cstride, X16, lane);
+    gemm_x3_sg<FT, ZERO, SYNCP, FT>(acc, A0, W, KC, cstride, X16, lane);
   else
     gemm_x3<FT, ZERO, false>(acc, A0, W, KC, cstride, X16, lane);
 }
@@ -243,6 +243,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   constexpr int PES = (6 * 7 + NW - 1) / NW;       // PE slots per lane (6 * num_freqs <= 42)
   // 8 waves (256 registers each): two-pass epilogues instead of a materialised layer input v
   constexpr bool TWO = NW > 4;
+  constexpr int NPF = TWO ? FT : kPrefetch;   // chunk-0 weight tiles loaded ahead of each layer's publish
   static_assert(!(SAVE && TWO), "the training forward keeps the 4-wave layout");
   const floatx4 bz[FT] = {};
   if constexpr ((VAR & 4) != 0) {
@@ -334,7 +335,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   }
   FragX3 A0[FT];   // chunk 0 of the next GEMM's weights, prefetched before the publish ahead of it
   const uint4* Win = P16 + L.x3_in / 4 + 2 * 64 * FT * wid;
-  prefetch_a<FT>(A0, Win, lane);
+  prefetch_a<FT, NPF>(A0, Win, lane);
   AVR_STAMP(1);
   float s_x;
   {
@@ -412,35 +413,48 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     AVR_STAMP(5 + 5 * (b & 3));
     if (SAVE) save_layer<FT, NW>(a, 2 * b, v, mx, base, roff, wid, g, j, lane);
     const uint4* W0 = P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
-    prefetch_a<FT>(A0, W0, lane);
-    if constexpr (TWO)
-      s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
-    else
-      s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
-    AVR_STAMP(6 + 5 * (b & 3));
-    // fc_0 (from zero)
-    const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
-    gemm<FT, true, TWO, SYNCP>(t, A0, W0, KC, 64 * NTT, X16, lane);
-    AVR_STAMP(7 + 5 * (b & 3));
-    // fc_1 input relu(t + b0)
     const uint4* W1 = P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
+    prefetch_a<FT, NPF>(A0, W0, lane);
     if constexpr (TWO) {
+      // the fc_1 bias loads are issued before the t publish, whose barriers cover their latency
+      s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
+      AVR_STAMP(6 + 5 * (b & 3));
+      const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
+      gemm<FT, true, TWO, SYNCP>(t, A0, W0, KC, 64 * NTT, X16, lane);
+      AVR_STAMP(7 + 5 * (b & 3));
       floatx4 bv[FT];
       load_bias<FT, true>(bv, a.packed + L.b_fc0[b], wid, g);
       mx = max_relu_affine<FT, true>(t, 1.0f / S_t, bv);
-      prefetch_a<FT>(A0, W1, lane);
+      floatx4 bb[FT];
+      load_bias<FT, true>(bb, a.packed + L.b_fc1[b], wid, g);
+      prefetch_a<FT, NPF>(A0, W1, lane);
       s_x = publish_affine<FT, NW, true>(X16, t, 1.0f / S_t, bv, mx, red, wid, lane, g, j);
+      AVR_STAMP(8 + 5 * (b & 3));
+      // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
+      const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
+      const float r = S1 / S_h;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb[ft] * S1;
+      S_h = S1;
+      gemm<FT, false, TWO, SYNCP>(h, A0, W1, KC, 64 * NTT, X16, lane);
     } else {
+      s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+      AVR_STAMP(6 + 5 * (b & 3));
+      // fc_0 (from zero)
+      const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
+      gemm<FT, true, TWO, SYNCP>(t, A0, W0, KC, 64 * NTT, X16, lane);
+      AVR_STAMP(7 + 5 * (b & 3));
+      // fc_1 input relu(t + b0)
       mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
       if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, mx, base, roff, wid, g, j, lane);
-      prefetch_a<FT>(A0, W1, lane);
+      prefetch_a<FT, NPF>(A0, W1, lane);
       s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
-    }
-    AVR_STAMP(8 + 5 * (b & 3));
-    // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
-    const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
-    const float r = S1 / S_h;
-    {
+      AVR_STAMP(8 + 5 * (b & 3));
+      // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
+      const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
+      const float r = S1 / S_h;
       floatx4 bb[FT];   // all bias loads first (one wait, not one per tile)
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft)
@@ -450,9 +464,9 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
         for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb[ft];
+      S_h = S1;
+      gemm<FT, false, TWO, SYNCP>(h, A0, W1, KC, 64 * NTT, X16, lane);
     }
-    S_h = S1;
-    gemm<FT, false, TWO, SYNCP>(h, A0, W1, KC, 64 * NTT, X16, lane);
     AVR_STAMP(9 + 5 * (b & 3));
   }
 

@@ -105,12 +105,13 @@ __device__ __forceinline__ void chunk_step(floatx4 (&acc)[FT][4], const FragX3 (
 // Only the first kPrefetch tiles (the first group of chunk 0) are prefetched:
 // more would push the epilogue into spills, and a scratch store waits for
 // every outstanding load.
+// (The 8-wave layout, 4 tiles per wave, prefetches all of them: NPF = FT.)
 constexpr int kPrefetch = 2;
 
-template <int FT>
+template <int FT, int NPF = kPrefetch>
 __device__ __forceinline__ void prefetch_a(FragX3 (&A0)[FT], const uint4* __restrict__ W, int lane) {
 #pragma unroll
-  for (int ft = 0; ft < (FT < kPrefetch ? FT : kPrefetch); ++ft) A0[ft] = load_frag(W + (unsigned)(2 * lane + 2 * 64 * ft));
+  for (int ft = 0; ft < (FT < NPF ? FT : NPF); ++ft) A0[ft] = load_frag(W + (unsigned)(2 * lane + 2 * 64 * ft));
 }
 
 // A0 holds chunk 0 (prefetch_a).
@@ -173,14 +174,15 @@ __device__ __forceinline__ void chunk_step_sg(floatx4 (&acc)[FT][4], const FragX
 }
 
 // SYNCP: s_barrier after every chunk pair (1), every second pair (2), never (0).
-template <int FT, bool ZERO, int SYNCP>
+// A0 holds chunk 0's first NPF tiles (prefetch_a<FT, NPF>).
+template <int FT, bool ZERO, int SYNCP, int NPF = FT>
 __device__ __forceinline__ void gemm_x3_sg(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W,
                                            int KC, int cstride, const uint4* X16, int lane) {
   const int g = lane >> 4, j = lane & 15;
   const unsigned lo = 2 * lane;      // W (wave-uniform) + lo: this lane's fragment
   FragX3 A1[FT];
 #pragma unroll
-  for (int ft = kPrefetch; ft < FT; ++ft) A0[ft] = load_frag(W + (lo + 2 * 64 * ft));
+  for (int ft = NPF; ft < FT; ++ft) A0[ft] = load_frag(W + (lo + 2 * 64 * ft));
   BPair B = read_b(X16, 0, 0, g, j);
   __builtin_amdgcn_sched_barrier(0);
   for (int c = 0; c < KC; c += 2) {
