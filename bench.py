@@ -13,7 +13,9 @@ compositing, depth -- plus, on N > 1 GPUs, the RCCL gather of every rank's
 (rgb_coarse, rgb_fine, depth) to rank 0. The per-scene preparation (weight
 repack and lin_z latent table) is redone inside every step, not cached.
 
-python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 via torch.distributed.run.
+python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3|4|5]; N > 1 via torch.distributed.run.
+--config 5 (BASELINE configs[4]): a fixed 4 x 800 x 800 rays per step for the whole job, dealt to the ranks in
+64-ray tiles by avr.parallel.render_sharded and gathered with one all_gather ("scaling": "strong").
 Prints one JSON line on rank 0.
 """
 import argparse
@@ -296,8 +298,10 @@ def main():
     ap.add_argument("--precision", choices=["x3", "fp32"], default="x3",
                     help="field MFMA path: split-fp16 (3 products, fp32 accumulate) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", type=int, choices=[3, 4], default=3,
-                    help="BASELINE config: 3 = 65536 random rays (default); 4 = one 800x800 frame per step "
+    ap.add_argument("--config", type=int, choices=[3, 4, 5], default=3,
+                    help="BASELINE config: 3 = 65536 random rays (default); 5 = 4 orbit views of 800x800 per step "
+                         "sharded over the ranks in 64-ray tiles (strong scaling, avr.parallel.render_sharded); "
+                         "4 = one 800x800 frame per step "
                          "with fine-pass early termination at T_stop 1e-5")
     ap.add_argument("--sigma-bias", type=float, default=0.0,
                     help="density bias of the synthetic field (config 4: opacity of the scene)")
@@ -338,19 +342,38 @@ def main():
         x_pix = get_opencv_pixel_coordinates(800, 800).reshape(1, -1, 2).to(device)
         R = x_pix.shape[1]
         rend.t_stop = 1e-5
+    elif args.config == 5:
+        # BASELINE config 5: 4 views x 800x800 per step for the whole job; every rank renders its 64-ray tiles
+        # of all 4 views and one all_gather assembles the frames (avr.parallel.render_sharded)
+        # (one scene: the 4 views are one ray batch of 4 x 640 000 rays with a per-ray pose)
+        from avr.video import get_opencv_pixel_coordinates
+        n_views = 4
+        x_pix = get_opencv_pixel_coordinates(800, 800).reshape(1, -1, 2).repeat(1, n_views, 1).to(device)
+        R = x_pix.shape[1]
     else:
         R = args.rays
         g = torch.Generator(device="cpu").manual_seed(100 + rank)
         x_pix = torch.rand(1, R, 2, generator=g).to(device)
-    c2w = orbit_c2w(0.7 + 0.5 * rank).to(device).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
     K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]], device=device)
     gathered = None
-    if world > 1:
-        gathered = torch.empty(world * R * 7, device=device)
+    if args.config == 5:
+        from avr.parallel import render_sharded
+        c2w = torch.stack([orbit_c2w(2 * np.pi * v / n_views) for v in range(n_views)]).to(device)
+        c2w = c2w.repeat_interleave(R // n_views, 0).reshape(1, R, 4, 4)
+    else:
+        c2w = orbit_c2w(0.7 + 0.5 * rank).to(device).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
+        if world > 1:
+            gathered = torch.empty(world * R * 7, device=device)
 
     def step():
         fused._packed.clear()       # per-scene prep inside the step: repack weights, rebuild lin_z tables
         with torch.no_grad():
+            if args.config == 5:
+                if world > 1:
+                    rgb_c, rgb_f, depth, _ = render_sharded(lambda c, k, x: rend(c, k, x, net), c2w, K, x_pix)
+                else:
+                    rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
+                return rgb_f
             rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
             if world > 1:
                 import torch.distributed as dist
@@ -385,7 +408,8 @@ def main():
         elapsed, field_ms = float(t[0]), float(t[1])
     assert bool(torch.isfinite(out).all())
 
-    rays_total = R * world * args.steps
+    # whole-job rays: config 5 renders a fixed 4 x 800 x 800 per step over all ranks (strong scaling)
+    rays_total = (R if args.config == 5 else R * world) * args.steps
     value = rays_total / elapsed
     samples_per_ray = args.n_coarse + args.n_coarse + args.n_fine
     fps = field_flops_per_sample()
@@ -407,18 +431,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config == 5 else "weak",
         "vs_baseline": None,
         "dtype": "fp32" if args.precision == "fp32" else "fp32 (field products as 3 fp16 MFMA terms)",
-        "data": "synthetic rays (x_pix ~ U[0,1)^2, orbit pose), random-init default.conf field, random 512x64x64 "
-                "latent",
+        "data": ("synthetic rays (x_pix ~ U[0,1)^2, orbit pose)" if args.config == 3 else
+                 "synthetic rays (get_opencv_pixel_coordinates 800x800 grid, orbit poses)")
+                + ", random-init default.conf field, random 512x64x64 latent",
         "config": {"workload": (f"BASELINE config 3: {R} rays/GPU x ({args.n_coarse} coarse + {args.n_fine} fine, "
                                 "n_fine_depth 0), conf/default.conf PixelNeRF field (3x512 ResnetFC, d_latent 512)")
                    if args.config == 3 else
                    (f"BASELINE config 4: 800x800 frame ({R} rays)/GPU x ({args.n_coarse} coarse + {args.n_fine} "
                     f"fine), fine-pass early termination T_stop 1e-5, sigma bias {args.sigma_bias}, "
-                    "conf/default.conf PixelNeRF field"),
-                   "rays_per_gpu": R, "n_coarse": args.n_coarse, "n_fine": args.n_fine,
+                    "conf/default.conf PixelNeRF field") if args.config == 4 else
+                   (f"BASELINE config 5: 4 orbit views x 800x800 ({R} rays) per step over {world} GPU(s) in "
+                    f"64-ray tiles x ({args.n_coarse} coarse + {args.n_fine} fine), conf/default.conf PixelNeRF field"),
+                   "rays_per_gpu": R if args.config != 5 else -(-R // world), "n_coarse": args.n_coarse, "n_fine": args.n_fine,
                    "field_samples_per_ray": samples_per_ray, "parallelism": f"ray-shard x{world} + RCCL gather"},
         "roofline": {
             "kernel": kname,
