@@ -119,11 +119,11 @@ __device__ __forceinline__ void stage_rows(char* stage, const float* __restrict_
 
 typedef __attribute__((address_space(3))) char lds_char;
 
-template <int FT, bool ZERO, bool TWO, int SYNCP>
+template <int FT, bool ZERO, bool TWO>
 __device__ __forceinline__ void gemm(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W, int KC,
                                      int cstride, const uint4* X16, int lane) {
   if constexpr (TWO)
-    gemm_x3_sg<FT, ZERO, SYNCP, FT>(acc, A0, W, KC, cstride, X16, lane);
+    gemm_x3_sg<FT, ZERO, FT>(acc, A0, W, KC, cstride, X16, lane);
   else
     gemm_x3<FT, ZERO, false>(acc, A0, W, KC, cstride, X16, lane);
 }
@@ -227,15 +227,8 @@ __device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const 
 // VALU issue rate of the epilogues and hides one wave's stalls behind the
 // other); wave w owns the FT 16-row feature tiles FT*w .. FT*w + FT-1.
 // SAVE (training forward): also write every GEMM input and its relu mask.
-// VAR (8-wave layout experiments): bits 0-1 GEMM sync period (see gemm_x3_sg:
-// 0 -> every chunk pair, 1 -> every second pair, 2 -> none); bit 2: waves 4-7 at
-// s_setprio 1; bit 3: waves 0-3 at s_setprio 1; bit 4: block 0's lin_z stage rows
-// past lin_in's X issued before the lin_in GEMM. (Issuing the next block's first
-// stage rows in the middle of fc_1 measured 1.4 % slower: every later weight
-// load then waits for the LDS-DMA in the in-order vmcnt.)
-template <int FT, int NW, bool SAVE, int VAR = 0>
+template <int FT, int NW, bool SAVE>
 __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
-  constexpr int SYNCP = (VAR & 3) == 0 ? 1 : ((VAR & 3) == 1 ? 2 : 0);
   constexpr int HID = 16 * FT * NW;
   using P = LdsPlan<HID>;
   constexpr int KC = P::KC;
@@ -246,10 +239,10 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   constexpr int NPF = TWO ? FT : kPrefetch;   // chunk-0 weight tiles loaded ahead of each layer's publish
   static_assert(!(SAVE && TWO), "the training forward keeps the 4-wave layout");
   const floatx4 bz[FT] = {};
-  if constexpr ((VAR & 4) != 0) {
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-  }
-  if constexpr ((VAR & 8) != 0) {
+  // 8 waves: waves 0-3 at priority 1 leave each GEMM first, so their epilogue VALU overlaps the last MFMAs of
+  // waves 4-7 on the same SIMDs (measured against no priority, priority for waves 4-7, and a barrier every one
+  // or two K-chunk pairs inside the GEMM: this was the fastest)
+  if constexpr (TWO) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 256) __builtin_amdgcn_s_setprio(1);
   }
   extern __shared__ float lds[];
@@ -374,13 +367,14 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   // 8 waves: stage rows of the next lin_z table that are already in flight
   // ([p0, p1), issued while the preceding GEMM still read other parts of X)
   int p0 = 0, p1 = 0;
-  constexpr bool PRE0 = TWO && (VAR & 16);
+  // 8 waves: block 0's lin_z stage rows that do not overlap lin_in's X are DMA'd before the lin_in GEMM
+  constexpr bool PRE0 = TWO;
   if (PRE0 && a.n_lin_z > 0 && D <= P::CAP && D > P::IN_ROWS0) {
     stage_rows<HID, NW>(stage, a.table, tail, P::IN_ROWS0, D - P::IN_ROWS0, P::RS, lane, wid, P::IN_ROWS0);
     p0 = P::IN_ROWS0;
     p1 = D;
   }
-  gemm<FT, false, TWO, SYNCP>(h, A0, Win, kX3InChunks, 64 * NTT, X16, lane);
+  gemm<FT, false, TWO>(h, A0, Win, kX3InChunks, 64 * NTT, X16, lane);
   AVR_STAMP(4);
 
   for (int b = 0; b < a.n_blocks; ++b) {
@@ -420,7 +414,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
       AVR_STAMP(6 + 5 * (b & 3));
       const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
-      gemm<FT, true, TWO, SYNCP>(t, A0, W0, KC, 64 * NTT, X16, lane);
+      gemm<FT, true, TWO>(t, A0, W0, KC, 64 * NTT, X16, lane);
       AVR_STAMP(7 + 5 * (b & 3));
       floatx4 bv[FT];
       load_bias<FT, true>(bv, a.packed + L.b_fc0[b], wid, g);
@@ -438,13 +432,13 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
 #pragma unroll
         for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb[ft] * S1;
       S_h = S1;
-      gemm<FT, false, TWO, SYNCP>(h, A0, W1, KC, 64 * NTT, X16, lane);
+      gemm<FT, false, TWO>(h, A0, W1, KC, 64 * NTT, X16, lane);
     } else {
       s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
       AVR_STAMP(6 + 5 * (b & 3));
       // fc_0 (from zero)
       const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
-      gemm<FT, true, TWO, SYNCP>(t, A0, W0, KC, 64 * NTT, X16, lane);
+      gemm<FT, true, TWO>(t, A0, W0, KC, 64 * NTT, X16, lane);
       AVR_STAMP(7 + 5 * (b & 3));
       // fc_1 input relu(t + b0)
       mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
@@ -465,7 +459,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
 #pragma unroll
         for (int sg = 0; sg < 4; ++sg) h[ft][sg] = h[ft][sg] * r + bb[ft];
       S_h = S1;
-      gemm<FT, false, TWO, SYNCP>(h, A0, W1, KC, 64 * NTT, X16, lane);
+      gemm<FT, false, TWO>(h, A0, W1, KC, 64 * NTT, X16, lane);
     }
     AVR_STAMP(9 + 5 * (b & 3));
   }
@@ -513,19 +507,19 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     a.out[roff + m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
 }
 
-template <int FT, int NW, bool SAVE, int VAR = 0>
+template <int FT, int NW, bool SAVE>
 static int launch_x3(const FieldArgs& a, hipStream_t s) {
   const size_t shm = LdsPlan<16 * FT * NW>::BYTES;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT, NW, SAVE, VAR>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT, NW, SAVE>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
       return fail(AVR_E_HIP, "field_x3_kernel: cannot set dynamic LDS to %zu", shm);
     attr = true;
   }
   const int64_t blocks = SAVE ? a.blocks_per_scene * a.n_scenes : (a.M + kX3Samples - 1) / kX3Samples;
   AVR_REQUIRE(blocks < (1ll << 31), "field: too many points");
-  field_x3_kernel<FT, NW, SAVE, VAR><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
+  field_x3_kernel<FT, NW, SAVE><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("field_x3_kernel");
 }
 
@@ -539,17 +533,9 @@ static int x3_waves() {
 }
 
 int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s) {
-  // inference at d_hidden 512: 8 waves x 4 tiles, no GEMM-loop barriers, waves 0-3 at priority 1, block 0's
-  // stage rows issued ahead (VAR 26; +2.7-3.1 % over the 4-wave layout on the same box); AVR_X3_WAVES=4 selects
-  // the 4-wave layout, AVR_X3_VAR another 8-wave variant (diagnostics)
-  if (d_hidden == 512 && !a.act && x3_waves() == 8) {
-    const char* e = getenv("AVR_X3_VAR");
-    switch (e ? atoi(e) : 26) {
-      case 10: return launch_x3<4, 8, false, 10>(a, s);
-      case 2: return launch_x3<4, 8, false, 2>(a, s);
-      default: return launch_x3<4, 8, false, 26>(a, s);
-    }
-  }
+  // inference at d_hidden 512: 8 waves x 4 tiles (+2.7-4.7 % over the 4-wave layout on the same box);
+  // AVR_X3_WAVES=4 selects the 4-wave layout (diagnostics)
+  if (d_hidden == 512 && !a.act && x3_waves() == 8) return launch_x3<4, 8, false>(a, s);
   switch (d_hidden) {
     case 64: return a.act ? launch_x3<1, 4, true>(a, s) : launch_x3<1, 4, false>(a, s);
     case 128: return a.act ? launch_x3<2, 4, true>(a, s) : launch_x3<2, 4, false>(a, s);

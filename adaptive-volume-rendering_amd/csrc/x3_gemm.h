@@ -173,9 +173,9 @@ __device__ __forceinline__ void chunk_step_sg(floatx4 (&acc)[FT][4], const FragX
   }
 }
 
-// SYNCP: s_barrier after every chunk pair (1), every second pair (2), never (0).
-// A0 holds chunk 0's first NPF tiles (prefetch_a<FT, NPF>).
-template <int FT, bool ZERO, int SYNCP, int NPF = FT>
+// A0 holds chunk 0's first NPF tiles (prefetch_a<FT, NPF>). No barrier in the
+// loop: the two waves of a SIMD drift apart by priority (field_x3_kernel).
+template <int FT, bool ZERO, int NPF = FT>
 __device__ __forceinline__ void gemm_x3_sg(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W,
                                            int KC, int cstride, const uint4* X16, int lane) {
   const int g = lane >> 4, j = lane & 15;
@@ -194,7 +194,6 @@ __device__ __forceinline__ void gemm_x3_sg(floatx4 (&acc)[FT][4], FragX3 (&A0)[F
     else
       chunk_step_sg<FT, false>(acc, A0, A1, w1, lo, B, X16, c, c + 1, g, j);
     chunk_step_sg<FT, false>(acc, A1, A0, w2, lo, B, X16, c + 1, c2, g, j);
-    if (SYNCP == 1 || (SYNCP == 2 && (c & 2))) __builtin_amdgcn_s_barrier();
   }
 }
 
