@@ -17,7 +17,7 @@ rc=$?; tail -1 $OUT/bench.log; [ $rc -eq 0 ] || { echo "bench rc=$rc"; exit $rc;
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o bench -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1
 rc=$?; [ $rc -eq 0 ] || { echo "rocprof rc=$rc"; tail -5 $OUT/prof.log; exit $rc; }
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -f csv -d $OUT/pmc$i -o pmc -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/pmc$i.log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "pmc pass $i rc=$rc"; tail -5 $OUT/pmc$i.log; exit $rc; }
@@ -43,3 +43,5 @@ j = {"kernel": "field_x3_kernel<4,8> (8 waves)", "source": f"rocprofv3 --pmc ove
 json.dump(j, open(f"{out}/field_pmc.json", "w"), indent=1)
 print(json.dumps(j))
 PY
+# per-kernel summary of every pass: HBM GB/s from FETCH/WRITE, MFMA busy, L2 hit rate
+python scripts/pmc_summary.py $OUT/pmc_kernels.json $OUT/pmc1 $OUT/pmc2 $OUT/pmc3 $OUT/pmc4
