@@ -25,15 +25,34 @@ __device__ __forceinline__ float coarse_z(float near_, float span, int s, int n,
   return fadd(fadd(near_, fmul(span, step)), fdiv(fmul(u, span), (float)n));
 }
 
+// near + span * (s / n) depends on s only: each workgroup tabulates it once in
+// LDS (kCoarseTab entries; larger n computes it per sample), so a sample costs
+// one IEEE division. 32-bit index arithmetic when the sample count allows.
+constexpr int kCoarseTab = 1024;
+
 __global__ void __launch_bounds__(256) sample_coarse_kernel(float near_, float far_, int64_t n_rays, int n,
                                                             const float* __restrict__ noise, uint64_t seed,
                                                             uint64_t offset, float* __restrict__ z) {
+  __shared__ float base_tab[kCoarseTab];
   const int nq = (n + 3) >> 2;                           // 4-sample blocks per ray
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_rays * nq) return;
-  const int64_t r = i / nq;
-  const int q = (int)(i - r * nq);
   const float span = fsub(far_, near_);
+  const bool tab = n <= kCoarseTab;
+  if (tab)
+    for (int s = threadIdx.x; s < n; s += blockDim.x) base_tab[s] = fadd(near_, fmul(span, fdiv((float)s, (float)n)));
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = n_rays * nq;
+  if (i >= total) return;
+  int64_t r;
+  int q;
+  if (total < (1ll << 32)) {
+    const unsigned ui = (unsigned)i, ur = ui / (unsigned)nq;
+    r = ur;
+    q = (int)(ui - ur * (unsigned)nq);
+  } else {
+    r = i / nq;
+    q = (int)(i - r * nq);
+  }
   float u[4];
   if (noise) {
 #pragma unroll
@@ -44,7 +63,10 @@ __global__ void __launch_bounds__(256) sample_coarse_kernel(float near_, float f
   }
   float o[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) o[k] = coarse_z(near_, span, 4 * q + k, n, u[k]);
+  for (int k = 0; k < 4; ++k) {
+    const int s = 4 * q + k;
+    o[k] = tab ? fadd(base_tab[s < n ? s : 0], fdiv(fmul(u[k], span), (float)n)) : coarse_z(near_, span, s, n, u[k]);
+  }
   float* zr = z + r * n + 4 * q;
   if ((n & 3) == 0) {
     *reinterpret_cast<float4*>(zr) = make_float4(o[0], o[1], o[2], o[3]);
