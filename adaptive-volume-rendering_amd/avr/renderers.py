@@ -11,7 +11,8 @@ path, and every stage raises if libavr_hip.so is missing.
 
 Two evaluation modes for the radiance field:
   * fused  — `radiance_field` is an eligible NewPixelNeRFNet and no gradient
-    is needed: sigma/RGB come from the fp32-MFMA field kernel straight from
+    is needed: sigma/RGB come from the split-fp16 ("x3", fp32-equivalent)
+    MFMA field kernel straight from
     (ro, rd, z), with no points / viewdirs / mlp_input tensors materialised;
   * module — anything else (any nn.Module honouring rf(xyz, viewdirs=, coarse=)),
     or training: the module is called on the sample points, and compositing

@@ -110,7 +110,9 @@ __global__ void absmax_kernel(const float* __restrict__ W, int64_t n, unsigned* 
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
-// x3 fragments: dst[((c*FTt + ft)*64 + l)*16 + {e, 8+e}] = (hi, lo) of
+// x3 fragments: dst[((c*FTt + ft)*2 + {0, 1})*512 + 8l + e] = (hi, lo) of
+// (a tile's 64 hi lanes, then its 64 lo lanes: each 16-B-per-lane load of one
+// half reads 1 KiB contiguous, whole 128-B lines)
 // W[16ft + (l&15)][32c + (e<4 ? 4g+e : 16+4g+e-4)] * s_w, g = l>>4, with
 // s_w = 2^(14 - ceil-exponent of max|W|) from the layer's header word.
 // (rs, cs) = element strides of W's rows / columns: (in_dim, 1) for W, (1, ld) for W^T.
@@ -130,9 +132,9 @@ __global__ void pack_x3_kernel(const float* __restrict__ W, int out_dim, int in_
   const float v = (row < out_dim && col < in_dim) ? W[(int64_t)row * rs + (int64_t)col * cs] * sw : 0.f;
   const _Float16 hi = (_Float16)v;
   const _Float16 lo = (_Float16)(v - (float)hi);
-  const int64_t base = (((int64_t)c * FTt + ft) * 64 + l) * 16;
+  const int64_t base = ((int64_t)c * FTt + ft) * 2 * 64 * 8 + l * 8;
   dst[base + e] = hi;
-  dst[base + 8 + e] = lo;
+  dst[base + 64 * 8 + e] = lo;
 }
 
 // ----------------------------------------------------------------- fp32 MFMA tiles

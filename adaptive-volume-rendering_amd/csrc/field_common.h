@@ -20,7 +20,7 @@ constexpr int kX3MaxLayers = 2 + 2 * AVR_MAX_BLOCKS;
 
 // Packed blob (floats). fp32 part: [t][ot][lane] float4 fragments for
 // v_mfma_f32_16x16x4_f32 (also used by the latent-table kernel for lin_z).
-// x3 part: [c][ft][lane][16 x fp16] = (hi[8], lo[8]) fragments for
+// x3 part: [c][ft][hi | lo][lane][8 x fp16] fragments for
 // v_mfma_f32_16x16x32_f16, scaled by 2^e per layer (header holds max|W| bits).
 struct Layout {
   int NT;                 // d_hidden / 16

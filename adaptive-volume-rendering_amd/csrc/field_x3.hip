@@ -468,7 +468,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   // (a quarter of lin_out's A fragments are loaded ahead of the publish, the rest after)
   FragX3 Ao[KC];
   const uint4* wo = P16 + L.x3_out / 4;
-  const unsigned wlo = 2 * lane;
+  const unsigned wlo = lane;
   if (wid < 4) {
 #pragma unroll
     for (int c = 0; c < KC / 4; ++c) Ao[c] = load_frag(wo + (wlo + 2 * 64 * c));

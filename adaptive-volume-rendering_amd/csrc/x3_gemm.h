@@ -16,9 +16,11 @@ struct FragX3 {
   half8 hi, lo;
 };
 
+// p = tile base + lane (uint4 units); the tile holds its 64 lanes' hi halves,
+// then their lo halves (pack_x3_kernel), so each half loads 1 KiB contiguous.
 __device__ __forceinline__ FragX3 load_frag(const uint4* p) {
   FragX3 f;
-  const uint4 a = p[0], b = p[1];
+  const uint4 a = p[0], b = p[64];
   f.hi = __builtin_bit_cast(half8, a);
   f.lo = __builtin_bit_cast(half8, b);
   return f;
@@ -111,7 +113,7 @@ constexpr int kPrefetch = 2;
 template <int FT, int NPF = kPrefetch>
 __device__ __forceinline__ void prefetch_a(FragX3 (&A0)[FT], const uint4* __restrict__ W, int lane) {
 #pragma unroll
-  for (int ft = 0; ft < (FT < NPF ? FT : NPF); ++ft) A0[ft] = load_frag(W + (unsigned)(2 * lane + 2 * 64 * ft));
+  for (int ft = 0; ft < (FT < NPF ? FT : NPF); ++ft) A0[ft] = load_frag(W + (unsigned)(lane + 2 * 64 * ft));
 }
 
 // A0 holds chunk 0 (prefetch_a).
@@ -119,7 +121,7 @@ template <int FT, bool ZERO, bool SYNC>
 __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W, int KC,
                                         int cstride, const uint4* X16, int lane) {
   const int g = lane >> 4, j = lane & 15;
-  const uint4* wl = W + 2 * lane;
+  const uint4* wl = W + lane;
   FragX3 A1[FT];
   BPair B[4];
 #pragma unroll
@@ -179,7 +181,7 @@ template <int FT, bool ZERO, int NPF = FT>
 __device__ __forceinline__ void gemm_x3_sg(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W,
                                            int KC, int cstride, const uint4* X16, int lane) {
   const int g = lane >> 4, j = lane & 15;
-  const unsigned lo = 2 * lane;      // W (wave-uniform) + lo: this lane's fragment
+  const unsigned lo = lane;          // W (wave-uniform) + lo: this lane's fragment
   FragX3 A1[FT];
 #pragma unroll
   for (int ft = NPF; ft < FT; ++ft) A0[ft] = load_frag(W + (lo + 2 * 64 * ft));

@@ -226,7 +226,7 @@ def run_train(args, device):
     samples) and field, MSE on rgb coarse + fine, backward, Adam (lr 1e-4).
     The latent maps are fixed inputs (the ResNet34 encoder is out of scope).
     Timed twice: autograd through the HIP field (x3 training forward + HIP
-    backward chain + hipBLASLt weight-gradient GEMMs) and PyTorch autograd of
+    backward chain + the x3 weight-gradient kernel) and PyTorch autograd of
     the same module (forward_torch; the rest of the step is identical)."""
     from avr.conf import default_conf
     from avr.renderers import VolumeRenderer
