@@ -71,36 +71,52 @@ def depth_from_world(ro, rd, dist, c2w_info):
     return depth_from_world_fwd(ro, rd, dist, c2w_info)[0]
 
 
-def sample_coarse(near, far, n_rays, n_samples, device, noise=None, seed=0, offset=0):
+def _ray_ids(ray_ids, n_rays):
+    if ray_ids is None:
+        return None
+    ray_ids = ray_ids.reshape(-1).to(torch.int64).contiguous()
+    if ray_ids.numel() != n_rays:
+        raise _lib.AVRError(f"ray_ids has {ray_ids.numel()} entries for {n_rays} rays")
+    require_device(ray_ids)
+    return ray_ids
+
+
+def sample_coarse(near, far, n_rays, n_samples, device, noise=None, seed=0, offset=0, ray_ids=None):
     """sample_coarse (renderers.py:4-24) -> z (n_rays, n_samples). `noise` is the
-    rand_like draw (n_rays, n_samples) or None for in-kernel Philox."""
+    rand_like draw (n_rays, n_samples) or None for in-kernel Philox keyed on
+    offset + ray (or offset + ray_ids[ray]: global ray ids of a sharded frame)."""
     z = torch.empty(n_rays, n_samples, device=device, dtype=F32)
     if noise is not None:
         noise = _f32c(noise.reshape(n_rays, n_samples))
         require_device(noise)
-    call("avr_sample_coarse", float(near), float(far), n_rays, n_samples, ptr(noise), seed, offset, ptr(z),
-         stream_of(z))
+    ray_ids = _ray_ids(ray_ids, n_rays)
+    call("avr_sample_coarse", float(near), float(far), n_rays, n_samples, ptr(noise), seed, offset, ptr(ray_ids),
+         ptr(z), stream_of(z))
     return z
 
 
 def sample_fine(weights, z_coarse, near, far, n_importance, n_depth, depth_std, u=None, u2=None, noise_depth=None,
-                seed=0, offset=0, want_idx=False, want_fine=False):
+                seed=0, offset=0, want_idx=False, want_fine=False, ray_ids=None):
     """sample_fine + sample_depth + clamp + sort (renderers.py:27-66, :252-258).
     weights, z_coarse (R, Nc) -> z_sorted (R, Nc+Nf+Nd) [, idx (R,Nf) int32, z_fine (R,Nf)]."""
     R, Nc = z_coarse.shape
     weights = _f32c(weights.reshape(R, Nc))
     z_coarse = _f32c(z_coarse)
     dev = z_coarse.device
+    if (u is None) != (u2 is None):
+        raise _lib.AVRError("sample_fine: u and u2 must be given together")
     if u is not None:
         u = _f32c(u.reshape(R, n_importance))
         u2 = _f32c(u2.reshape(R, n_importance))
         noise_depth = _f32c(noise_depth.reshape(R, n_depth)) if n_depth > 0 else None
     require_device(weights, z_coarse, u, u2, noise_depth)
+    ray_ids = _ray_ids(ray_ids, R)
     z_sorted = torch.empty(R, Nc + n_importance + n_depth, device=dev, dtype=F32)
     idx = torch.empty(R, n_importance, device=dev, dtype=torch.int32) if want_idx else None
     z_fine = torch.empty(R, n_importance, device=dev, dtype=F32) if want_fine else None
     call("avr_sample_fine", ptr(weights), ptr(z_coarse), float(near), float(far), R, Nc, n_importance, n_depth,
-         float(depth_std), ptr(u), ptr(u2), ptr(noise_depth), seed, offset, ptr(z_sorted), ptr(idx), ptr(z_fine),
+         float(depth_std), ptr(u), ptr(u2), ptr(noise_depth), seed, offset, ptr(ray_ids), ptr(z_sorted), ptr(idx),
+         ptr(z_fine),
          stream_of(z_coarse))
     return z_sorted, idx, z_fine
 
@@ -230,15 +246,41 @@ def sample_coarse_rays(near, far, n_samples, noise=None, seed=0, offset=0):
     return z
 
 
-def depth_of_points(world, c2w_info):
-    """depth_from_world(world, cam2world) for explicit world points (SB, R, 3) -> (SB, R)."""
+def depth_of_points_fwd(world, c2w_info):
     c2w, sb_stride, ray_stride = c2w_info
     SB, R, _ = world.shape
-    world = _f32c(world)
+    world = _f32c(world.detach())
     depth = torch.empty(SB, R, device=world.device, dtype=F32)
     call("avr_depth_from_world", ptr(world), None, None, ptr(c2w), sb_stride, ray_stride, SB, R, ptr(depth), None,
          stream_of(world))
     return depth
+
+
+class _DepthOfPoints(torch.autograd.Function):
+    """depth = -(inv(c2w)[2, :3] . x + inv(c2w)[2, 3]): d depth / d x = -inv(c2w)[2, :3]
+    (utils.py:358-361 is differentiable in the world points: the raymarchers' depth
+    loss reaches the LSTM through them, renderers.py:349, :486)."""
+
+    @staticmethod
+    def forward(ctx, world, c2w_info):
+        ctx.c2w_info = c2w_info
+        ctx.shape = world.shape
+        return depth_of_points_fwd(world, c2w_info)
+
+    @staticmethod
+    def backward(ctx, g):
+        c2w = ctx.c2w_info[0]
+        SB, R, _ = ctx.shape
+        row = -torch.linalg.inv(c2w.double())[..., 2, :3].to(F32)       # (SB, R or 1, 3)
+        return g.reshape(SB, R, 1) * row.expand(SB, R, 3), None
+
+
+def depth_of_points(world, c2w_info):
+    """depth_from_world(world, cam2world) for explicit world points (SB, R, 3) -> (SB, R);
+    differentiable w.r.t. world."""
+    if torch.is_grad_enabled() and world.requires_grad:
+        return _DepthOfPoints.apply(world, c2w_info)
+    return depth_of_points_fwd(world, c2w_info)
 
 
 def raymarch(view, gate_table, lstm, out_layer, ro, rd, init_dist, steps, trace=False):

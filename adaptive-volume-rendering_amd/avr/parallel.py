@@ -9,6 +9,8 @@ other exchange on the path: rays are independent and the field weights and
 latent are read-only, so each rank builds them locally (or receives them once
 through `broadcast_scene`).
 """
+import inspect
+
 import torch
 import torch.distributed as dist
 
@@ -35,9 +37,19 @@ def broadcast_scene(net, src=0, group=None):
         dist.broadcast(t.data, src, group=group)
 
 
+def _takes_ray_ids(fn):
+    try:
+        params = inspect.signature(fn).parameters
+    except (TypeError, ValueError):
+        return False
+    return "ray_ids" in params or any(p.kind == p.VAR_KEYWORD for p in params.values())
+
+
 def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None):
-    """render_fn(cam2world, intrinsics, x_pix) -> (rgb_c, rgb_f, depth, depth)
-    on this rank's tiles; returns the full-frame outputs on every rank.
+    """render_fn(cam2world, intrinsics, x_pix[, ray_ids=, n_rays_total=]) ->
+    (rgb_c, rgb_f, depth, depth) on this rank's tiles; returns the full-frame
+    outputs on every rank. A render_fn that accepts `ray_ids` (a
+    VolumeRenderer call) gets the frame-wide index of each of its rays.
     cam2world (SB,R,4,4) may be a stride-0 expand; x_pix (SB,R,2)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -47,7 +59,12 @@ def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None)
     c2w_local = cam2world if cam2world.shape[1] == 1 else cam2world[:, idx]
     if c2w_local.shape[1] == 1 and idx.numel() != 1:
         c2w_local = c2w_local.expand(SB, idx.numel(), 4, 4)
-    rgb_c, rgb_f, depth, _ = render_fn(c2w_local, intrinsics, x_pix[:, idx].contiguous())
+    if _takes_ray_ids(render_fn):
+        # frame-wide ray indices: the renderer's Philox draws then match the single-GPU render of the frame
+        rgb_c, rgb_f, depth, _ = render_fn(c2w_local, intrinsics, x_pix[:, idx].contiguous(), ray_ids=idx,
+                                           n_rays_total=R)
+    else:
+        rgb_c, rgb_f, depth, _ = render_fn(c2w_local, intrinsics, x_pix[:, idx].contiguous())
     n_loc = idx.numel()
     cap = max_local_rays(R, world, tile)
     packed = torch.zeros(SB, cap, 7, device=dev, dtype=torch.float32)

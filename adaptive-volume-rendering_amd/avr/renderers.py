@@ -57,16 +57,28 @@ def sample_fine(near_depth, far_depth, num_samples: int, weights, device: torch.
     """renderers.py:27-54. weights (SB, R, Nc, 1) -> z (SB, R, num_samples),
     unsorted, with the reference's rand / rand_like draws (or the given u, u2)."""
     SB, R, Nc, _ = weights.shape
-    near, far = float(near_depth.reshape(-1)[0]), float(far_depth.reshape(-1)[0])
+    if (u is None) != (u2 is None):
+        raise ValueError("sample_fine: u and u2 must be given together")
     if u is None:
         u = _noise((SB, R, num_samples), weights, "rand")
         u2 = _noise((SB, R, num_samples), weights, "rand")
+    near_t = torch.as_tensor(near_depth, dtype=torch.float32, device=weights.device)
+    far_t = torch.as_tensor(far_depth, dtype=torch.float32, device=weights.device)
+    uniform = bool((near_t == near_t.reshape(-1)[0]).all()) and bool((far_t == far_t.reshape(-1)[0]).all())
+    near, far = float(near_t.reshape(-1)[0]), float(far_t.reshape(-1)[0])
     # the z_coarse input only feeds the merge; any (R, Nc) tensor works here
     zc = torch.zeros(SB * R, Nc, device=weights.device, dtype=torch.float32)
     _, idx, zf = ops.sample_fine(weights.detach().reshape(SB * R, Nc), zc, near, far, num_samples, 0, 0.0, u=u,
                                  u2=u2, want_idx=True, want_fine=True)
-    zf = zf.reshape(SB, R, num_samples)
-    return (zf, idx.reshape(SB, R, num_samples)) if return_idx else zf
+    idx = idx.reshape(SB, R, num_samples)
+    if uniform:
+        zf = zf.reshape(SB, R, num_samples)
+    else:
+        # per-ray bounds: the kernel's bins with renderers.py:45-46's fp32 ops on (SB, R) near/far
+        z_steps = (idx.float() + u2.reshape(SB, R, num_samples)) / Nc
+        near_t, far_t = near_t.expand(SB, R), far_t.expand(SB, R)
+        zf = near_t.unsqueeze(-1) + (far_t - near_t).unsqueeze(-1) * z_steps
+    return (zf, idx) if return_idx else zf
 
 
 def sample_depth(depth, num_samples: int, depth_std, noise=None):
@@ -151,7 +163,12 @@ class VolumeRenderer(nn.Module):
             "depth": torch.randn(SB, R, self.n_fine_depth, device=dev),
         }
 
-    def forward(self, cam2world, intrinsics, x_pix, radiance_field: nn.Module, noise=None):
+    def forward(self, cam2world, intrinsics, x_pix, radiance_field: nn.Module, noise=None, ray_ids=None,
+                n_rays_total=None):
+        """ray_ids (R,) / n_rays_total: these R rays are rays ray_ids of an
+        n_rays_total-ray frame (a rank's share, avr.parallel.render_sharded):
+        the in-kernel Philox draws are keyed by the frame-wide ray index, so
+        a sharded render equals the single-GPU render of the same seed."""
         SB, R, _ = x_pix.shape
         dev = x_pix.device
         near, far = float(self.near[0]), float(self.far[0])
@@ -159,12 +176,17 @@ class VolumeRenderer(nn.Module):
         Nc, Nt = self.n_coarse, self.n_coarse + self.n_fine
         draws = self._draws(SB, R, dev, noise)
         seed, off = (self.seed or 0), self._offset
+        ids = None
+        if ray_ids is not None:
+            Rt = int(n_rays_total)
+            ids = (torch.arange(SB, device=dev, dtype=torch.int64)[:, None] * Rt
+                   + ray_ids.to(dev, torch.int64).reshape(1, R)).reshape(-1)
         if self.seed is not None:
-            self._offset += SB * R
+            self._offset += SB * (R if ray_ids is None else int(n_rays_total))
 
         ro, rd, c2w_info = ops.world_rays(x_pix, intrinsics, cam2world)
         zc = ops.sample_coarse(near, far, SB * R, Nc, dev, noise=None if draws is None else draws["coarse"],
-                               seed=seed, offset=off)
+                               seed=seed, offset=off, ray_ids=ids)
 
         fuse = hasattr(radiance_field, "can_fuse") and radiance_field.can_fuse(x_pix)
         self.last_path = "fused" if fuse else "module"
@@ -186,7 +208,7 @@ class VolumeRenderer(nn.Module):
         z_sorted, _, _ = ops.sample_fine(
             w_c.detach(), zc, near, far, nf, self.n_fine_depth, self.depth_std,
             u=None if draws is None else draws["u"], u2=None if draws is None else draws["u2"],
-            noise_depth=None if draws is None else draws["depth"], seed=seed, offset=off)
+            noise_depth=None if draws is None else draws["depth"], seed=seed, offset=off, ray_ids=ids)
         if self.t_stop is not None and not torch.is_grad_enabled():
             rgb_f, dist_f = self._fine_early_termination(ro, rd, z_sorted, radiance_field, fuse, SB, R)
         else:

@@ -32,7 +32,8 @@ constexpr int kCoarseTab = 1024;
 
 __global__ void __launch_bounds__(256) sample_coarse_kernel(float near_, float far_, int64_t n_rays, int n,
                                                             const float* __restrict__ noise, uint64_t seed,
-                                                            uint64_t offset, float* __restrict__ z) {
+                                                            uint64_t offset, const int64_t* __restrict__ ray_ids,
+                                                            float* __restrict__ z) {
   __shared__ float base_tab[kCoarseTab];
   const int nq = (n + 3) >> 2;                           // 4-sample blocks per ray
   const float span = fsub(far_, near_);
@@ -58,7 +59,8 @@ __global__ void __launch_bounds__(256) sample_coarse_kernel(float near_, float f
 #pragma unroll
     for (int k = 0; k < 4; ++k) u[k] = 4 * q + k < n ? noise[r * n + 4 * q + k] : 0.f;
   } else {
-    const float4 v = philox_uniform4(seed, offset + (uint64_t)r, (uint32_t)q, kStreamCoarse);
+    const uint64_t key = offset + (uint64_t)(ray_ids ? ray_ids[r] : r);
+    const float4 v = philox_uniform4(seed, key, (uint32_t)q, kStreamCoarse);
     u[0] = v.x; u[1] = v.y; u[2] = v.z; u[3] = v.w;
   }
   float o[4];
@@ -183,7 +185,8 @@ __device__ __forceinline__ float wave_sort64(float v, int lane) {
 __global__ void __launch_bounds__(256) sample_fine_kernel(
     const float* __restrict__ weights, const float* __restrict__ z_coarse, float near_, float far_, int64_t n_rays,
     int Nc, int Nf, int Nd, float depth_std, const float* __restrict__ u_in, const float* __restrict__ u2_in,
-    const float* __restrict__ nd_in, uint64_t seed, uint64_t offset, int sort_n, float* __restrict__ z_sorted,
+    const float* __restrict__ nd_in, uint64_t seed, uint64_t offset, const int64_t* __restrict__ ray_ids, int sort_n,
+    float* __restrict__ z_sorted,
     int32_t* __restrict__ idx_out, float* __restrict__ z_fine_out) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -195,6 +198,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
   float* sbuf = scratch + 64;   // lists: coarse [0, Nc) | fine [Nc, Nc+Nf) | depth [Nc+Nf, Ntot)
   float* obuf = sbuf + sort_n;
   const float span = fsub(far_, near_);
+  const uint64_t key = offset + (uint64_t)(ray_ids ? ray_ids[ray] : ray);   // Philox counter of this ray
 
   // 1) + 2)
   const float* w = weights + ray * Nc;
@@ -227,8 +231,8 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
   // 3) importance samples
   float zf_mine = FLT_MAX;
   for (int f = lane; f < Nf; f += 64) {
-    const float u = u_in ? u_in[ray * Nf + f] : philox_uniform(seed, offset + (uint64_t)ray, f, kStreamU);
-    const float u2 = u2_in ? u2_in[ray * Nf + f] : philox_uniform(seed, offset + (uint64_t)ray, f, kStreamU2);
+    const float u = u_in ? u_in[ray * Nf + f] : philox_uniform(seed, key, f, kStreamU);
+    const float u2 = u2_in ? u2_in[ray * Nf + f] : philox_uniform(seed, key, f, kStreamU2);
     const int cnt = count_below<false>(cdf, Nc + 1, u);   // #{cdf <= u}
     const int idx = cnt > 0 ? cnt - 1 : 0;
     const float steps = fdiv(fadd((float)idx, u2), (float)Nc);
@@ -241,7 +245,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
   // 4) depth samples: clamp(randn * std, near, far)  (quirk Q6)
   float zd_mine = FLT_MAX;
   for (int d = lane; d < Nd; d += 64) {
-    const float n = nd_in ? nd_in[ray * Nd + d] : philox_normal(seed, offset + (uint64_t)ray, d, kStreamDepth);
+    const float n = nd_in ? nd_in[ray * Nd + d] : philox_normal(seed, key, d, kStreamDepth);
     zd_mine = fminf(fmaxf(fmul(n, depth_std), near_), far_);
     sbuf[Nc + Nf + d] = zd_mine;
   }
@@ -291,7 +295,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
 using namespace avr;
 
 extern "C" int avr_sample_coarse(float near_, float far_, int64_t n_rays, int n_samples, const float* noise,
-                                 uint64_t seed, uint64_t offset, float* z, void* stream) {
+                                 uint64_t seed, uint64_t offset, const int64_t* ray_ids, float* z, void* stream) {
   AVR_REQUIRE(n_rays >= 0 && n_samples > 0, "avr_sample_coarse: bad sizes");
   const int64_t n = n_rays * n_samples;
   if (n == 0) return AVR_OK;
@@ -299,7 +303,7 @@ extern "C" int avr_sample_coarse(float near_, float far_, int64_t n_rays, int n_
   const int64_t threads = n_rays * ((n_samples + 3) / 4);
   sample_coarse_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, as_stream(stream)>>>(near_, far_, n_rays,
                                                                                        n_samples, noise, seed,
-                                                                                       offset, z);
+                                                                                       offset, ray_ids, z);
   return check_launch("sample_coarse_kernel");
 }
 
@@ -318,7 +322,7 @@ extern "C" int avr_sample_coarse_rays(const float* near_, const float* far_, int
 extern "C" int avr_sample_fine(const float* weights, const float* z_coarse, float near_, float far_, int64_t n_rays,
                                int n_coarse, int n_importance, int n_depth, float depth_std, const float* u,
                                const float* u2, const float* noise_depth, uint64_t seed, uint64_t offset,
-                               float* z_sorted, int32_t* idx, float* z_fine, void* stream) {
+                               const int64_t* ray_ids, float* z_sorted, int32_t* idx, float* z_fine, void* stream) {
   AVR_REQUIRE(n_rays >= 0, "avr_sample_fine: negative n_rays");
   AVR_REQUIRE(n_rays == 0 || (weights && z_coarse && z_sorted), "avr_sample_fine: null pointer");
   AVR_REQUIRE(n_coarse > 0 && n_coarse <= kMaxCoarse, "avr_sample_fine: n_coarse must be in [1, %d]", kMaxCoarse);
@@ -335,6 +339,6 @@ extern "C" int avr_sample_fine(const float* weights, const float* z_coarse, floa
   const size_t shm = (size_t)kFineWaves * fine_wave_floats(n_coarse, sort_n, ntot) * sizeof(float);
   sample_fine_kernel<<<grid, 64 * kFineWaves, shm, as_stream(stream)>>>(
       weights, z_coarse, near_, far_, n_rays, n_coarse, n_importance, n_depth, depth_std, u, u2, noise_depth, seed,
-      offset, sort_n, z_sorted, idx, z_fine);
+      offset, ray_ids, sort_n, z_sorted, idx, z_fine);
   return check_launch("sample_fine_kernel");
 }

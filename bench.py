@@ -27,6 +27,8 @@ import time
 import numpy as np
 import torch
 
+dist = None   # torch.distributed, imported when the job has more than one rank
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "adaptive-volume-rendering_amd"))
 
@@ -184,39 +186,119 @@ class HbmKernelTimer:
         return res
 
 
-def cpu_baseline(rays_cap=4096, budget_s=12.0):
-    """The oracle (numpy restatement of the reference path, 'port') on this
-    host's cores, on a bounded sample of the same workload: 128-ray chunks of
-    the 128 + 64 configuration with the same field architecture."""
+def cpu_share():
+    """CPU threads this process may use on the host: the affinity mask, the
+    cgroup CPU quota and OMP_NUM_THREADS (the GPU box pins these to the box's
+    share of the host), plus the host's physical core count for the record."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    cores, model = set(), ""
+    try:
+        phys = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and not model:
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                cores.add((phys, v))
+    except OSError:
+        pass
+    return n, len(cores) or None, model
+
+
+def _median_rate(fn, units, runs=3):
+    """1 untimed warm-up call, then the median rate of `runs` timed calls."""
+    fn(warm=True)
+    rates = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fn()
+        rates.append(units / (time.perf_counter() - t0))
+    return float(np.median(rates)), rates
+
+
+def cpu_baseline(c3_rays=384, c1_rays=2048):
+    """The reference's CPU path on this host's cores, SURVEY §8d protocol:
+    every thread this process may use, 1 warm-up, median of 3. Two ports are
+    timed and the faster one is the baseline (which one wins depends on the
+    host's BLAS / oneDNN): oracle/torch_port.py (the reference's own torch
+    operators: per-sample lin_z, grid_sample, searchsorted, cumprod) and the
+    numpy oracle (oracle/avr_oracle.py, row-layout latent gathers).
+      * C3 sample: c3_rays rays of the 128 + 64 configuration (same field
+        architecture, random-init weights, 512x64x64 latent) per run;
+      * C1 (BASELINE configs[0], the reference's own CPU case: 64 coarse
+        samples, coarse pass only): c1_rays of its 4096 rays per run, torch port."""
     sys.path.insert(0, REPO)
+    from threadpoolctl import threadpool_limits
     from oracle import avr_oracle as O
     from oracle import synth
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-    except Exception:  # noqa: BLE001
-        threads = 1
+    from oracle import torch_port as TP
+    threads, physical, model = cpu_share()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     pc = synth.resnetfc_params(42, 512, 512, 3, 1000, 40)
     pf = synth.resnetfc_params(42, 512, 512, 3, 1000, 57)
     poses, focal, c, image_shape, latent_scaling = synth.source_view((64, 64))
     latent = synth.hashed_normalish((1, 512, 64, 64), 45, 1.0)
-    field = O.PixelNeRFField(pc, pf, latent, poses, focal, c, image_shape, latent_scaling)
+    tfield = TP.TorchField(pc, pf, latent, poses, focal, c, image_shape, latent_scaling)
+    nfield = O.PixelNeRFField(pc, pf, latent, poses, focal, c, image_shape, latent_scaling)
+    gen = torch.Generator().manual_seed(0)
     rng = np.random.default_rng(0)
-    chunk, done, t_total = 128, 0, 0.0
-    K = synth.default_intrinsics()[None]
-    c2w1 = synth.orbit_cam2world(0.7)
-    while done < rays_cap and t_total < budget_s:
-        x_pix = rng.random((1, chunk, 2), dtype=np.float32)
-        c2w = np.broadcast_to(c2w1, (1, chunk, 4, 4))
-        noise = [rng.random((1, chunk, n), dtype=np.float32) for n in (128, 64, 64)]
-        t0 = time.perf_counter()
-        O.render(c2w, K, x_pix, field, 0.8, 1.8, 128, 64, 0, 0.01, True, noise[0], noise[1], noise[2],
-                 np.zeros((1, chunk, 0), np.float32))
-        t_total += time.perf_counter() - t0
-        done += chunk
-    return {"value": round(done / t_total, 2), "unit": "rays/s", "cores": int(threads), "kind": "port",
-            "sample": f"{done} rays x (128 coarse + 64 fine), oracle/avr_oracle.render (numpy, fp32 BLAS "
-                      f"{threads} threads), {t_total:.1f} s, host {os.cpu_count()} logical CPUs"}
+    K = synth.default_intrinsics()[None].astype(np.float32)
+    c2w1 = synth.orbit_cam2world(0.7).astype(np.float32)
+    Kt, c2wt = torch.from_numpy(K), torch.from_numpy(c2w1).reshape(1, 1, 4, 4)
+
+    def c3_torch(warm=False, chunk=128):
+        for _ in range(1 if warm else c3_rays // chunk):
+            TP.render(c2wt.expand(1, chunk, 4, 4), Kt, torch.rand(1, chunk, 2, generator=gen), tfield, 0.8, 1.8, 128,
+                      64, True, gen)
+
+    def c3_numpy(warm=False, chunk=128):
+        for _ in range(1 if warm else c3_rays // chunk):
+            noise = [rng.random((1, chunk, n), dtype=np.float32) for n in (128, 64, 64)]
+            O.render(np.broadcast_to(c2w1, (1, chunk, 4, 4)), K, rng.random((1, chunk, 2), dtype=np.float32),
+                     nfield, 0.8, 1.8, 128, 64, 0, 0.01, True, noise[0], noise[1], noise[2],
+                     np.zeros((1, chunk, 0), np.float32))
+
+    def c1_torch(warm=False, chunk=512):
+        for _ in range(1 if warm else c1_rays // chunk):
+            TP.render(c2wt.expand(1, chunk, 4, 4), Kt, torch.rand(1, chunk, 2, generator=gen), tfield, 0.8, 1.8, 64,
+                      0, True, gen, coarse_only=True)
+
+    t0 = time.perf_counter()
+    try:
+        with torch.no_grad(), threadpool_limits(limits=threads):
+            vt, rt = _median_rate(c3_torch, c3_rays)
+            vn, rn = _median_rate(c3_numpy, c3_rays)
+            v1, r1 = _median_rate(c1_torch, c1_rays)
+    finally:
+        torch.set_num_threads(prev_threads)
+    best = "torch_port" if vt >= vn else "numpy_oracle"
+    host = f"{model or 'host CPU'}, {os.cpu_count()} logical CPUs / {physical} physical cores on the host"
+    return {"value": round(max(vt, vn), 2), "unit": "rays/s", "cores": int(threads), "kind": "port", "runs": 3,
+            "stat": "median", "warmup": 1, "port": best,
+            "sample": f"{c3_rays} rays x (128 coarse + 64 fine) per run, the faster of oracle/torch_port.render "
+                      f"(the reference's torch CPU operators) and oracle/avr_oracle.render (numpy), fp32, on "
+                      f"{threads} threads = this process's CPU share (affinity / cgroup quota / OMP_NUM_THREADS); "
+                      f"{host}",
+            "torch_port": {"value": round(vt, 2), "runs_rays_per_s": [round(x, 2) for x in rt]},
+            "numpy_oracle": {"value": round(vn, 2), "runs_rays_per_s": [round(x, 2) for x in rn]},
+            "config1": {"value": round(v1, 2), "unit": "rays/s", "runs": 3, "stat": "median",
+                        "sample": f"BASELINE configs[0] (4096 rays x 64 coarse samples, coarse pass only: rays, "
+                                  f"stratified z, coarse field, volume integral), {c1_rays} rays per run, torch port",
+                        "runs_rays_per_s": [round(x, 2) for x in r1]},
+            "wall_s": round(time.perf_counter() - t0, 1)}
 
 
 def run_train(args, device):
@@ -287,32 +369,120 @@ def run_train(args, device):
     print(json.dumps(line), flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as sock:
+        sock.bind(("127.0.0.1", 0))
+        return sock.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`--gpus N` (N > 1) started without a torch.distributed launcher: run the
+    N ranks as a child `torch.distributed.run` (one process per GPU, rendezvous
+    on 127.0.0.1) and return its exit status. This process has not touched
+    the GPU (nothing before this call initialises HIP), and it is never
+    replaced by exec: the ranks are children."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def standin_render(c2w, K, x_pix, ray_ids=None, n_rays_total=None):
+    """--device cpu: a deterministic per-ray function of the ray's own inputs
+    (the HIP renderer needs a GPU). It exercises the launcher, the tile
+    dealing and the gather of the config-5 path on gloo; it measures nothing."""
+    rgb_c = torch.stack([x_pix[..., 0], x_pix[..., 1], x_pix.sum(-1)], -1)
+    rgb_f = torch.sin(rgb_c * 3.0) + c2w[..., 0, 3:4]
+    depth = x_pix[..., 0] * 10 + K[:, 0, 0, None]
+    return rgb_c, rgb_f, depth, depth
+
+
+def run_standin(args, config, world, rank):
+    from avr.parallel import render_sharded
+    from avr.video import get_opencv_pixel_coordinates
+    n_views = 4 if config == 5 else 1
+    x_pix = get_opencv_pixel_coordinates(args.frame, args.frame).reshape(1, -1, 2).repeat(1, n_views, 1)
+    R = x_pix.shape[1]
+    c2w = torch.stack([orbit_c2w(2 * np.pi * v / n_views) for v in range(n_views)])
+    c2w = c2w.repeat_interleave(R // n_views, 0).reshape(1, R, 4, 4)
+    K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]])
+
+    def step():
+        if world > 1:
+            return render_sharded(standin_render, c2w, K, x_pix)
+        return standin_render(c2w, K, x_pix)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    if rank == 0:
+        line = {"metric": "rays/sec (128 coarse + 64 fine samples) + achieved HBM GB/s vs roofline",
+                "value": round(R * args.steps / elapsed, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                "scaling": "strong" if config == 5 else "weak", "vs_baseline": None, "dtype": "fp32",
+                "data": "STAND-IN renderer on the CPU (--device cpu): launcher / sharding test, not a measurement",
+                "config": {"workload": f"stand-in, {n_views} views x {args.frame}x{args.frame}", "rays_per_step": R,
+                           "parallelism": f"ray-shard x{world} + gloo gather"},
+                "checksum": [round(float(o.double().sum()), 6) for o in out[:3]]}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
+    global dist
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without torch.distributed.run's environment, N > 1 starts the ranks "
+                         "itself")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rays", type=int, default=65536, help="rays per GPU per step")
+    ap.add_argument("--rays", type=int, default=65536, help="config 3: rays per GPU per step")
     ap.add_argument("--n-coarse", type=int, default=128)
     ap.add_argument("--n-fine", type=int, default=64)
     ap.add_argument("--precision", choices=["x3", "fp32"], default="x3",
                     help="field MFMA path: split-fp16 (3 products, fp32 accumulate) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", type=int, choices=[3, 4, 5], default=3,
-                    help="BASELINE config: 3 = 65536 random rays (default); 5 = 4 orbit views of 800x800 per step "
-                         "sharded over the ranks in 64-ray tiles (strong scaling, avr.parallel.render_sharded); "
-                         "4 = one 800x800 frame per step "
-                         "with fine-pass early termination at T_stop 1e-5")
+    ap.add_argument("--config", type=int, choices=[3, 4, 5], default=None,
+                    help="BASELINE config (default: 3 on one GPU, 5 on more): 3 = 65536 random rays per GPU (weak "
+                         "scaling); 5 = 4 orbit views of 800x800 per step for the whole job, dealt to the ranks in "
+                         "64-ray tiles (strong scaling, avr.parallel.render_sharded); 4 = one 800x800 frame per "
+                         "step with fine-pass early termination at T_stop 1e-5")
+    ap.add_argument("--frame", type=int, default=800, help="configs 4/5: frame side in pixels")
     ap.add_argument("--sigma-bias", type=float, default=0.0,
                     help="density bias of the synthetic field (config 4: opacity of the scene)")
     ap.add_argument("--mode", choices=["render", "train"], default="render",
                     help="render: the headline inference metric; train: one train.py step per step (1 GPU)")
     ap.add_argument("--train-modes", default="hip,torch", help="--mode train: which autograd paths to time")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: stand-in renderer on gloo (tests the launcher and the config-5 sharding only)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    config = args.config if args.config is not None else (3 if world == 1 else 5)
+    if args.device == "cpu":
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        return run_standin(args, config, world, rank)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
@@ -334,21 +504,22 @@ def main():
     hbm = HbmKernelTimer(avr.ops)
     hbm.install()
     rend = VolumeRenderer(0.8, 1.8, args.n_coarse, args.n_fine, 0, 0.01, True)
-    rend.seed = 1234 + rank
-    if args.config == 4:
+    # config 5: one frame-wide Philox stream keyed by global ray ids (render_sharded); else a batch per rank
+    rend.seed = 1234 if config == 5 else 1234 + rank
+    if config == 4:
         # one full 800x800 frame per step (get_opencv_pixel_coordinates grid), fine pass with early
         # termination at T_stop = 1e-5; with N GPUs each rank renders its own frame
         from avr.video import get_opencv_pixel_coordinates
-        x_pix = get_opencv_pixel_coordinates(800, 800).reshape(1, -1, 2).to(device)
+        x_pix = get_opencv_pixel_coordinates(args.frame, args.frame).reshape(1, -1, 2).to(device)
         R = x_pix.shape[1]
         rend.t_stop = 1e-5
-    elif args.config == 5:
+    elif config == 5:
         # BASELINE config 5: 4 views x 800x800 per step for the whole job; every rank renders its 64-ray tiles
         # of all 4 views and one all_gather assembles the frames (avr.parallel.render_sharded)
         # (one scene: the 4 views are one ray batch of 4 x 640 000 rays with a per-ray pose)
         from avr.video import get_opencv_pixel_coordinates
         n_views = 4
-        x_pix = get_opencv_pixel_coordinates(800, 800).reshape(1, -1, 2).repeat(1, n_views, 1).to(device)
+        x_pix = get_opencv_pixel_coordinates(args.frame, args.frame).reshape(1, -1, 2).repeat(1, n_views, 1).to(device)
         R = x_pix.shape[1]
     else:
         R = args.rays
@@ -356,7 +527,7 @@ def main():
         x_pix = torch.rand(1, R, 2, generator=g).to(device)
     K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]], device=device)
     gathered = None
-    if args.config == 5:
+    if config == 5:
         from avr.parallel import render_sharded
         c2w = torch.stack([orbit_c2w(2 * np.pi * v / n_views) for v in range(n_views)]).to(device)
         c2w = c2w.repeat_interleave(R // n_views, 0).reshape(1, R, 4, 4)
@@ -368,15 +539,15 @@ def main():
     def step():
         fused._packed.clear()       # per-scene prep inside the step: repack weights, rebuild lin_z tables
         with torch.no_grad():
-            if args.config == 5:
+            if config == 5:
                 if world > 1:
-                    rgb_c, rgb_f, depth, _ = render_sharded(lambda c, k, x: rend(c, k, x, net), c2w, K, x_pix)
+                    rgb_c, rgb_f, depth, _ = render_sharded(lambda c, k, x, **ids: rend(c, k, x, net, **ids),
+                                                            c2w, K, x_pix)
                 else:
                     rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
                 return rgb_f
             rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
             if world > 1:
-                import torch.distributed as dist
                 local = torch.cat([rgb_c.reshape(-1), rgb_f.reshape(-1), depth.reshape(-1)])
                 dist.all_gather_into_tensor(gathered, local)
         return rgb_f
@@ -388,7 +559,6 @@ def main():
     timer.reset()
     hbm.on = True
     if world > 1:
-        import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -409,7 +579,7 @@ def main():
     assert bool(torch.isfinite(out).all())
 
     # whole-job rays: config 5 renders a fixed 4 x 800 x 800 per step over all ranks (strong scaling)
-    rays_total = (R if args.config == 5 else R * world) * args.steps
+    rays_total = (R if config == 5 else R * world) * args.steps
     value = rays_total / elapsed
     samples_per_ray = args.n_coarse + args.n_coarse + args.n_fine
     fps = field_flops_per_sample()
@@ -431,21 +601,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "strong" if args.config == 5 else "weak",
+        "scaling": "strong" if config == 5 else "weak",
         "vs_baseline": None,
         "dtype": "fp32" if args.precision == "fp32" else "fp32 (field products as 3 fp16 MFMA terms)",
-        "data": ("synthetic rays (x_pix ~ U[0,1)^2, orbit pose)" if args.config == 3 else
+        "data": ("synthetic rays (x_pix ~ U[0,1)^2, orbit pose)" if config == 3 else
                  "synthetic rays (get_opencv_pixel_coordinates 800x800 grid, orbit poses)")
                 + ", random-init default.conf field, random 512x64x64 latent",
         "config": {"workload": (f"BASELINE config 3: {R} rays/GPU x ({args.n_coarse} coarse + {args.n_fine} fine, "
                                 "n_fine_depth 0), conf/default.conf PixelNeRF field (3x512 ResnetFC, d_latent 512)")
-                   if args.config == 3 else
+                   if config == 3 else
                    (f"BASELINE config 4: 800x800 frame ({R} rays)/GPU x ({args.n_coarse} coarse + {args.n_fine} "
                     f"fine), fine-pass early termination T_stop 1e-5, sigma bias {args.sigma_bias}, "
-                    "conf/default.conf PixelNeRF field") if args.config == 4 else
+                    "conf/default.conf PixelNeRF field") if config == 4 else
                    (f"BASELINE config 5: 4 orbit views x 800x800 ({R} rays) per step over {world} GPU(s) in "
                     f"64-ray tiles x ({args.n_coarse} coarse + {args.n_fine} fine), conf/default.conf PixelNeRF field"),
-                   "rays_per_gpu": R if args.config != 5 else -(-R // world), "n_coarse": args.n_coarse, "n_fine": args.n_fine,
+                   "rays_per_gpu": R if config != 5 else -(-R // world), "n_coarse": args.n_coarse, "n_fine": args.n_fine,
                    "field_samples_per_ray": samples_per_ray, "parallelism": f"ray-shard x{world} + RCCL gather"},
         "roofline": {
             "kernel": kname,
@@ -466,9 +636,14 @@ def main():
     line["hbm_kernels"] = hbm.report()
     pmc = os.path.join(REPO, "profiles", "field_pmc.json")
     if os.path.exists(pmc):
+        # not measured in this run: the committed rocprofv3 --pmc pass over this bench (TCC_EA0 read/write
+        # bytes, FETCH_SIZE x2 on gfx950), i.e. L2->fabric bytes INCLUDING Infinity-Cache (MALL) hits
         with open(pmc) as f:
-            line["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
-    if args.config == 4:
+            j = json.load(f)
+        line["roofline"]["traffic"] = j.get("hbm_bytes_per_launch")
+        line["roofline"]["traffic_source"] = ("profiles/field_pmc.json constant (" + str(j.get("source", "")) +
+                                              "): L2->fabric bytes per field launch incl. MALL hits, not DRAM-only")
+    if config == 4:
         line["config"]["fine_samples_evaluated_fraction"] = round(
             fine_evaluated / (args.steps * R * (args.n_coarse + args.n_fine)), 4)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 3
+#define AVR_ABI_VERSION 4
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -66,9 +66,12 @@ int avr_depth_from_world(const float* ro, const float* rd, const float* dist, co
  * sample_coarse — renderers.py:4-24 (infinity == -1 branch).
  *   z (n_rays, n_samples) = near + (far-near)*i/N + U*(far-near)/N
  *   noise (n_rays, n_samples) U[0,1) draws, or NULL: counter-based Philox
- *   keyed on (seed, offset + ray, sample).                                     */
+ *   keyed on (seed, offset + id(ray), sample).
+ *   ray_ids (n_rays) int64 or NULL: id(ray) = ray_ids[ray] instead of ray --
+ *   a rank's share of a sharded frame keyed by each ray's index in the whole
+ *   frame, so the draws do not depend on how the frame was dealt out.          */
 int avr_sample_coarse(float near_, float far_, int64_t n_rays, int n_samples, const float* noise,
-                      uint64_t seed, uint64_t offset, float* z, void* stream);
+                      uint64_t seed, uint64_t offset, const int64_t* ray_ids, float* z, void* stream);
 
 /* sample_coarse with per-ray near/far (n_rays) — AdaptiveVolumeRenderer's band
  * around the raymarched distance (renderers.py:492-493).                        */
@@ -81,15 +84,16 @@ int avr_sample_coarse_rays(const float* near_, const float* far_, int64_t n_rays
  *   z_coarse (n_rays, n_coarse)
  *   u, u2    (n_rays, n_importance) the rand / rand_like draws,
  *   noise_depth (n_rays, n_depth)   the randn_like draw;
- *            all three NULL together => in-kernel Philox (seed, offset).
+ *            all three NULL together => in-kernel Philox (seed, offset + id(ray)),
+ *            ray_ids as for avr_sample_coarse.
  *   z_sorted (n_rays, n_coarse + n_importance + n_depth) ascending
  *   idx      (n_rays, n_importance) int32 inverse-CDF bin (may be NULL)
  *   z_fine   (n_rays, n_importance) unsorted importance z (may be NULL)
  * n_coarse <= 256, total samples <= 512.                                       */
 int avr_sample_fine(const float* weights, const float* z_coarse, float near_, float far_, int64_t n_rays,
                     int n_coarse, int n_importance, int n_depth, float depth_std, const float* u, const float* u2,
-                    const float* noise_depth, uint64_t seed, uint64_t offset, float* z_sorted, int32_t* idx,
-                    float* z_fine, void* stream);
+                    const float* noise_depth, uint64_t seed, uint64_t offset, const int64_t* ray_ids,
+                    float* z_sorted, int32_t* idx, float* z_fine, void* stream);
 
 /* --------------------------------------------------------------- composite
  * volume_integral — renderers.py:69-119.

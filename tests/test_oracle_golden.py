@@ -116,3 +116,31 @@ def test_adaptive_renderer_golden(golden):
     np.testing.assert_allclose(rgb, g["rgb"], atol=1e-4)
     np.testing.assert_allclose(depth_c, g["depth_coarse"], atol=2e-5)
     np.testing.assert_allclose(depth, g["depth"], atol=1e-4)
+
+
+def test_torch_port_matches_oracle(golden):
+    """oracle/torch_port.py (bench.py's timed CPU baseline) renders what the
+    numpy oracle renders for the same draws (coarse and fine rgb, depth)."""
+    import torch
+    from oracle import torch_port as TP
+    g = golden("g4_field_small.npz")
+    pc, pf, latent = synth.field_from_meta(g)
+    args = (pc, pf, latent, g["poses"], g["focal"], g["c"], g["image_shape"], g["latent_scaling"])
+    kw = dict(n_blocks=int(g["n_blocks"]), combine_layer=int(g["combine_layer"]))
+    R, Nc, Nf = 96, 32, 16
+    rng = np.random.default_rng(3)
+    x_pix = rng.random((1, R, 2), dtype=np.float32)
+    c2w = np.broadcast_to(synth.orbit_cam2world(0.4), (1, R, 4, 4)).astype(np.float32)
+    K = synth.default_intrinsics()[None].astype(np.float32)
+    gen = torch.Generator().manual_seed(11)
+    rgb_c, rgb_f, depth = TP.render(torch.from_numpy(c2w.copy()), torch.from_numpy(K), torch.from_numpy(x_pix),
+                                    TP.TorchField(*args, **kw), 0.8, 1.8, Nc, Nf, True, gen)
+    gen = torch.Generator().manual_seed(11)       # the same draws, in the reference's order
+    nc = torch.rand(1, R, Nc, generator=gen).numpy()
+    u = torch.rand(1, R, Nf, generator=gen).numpy()
+    u2 = torch.rand(1, R, Nf, generator=gen).numpy()
+    o_c, o_f, o_d, _ = O.render(c2w, K, x_pix, O.PixelNeRFField(*args, **kw), 0.8, 1.8, Nc, Nf, 0, 0.01, True,
+                                nc, u, u2, np.zeros((1, R, 0), np.float32))
+    np.testing.assert_allclose(rgb_c.numpy(), o_c, atol=1e-4, rtol=0)
+    ok = (np.abs(rgb_f.numpy() - o_f).max(-1) <= 1e-4) & (np.abs(depth.numpy() - o_d) <= 1e-4)
+    assert ok.mean() >= 0.98, ok.mean()      # a fine bin may flip at an exact cdf tie between fp paths
