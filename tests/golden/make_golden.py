@@ -265,7 +265,8 @@ def g2_sample_fine(R):
     wd[0, :, 40, 0] = synth.hashed_uniform((R,), 26, 0.0, 0.3)
     ud = synth.hashed_uniform((1, R, Nf), 27, 0.999, 1.0)
     cases.append(("spiky", wd, ud))
-    for name, w, uu in cases:
+    for i, (name, w, uu) in enumerate(cases):
+        torch.manual_seed(2000 + i)        # the un-injected draws are reproducible from this recipe
         cap = Capture()
         if uu is not None:
             cap.inject["rand"] = [torch.from_numpy(uu)]
@@ -310,6 +311,9 @@ def g4_field():
         "small": (64, 3, 1000, 1, (8, 8), True),
         "small_mv": (64, 5, 3, 1, (8, 8), True),
         "full": (512, 3, 1000, 4, (64, 64), False),
+        # conf/default_mv.conf:4-21 (5 x 512, combine_layer 3): train.py:262's config
+        "mv512": (512, 5, 3, 4, (64, 64), False),
+        "d256": (256, 3, 1000, 4, (64, 64), False),
     }.items():
         net, meta, params = build_field(REF_M, d_hidden, n_blocks, combine, num_layers, lhw, 40, store)
         xyz = synth.hashed_uniform((1, B, 3), 41, -0.5, 0.5)
