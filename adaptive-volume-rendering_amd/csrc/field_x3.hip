@@ -295,6 +295,9 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   AVR_STAMP(27);
   const int D = a.n_lin_z > 0 ? dedup_texels(tail, lane, wid) : 0;
   AVR_STAMP(28);
+#ifdef AVR_STAMPS
+  if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 64 + 31] = (unsigned long long)D;
+#endif
   float pe[PES], xo = 0.f, vo = 0.f;
   float mx = 0.f;
   {

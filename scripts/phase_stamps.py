@@ -24,8 +24,13 @@ net = bench.build_scene(dev)
 net.field_precision = os.environ.get("PREC", "x3")
 f = net.fused()
 R, N = 65536, 192
-ro = torch.tensor([[0.3, -1.1, 0.5]], device=dev).expand(R, 3).contiguous()
-rd = torch.nn.functional.normalize(-ro + 0.3 * torch.randn(R, 3, device=dev), dim=-1)
+# the bench's rays (config 3: orbit pose 0.7, normalized intrinsics, x_pix ~ U[0,1)^2)
+from avr import ops  # noqa: E402
+K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]], device=dev)
+c2w = bench.orbit_c2w(0.7).to(dev).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
+x_pix = torch.rand(1, R, 2, generator=torch.Generator().manual_seed(100)).to(dev)
+ro, rd, _ = ops.world_rays(x_pix, K, c2w)
+ro, rd = ro[0].contiguous(), rd[0].contiguous()
 z = torch.sort(0.8 + torch.rand(R, N, device=dev), -1)[0]
 blocks = (R * N + 63) // 64
 stamps = torch.zeros(blocks * 64, dtype=torch.int64, device=dev)
@@ -62,3 +67,8 @@ for k in used[1:]:
 print(f"{'total (median per block)':28s} {tot:10.0f} cyc")
 span = (st[:, used[-1]].max() - st[:, 0].min())
 print("blocks per CU (approx)", blocks / 256, "span cycles", span)
+dd = st_all[:, 0, 31]
+if (dd > 0).mean() > 0.99:
+    q = np.percentile(dd, [0, 10, 50, 90, 99, 100])
+    print("distinct texels per workgroup D: min/p10/p50/p90/p99/max " + " ".join(f"{x:.0f}" for x in q)
+          + f"; D > 64: {100 * (dd > 64).mean():.2f} % of workgroups")

@@ -112,6 +112,9 @@ def test_c3_stagewise_vs_oracle(golden, precision):
     np.testing.assert_array_equal(to_np(zs[S]), np.sort(np.concatenate([to_np(zc[S]), zf_o[0]], -1), -1))
     # fine field where the oracle chose the same bins (same sorted z)
     same = (to_np(idx[S]) == aux["idx"][0]).all(-1)
+    d_fc = np.abs(to_np(fc[S]) - aux["field_coarse"][0])
+    print(f"{precision}: rays with the oracle's bins {same.mean():.5f}; coarse field max err rgb "
+          f"{d_fc[..., :3].max():.2e} sigma {d_fc[..., 3].max():.2e}")
     assert same.mean() >= 0.999, same.mean()
     np.testing.assert_allclose(to_np(ff[S])[same], aux["field_fine"][0][same], atol=5e-5, rtol=1e-4)
     # end to end
