@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .conf import Conf
+from .encoder import make_encoder
 
 
 def repeat_interleave(x, repeats, dim=0):
@@ -142,36 +143,6 @@ class ResnetFC(nn.Module):
                    use_spade=conf.get_bool("use_spade", False), **kwargs)
 
 
-class LatentEncoder(nn.Module):
-    """Holds the per-scene feature map that SpatialEncoder.forward
-    (models.py:276-329) would produce, and samples it like SpatialEncoder.index
-    (models.py:245-274). The ResNet34 itself is out of scope (per-scene CNN)."""
-
-    def __init__(self, latent_size=512, index_interp="bilinear", index_padding="border"):
-        super().__init__()
-        self.latent_size = latent_size
-        self.index_interp, self.index_padding = index_interp, index_padding
-        self.register_buffer("latent", torch.empty(1, 1, 1, 1), persistent=False)
-        self.register_buffer("latent_scaling", torch.empty(2, dtype=torch.float32), persistent=False)
-
-    def set_latent(self, latent):
-        self.latent = latent
-        ls = torch.tensor([latent.shape[-1], latent.shape[-2]], dtype=torch.float32, device=latent.device)
-        self.latent_scaling = ls / (ls - 1) * 2.0
-        return self.latent
-
-    def index(self, uv, cam_z=None, image_size=(), z_bounds=None):
-        if uv.shape[0] == 1 and self.latent.shape[0] > 1:
-            uv = uv.expand(self.latent.shape[0], -1, -1)
-        if len(image_size) > 0:
-            if len(image_size) == 1:
-                image_size = (image_size, image_size)
-            uv = uv * (self.latent_scaling / image_size) - 1.0
-        samples = F.grid_sample(self.latent, uv.unsqueeze(2), align_corners=True, mode=self.index_interp,
-                                padding_mode=self.index_padding)
-        return samples[:, :, :, 0]
-
-
 def make_mlp(conf, d_in, d_latent=0, allow_empty=False, bn=False, **kwargs):
     """models.py:18-28 (the resnet type; 'mlp' ImplicitNet is not part of this path)."""
     mlp_type = conf.get_string("type", "mlp")
@@ -183,16 +154,15 @@ def make_mlp(conf, d_in, d_latent=0, allow_empty=False, bn=False, **kwargs):
 
 
 class NewPixelNeRFNet(nn.Module):
-    """models.py:609-863 with the encoder replaced by LatentEncoder."""
+    """models.py:609-863. The encoder is avr.encoder.SpatialEncoder (ResNet34
+    feature pyramid, torchvision module names); encode() runs it on the source
+    images, encode_latent() installs a precomputed feature map instead."""
 
     def __init__(self, conf, stop_encoder_grad=False, bn=False):
         super().__init__()
         conf = conf if hasattr(conf, "get_bool") else Conf(conf)
         enc = conf["encoder"] if "encoder" in conf else Conf({})
-        num_layers = enc.get_int("num_layers", 4)
-        self.encoder = LatentEncoder([0, 64, 128, 256, 512, 1024][num_layers],
-                                     enc.get_string("index_interp", "bilinear"),
-                                     enc.get_string("index_padding", "border"))
+        self.encoder = make_encoder(enc if hasattr(enc, "get_bool") else Conf(enc))
         self.use_encoder = conf.get_bool("use_encoder", True)
         self.use_xyz = conf.get_bool("use_xyz", False)
         assert self.use_encoder or self.use_xyz
@@ -227,19 +197,42 @@ class NewPixelNeRFNet(nn.Module):
         self.hip_backward = True        # autograd through the HIP field (avr.field._FieldTrain)
         self._fused = None
 
+    def encode(self, images, poses, focal, z_bounds=None, c=None):
+        """models.py:682-737: run the encoder on the source views and keep
+        their world->camera poses, focal (fy negated) and principal point.
+        images (NS, 3, H, W) or (SB, NS, 3, H, W); poses (NS, 4, 4) or
+        (SB, NS, 4, 4) camera->world."""
+        self.num_objs = images.size(0)
+        if len(images.shape) == 5:
+            assert len(poses.shape) == 4
+            assert poses.size(1) == images.size(1)   # NS input views
+            self.num_views_per_obj = images.size(1)
+            images = images.reshape(-1, *images.shape[2:])
+            poses = poses.reshape(-1, 4, 4)
+        else:
+            self.num_views_per_obj = 1
+        self.encoder(images)
+        self._set_view(poses, focal, c, (images.shape[-1], images.shape[-2]), images.device)
+
     def encode_latent(self, latent, poses, focal, c=None, image_shape=None):
-        """The pose / focal / principal-point bookkeeping of encode()
-        (models.py:692-734) for a precomputed latent (NS, L, H, W)."""
+        """encode() for a precomputed feature map (NS, L, H, W) (e.g. cached
+        per scene): the same pose / focal / principal-point bookkeeping;
+        image_shape (W, H) of the source images, by default 2x the map (the
+        ResNet's stride-2 conv1)."""
         self.num_objs = latent.size(0)
         self.num_views_per_obj = 1
         self.encoder.set_latent(latent)
+        if image_shape is None:
+            image_shape = (latent.shape[-1] * 2, latent.shape[-2] * 2)
+        self._set_view(poses, focal, c, image_shape, latent.device)
+
+    def _set_view(self, poses, focal, c, image_shape, device):
+        """models.py:705-734."""
         rot = poses[:, :3, :3].transpose(1, 2)
         trans = -torch.bmm(rot, poses[:, :3, 3:])
         self.poses = torch.cat((rot, trans), dim=-1)
-        if image_shape is None:
-            image_shape = (latent.shape[-1] * 2, latent.shape[-2] * 2)  # ResNet conv1 stride 2
-        self.image_shape = torch.tensor([float(image_shape[0]), float(image_shape[1])], device=latent.device)
-        focal = torch.as_tensor(focal, dtype=torch.float32, device=latent.device)
+        self.image_shape = torch.tensor([float(image_shape[0]), float(image_shape[1])], device=device)
+        focal = torch.as_tensor(focal, dtype=torch.float32, device=device)
         if focal.dim() == 0:
             focal = focal[None, None].repeat((1, 2))
         elif focal.dim() == 1:
@@ -251,16 +244,12 @@ class NewPixelNeRFNet(nn.Module):
         if c is None:
             c = (self.image_shape * 0.5).unsqueeze(0)
         else:
-            c = torch.as_tensor(c, dtype=torch.float32, device=latent.device)
+            c = torch.as_tensor(c, dtype=torch.float32, device=device)
             if c.dim() == 0:
                 c = c[None, None].repeat((1, 2))
             elif c.dim() == 1:
                 c = c.unsqueeze(-1).repeat((1, 2))
         self.c = c
-
-    def encode(self, images, poses, focal, z_bounds=None, c=None):
-        raise NotImplementedError("the per-scene ResNet34 encoder is out of scope: compute the latent map "
-                                  "elsewhere and call encode_latent(latent, poses, focal, c)")
 
     # ------------------------------------------------------------------ forward
     def fused(self):

@@ -101,8 +101,8 @@ def render_orbit(renderer, radiance_field, intrinsics, num_frames, radius, heigh
 def generate_video(model_input, num_frames, radius, net, model, fine=True):
     """utils.py:481-537 with the same arguments: encode the first source view
     of model_input into `net`, then render the orbit through `model`
-    (a RadFieldAndRenderer). Encoding needs the ResNet34 encoder; a net whose
-    latent was set with encode_latent() keeps it (no `images` needed)."""
+    (a RadFieldAndRenderer). A net whose latent was set with encode_latent()
+    keeps it (no `images` needed); otherwise the source view is encoded."""
     intrinsics = model_input["intrinsics"][0:1, 0, ...]
     if "images" in model_input and net.encoder.latent.shape[-1] <= 1:   # no latent yet
         gt = model_input["images"]
