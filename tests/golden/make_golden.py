@@ -434,6 +434,45 @@ def g7_encoder():
     save("g7_encoder.npz", **out)
 
 
+def g8_batching():
+    """train.py:53-83's ray batching with the reference's utils (batched_index_select_nd,
+    bbox_sample) and its draw order, on a small synthetic collated batch."""
+    SB, NV, sl = 2, 3, 8
+    sl2 = sl * sl
+    images = torch.from_numpy(synth.hashed_uniform((SB, NV, sl2, 3), 81, -1.0, 1.0))
+    cam2world = torch.from_numpy(synth.hashed_uniform((SB, NV, 4, 4), 82))
+    intr = torch.from_numpy(synth.hashed_uniform((SB, NV, 3, 3), 83))
+    focal = torch.from_numpy(synth.hashed_uniform((SB, NV), 84, 50.0, 60.0))
+    c = torch.from_numpy(synth.hashed_uniform((SB, NV, 2), 85, 30.0, 34.0))
+    x_pix = torch.from_numpy(synth.hashed_uniform((SB, NV, sl2, 2), 86))
+    bbox = torch.tensor([[[1, 2, 5, 6], [0, 0, 7, 7], [3, 1, 4, 2]], [[2, 2, 2, 2], [0, 3, 6, 7], [1, 1, 6, 5]]],
+                        dtype=torch.float32)
+    out = dict(images=images.numpy(), cam2world=cam2world.numpy(), intrinsics=intr.numpy(), focal=focal.numpy(),
+               c=c.numpy(), x_pix=x_pix.numpy(), bbox=bbox.numpy())
+    for with_bbox in (False, True):
+        torch.manual_seed(880 + int(with_bbox))
+        R = 16
+        src_idx = torch.randint(0, NV, (SB, 1))
+        src_images = REF_U.batched_index_select_nd(images, src_idx).reshape(SB, 1, sl, sl, 3).permute(0, 1, 4, 2, 3)
+        poses = REF_U.batched_index_select_nd(cam2world, src_idx)
+        f = REF_U.batched_index_select_nd(focal, src_idx)[0, 0]
+        cc = REF_U.batched_index_select_nd(c, src_idx)[0, 0, :]
+        if with_bbox:
+            rays_idx = torch.stack([(lambda p: p[..., 0] * sl2 + p[..., 1] * sl + p[..., 2])(
+                REF_U.bbox_sample(bbox[sb], R)) for sb in range(SB)])
+        else:
+            rays_idx = torch.randint(0, NV * sl2, (SB, R))
+        xp = REF_U.batched_index_select_nd(x_pix.reshape(SB, -1, 2), rays_idx)
+        cw = REF_U.batched_index_select_nd(cam2world.unsqueeze(2).expand(SB, NV, sl2, 4, 4).reshape(SB, -1, 4, 4),
+                                           rays_idx)
+        gt = 0.5 * REF_U.batched_index_select_nd(images.reshape(SB, -1, 3), rays_idx) + 0.5
+        k = f"bbox{int(with_bbox)}"
+        out.update({f"{k}_seed": np.int64(880 + int(with_bbox)), f"{k}_src_images": src_images.numpy(),
+                    f"{k}_poses": poses.numpy(), f"{k}_focal": f.numpy(), f"{k}_c": cc.numpy(),
+                    f"{k}_x_pix": xp.numpy(), f"{k}_cam2world": cw.numpy(), f"{k}_gt": gt.numpy()})
+    save("g8_batching.npz", **out)
+
+
 if __name__ == "__main__":
     REF_U, REF_R, REF_M = import_reference()
     sys.path.insert(0, os.path.join(REPO, "adaptive-volume-rendering_amd"))
@@ -446,3 +485,4 @@ if __name__ == "__main__":
     g5_forward(64)
     g6_adaptive(48)
     g7_encoder()
+    g8_batching()
