@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -63,6 +63,10 @@ _SIGS = {
     "avr_sample_fine": [c_void_p, c_void_p, c_float, c_float, i64, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
                         c_void_p, u64, u64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_composite_fwd": [c_void_p, c_void_p, i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    "avr_composite_fwd_depth": [c_void_p, c_void_p, i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "avr_rays_sample_coarse": [c_void_p, c_void_p, c_void_p, i64, i64, i64, i64, c_float, c_float, c_int, c_void_p,
+                               u64, u64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_composite_bwd": [c_void_p, c_void_p, i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p],
     "avr_sample_coarse_rays": [c_void_p, c_void_p, i64, c_int, c_void_p, u64, u64, c_void_p, c_void_p],

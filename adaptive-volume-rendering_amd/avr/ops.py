@@ -38,6 +38,59 @@ def world_rays(x_pix, intrinsics, cam2world):
     return ro, rd, (c2w, sb_stride, ray_stride)
 
 
+def _c2w_view(cam2world):
+    c2w = cam2world.to(F32)
+    if c2w.dim() == 3:
+        c2w = c2w.unsqueeze(1)
+    if c2w.stride(-1) != 1 or c2w.stride(-2) != 4:
+        c2w = c2w.contiguous()
+    sb_stride = c2w.stride(0) if c2w.shape[0] > 1 else 0
+    ray_stride = c2w.stride(1) if c2w.shape[1] > 1 else 0
+    return c2w, sb_stride, ray_stride
+
+
+def rays_sample_coarse(x_pix, intrinsics, cam2world, near, far, n_samples, noise=None, seed=0, offset=0,
+                       ray_ids=None, want_depth_row=False):
+    """get_world_rays + sample_coarse in one launch (avr_rays_sample_coarse):
+    -> ro, rd (SB, R, 3), z (SB*R, n_samples), depth_row (SB*R, 4) fp64 or None,
+    c2w_info. Bit-identical to world_rays followed by sample_coarse."""
+    SB, R, _ = x_pix.shape
+    x_pix = _f32c(x_pix)
+    K = _f32c(intrinsics.reshape(SB, 3, 3))
+    c2w, sb_stride, ray_stride = _c2w_view(cam2world)
+    require_device(x_pix, K)
+    dev = x_pix.device
+    ro = torch.empty(SB, R, 3, device=dev, dtype=F32)
+    rd = torch.empty_like(ro)
+    z = torch.empty(SB * R, n_samples, device=dev, dtype=F32)
+    drow = torch.empty(SB * R, 4, device=dev, dtype=torch.float64) if want_depth_row else None
+    if noise is not None:
+        noise = _f32c(noise.reshape(SB * R, n_samples))
+        require_device(noise)
+    ray_ids = _ray_ids(ray_ids, SB * R)
+    call("avr_rays_sample_coarse", ptr(x_pix), ptr(K), ptr(c2w), sb_stride, ray_stride, SB, R, float(near), float(far),
+         n_samples, ptr(noise), seed, offset, ptr(ray_ids), ptr(ro), ptr(rd), ptr(drow), ptr(z), stream_of(x_pix))
+    return ro, rd, z, drow, (c2w, sb_stride, ray_stride)
+
+
+def composite_depth(z, field, ro, rd, depth_row, white_back=True, infinity=1.8, want_weights=False):
+    """volume_integral + depth_from_world of the expected distance in one launch
+    (avr_composite_fwd_depth; no autograd) -> rgb (R,3), dist (R,), weights or
+    None, depth (R,)."""
+    R, N = z.shape
+    z = _f32c(z)
+    field = _f32c(field.reshape(R, N, 4))
+    ro, rd = _f32c(ro.reshape(R, 3)), _f32c(rd.reshape(R, 3))
+    require_device(z, field, ro, rd, depth_row)
+    rgb = torch.empty(R, 3, device=z.device, dtype=F32)
+    dist = torch.empty(R, device=z.device, dtype=F32)
+    depth = torch.empty(R, device=z.device, dtype=F32)
+    w = torch.empty(R, N, device=z.device, dtype=F32) if want_weights else None
+    call("avr_composite_fwd_depth", ptr(z), ptr(field), R, N, int(bool(white_back)), float(infinity), ptr(ro),
+         ptr(rd), ptr(depth_row), ptr(rgb), ptr(dist), ptr(w), ptr(depth), stream_of(z))
+    return rgb, dist, w, depth
+
+
 def depth_from_world_fwd(ro, rd, dist, c2w_info, want_grad=False):
     c2w, sb_stride, ray_stride = c2w_info
     SB, R, _ = ro.shape

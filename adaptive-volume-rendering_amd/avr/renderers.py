@@ -184,9 +184,11 @@ class VolumeRenderer(nn.Module):
         if self.seed is not None:
             self._offset += SB * (R if ray_ids is None else int(n_rays_total))
 
-        ro, rd, c2w_info = ops.world_rays(x_pix, intrinsics, cam2world)
-        zc = ops.sample_coarse(near, far, SB * R, Nc, dev, noise=None if draws is None else draws["coarse"],
-                               seed=seed, offset=off, ray_ids=ids)
+        # without autograd or termination, depth comes from the fine composite's epilogue (fp64 depth rows)
+        fast_depth = not torch.is_grad_enabled() and self.t_stop is None
+        ro, rd, zc, depth_row, c2w_info = ops.rays_sample_coarse(
+            x_pix, intrinsics, cam2world, near, far, Nc, noise=None if draws is None else draws["coarse"], seed=seed,
+            offset=off, ray_ids=ids, want_depth_row=fast_depth)
 
         fuse = hasattr(radiance_field, "can_fuse") and radiance_field.can_fuse(x_pix)
         self.last_path = "fused" if fuse else "module"
@@ -213,9 +215,13 @@ class VolumeRenderer(nn.Module):
             rgb_f, dist_f = self._fine_early_termination(ro, rd, z_sorted, radiance_field, fuse, SB, R)
         else:
             ff = field(z_sorted, False)
-            # the fine weights are not returned (renderers.py:264-277): no store without autograd
-            rgb_f, dist_f, _ = ops.composite(z_sorted, ff, self.white_back, want_weights=False)
             self.last_fine_samples = z_sorted.numel()
+            if fast_depth:
+                # the fine weights are not returned (renderers.py:264-277): no store without autograd
+                rgb_f, dist_f, _, depth = ops.composite_depth(z_sorted, ff, ro, rd, depth_row, self.white_back)
+                depth = depth.reshape(SB, R)
+                return rgb_c.reshape(SB, R, 3), rgb_f.reshape(SB, R, 3), depth, depth
+            rgb_f, dist_f, _ = ops.composite(z_sorted, ff, self.white_back, want_weights=False)
         depth = ops.depth_from_world(ro, rd, dist_f.reshape(SB, R), c2w_info)
         assert z_sorted.shape[-1] == Nt
         return rgb_c.reshape(SB, R, 3), rgb_f.reshape(SB, R, 3), depth, depth

@@ -29,13 +29,56 @@ __device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b)
 __device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
 __device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
 
+// Gauss-Jordan inverse with partial pivoting in fp64 (torch.inverse is an LU
+// solve; fp64 here keeps the fp32-rounded results at the oracle's values).
+template <int N>
+__device__ __forceinline__ void invert(double (&a)[N][N], double (&inv)[N][N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) inv[i][j] = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+  for (int c = 0; c < N; ++c) {
+    int p = c;
+    double best = fabs(a[c][c]);
+#pragma unroll
+    for (int r = c + 1; r < N; ++r) {
+      const double v = fabs(a[r][c]);
+      if (v > best) { best = v; p = r; }
+    }
+#pragma unroll
+    for (int r = c + 1; r < N; ++r) {  // swap rows c and p (branch-free on the unrolled index)
+      if (r == p) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          double t = a[c][j]; a[c][j] = a[r][j]; a[r][j] = t;
+          t = inv[c][j]; inv[c][j] = inv[r][j]; inv[r][j] = t;
+        }
+      }
+    }
+    const double d = 1.0 / a[c][c];
+#pragma unroll
+    for (int j = 0; j < N; ++j) { a[c][j] *= d; inv[c][j] *= d; }
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      if (r == c) continue;
+      const double f = a[r][c];
+#pragma unroll
+      for (int j = 0; j < N; ++j) { a[r][j] -= f * a[c][j]; inv[r][j] -= f * inv[c][j]; }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ Philox4x32-10
 // Counter-based RNG for in-kernel noise (no noise bytes read from HBM).
 __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    // one v_mad_u64_u32 per product gives both halves (32-bit integer multiplies are
+    // the slow part of the generator; separate mul_lo / mul_hi would double them)
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
     k.x += 0x9E3779B9u;
     k.y += 0xBB67AE85u;
@@ -58,6 +101,45 @@ __device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t ray, uin
     case 1: return v.y;
     case 2: return v.z;
     default: return v.w;
+  }
+}
+
+// x / n for the sampling formulas: an exact power-of-two n makes the division an
+// exact scaling, i.e. bit-identical to x * (1/n) (also for subnormal results).
+// POW2 is a template argument of the kernels so the IEEE division is not even
+// emitted on the power-of-two path (a runtime select would compute both).
+template <bool POW2>
+__device__ __forceinline__ float div_count(float x, float n, float inv_n) {
+  if constexpr (POW2) return x * inv_n;
+  else return fdiv(x, n);
+}
+
+// The value of lane l ^ J (J a power of two < 64) without LDS traffic: DPP
+// quad permutes for 1 and 2, row shifts for 4 and 8, gfx950's
+// v_permlane16/32_swap for 16 and 32 (unlike __shfl_xor's ds_bpermute).
+__device__ __forceinline__ float lane_xor(float v, int J, int lane) {
+  const int b = __float_as_int(v);
+  switch (J) {
+    case 1: return __int_as_float(__builtin_amdgcn_update_dpp(b, b, 0xB1, 0xf, 0xf, false));
+    case 2: return __int_as_float(__builtin_amdgcn_update_dpp(b, b, 0x4E, 0xf, 0xf, false));
+    case 4: {
+      const int up = __builtin_amdgcn_update_dpp(b, b, 0x104, 0xf, 0xf, false);   // row_shl:4 (lane + 4)
+      const int dn = __builtin_amdgcn_update_dpp(b, b, 0x114, 0xf, 0xf, false);   // row_shr:4 (lane - 4)
+      return __int_as_float((lane & 4) ? dn : up);
+    }
+    case 8: {
+      const int up = __builtin_amdgcn_update_dpp(b, b, 0x108, 0xf, 0xf, false);
+      const int dn = __builtin_amdgcn_update_dpp(b, b, 0x118, 0xf, 0xf, false);
+      return __int_as_float((lane & 8) ? dn : up);
+    }
+    case 16: {
+      const auto r = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+      return __uint_as_float((lane & 16) ? r[0] : r[1]);
+    }
+    default: {
+      const auto r = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+      return __uint_as_float((lane & 32) ? r[0] : r[1]);
+    }
   }
 }
 

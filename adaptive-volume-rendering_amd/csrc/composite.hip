@@ -68,7 +68,11 @@ template <int K>
 __global__ void __launch_bounds__(256) composite_fwd_kernel(const float* __restrict__ z,
                                                             const float4* __restrict__ field, int64_t n_rays, int N,
                                                             int white_back, float infinity, float* __restrict__ rgb,
-                                                            float* __restrict__ dist, float* __restrict__ w_out) {
+                                                            float* __restrict__ dist, float* __restrict__ w_out,
+                                                            const float* __restrict__ ro,
+                                                            const float* __restrict__ rd,
+                                                            const double* __restrict__ depth_row,
+                                                            float* __restrict__ depth) {
   extern __shared__ float smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t ray = (int64_t)blockIdx.x * kCompWaves + wid;
@@ -78,6 +82,14 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(const float* __restr
   const float* zr = z + ray * N;
   const float4* fr = field + ray * N;
   const int n0 = K * lane;
+  // depth epilogue inputs, loaded up front so their latency hides under the ray's work
+  double4 drow = make_double4(0.0, 0.0, 0.0, 0.0);
+  float o3[3] = {0.f, 0.f, 0.f}, d3[3] = {0.f, 0.f, 0.f};
+  if (depth && lane == 0) {
+    drow = reinterpret_cast<const double4*>(depth_row)[ray];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) { o3[q] = ro[3 * ray + q]; d3[q] = rd[3 * ray + q]; }
+  }
   float4 f[K];
   float zv[K + 1];
 #pragma unroll
@@ -138,7 +150,15 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(const float* __restr
     rgb[3 * ray] = cr;
     rgb[3 * ray + 1] = cg;
     rgb[3 * ray + 2] = cb;
-    dist[ray] = (float)dd;
+    const float dist_f = (float)dd;
+    dist[ray] = dist_f;
+    if (depth) {   // depth_from_world(ro + rd * dist, cam2world), utils.py:358-361, as depth_kernel computes it
+      double zc = drow.w;
+      zc += drow.x * (double)fadd(o3[0], fmul(d3[0], dist_f));
+      zc += drow.y * (double)fadd(o3[1], fmul(d3[1], dist_f));
+      zc += drow.z * (double)fadd(o3[2], fmul(d3[2], dist_f));
+      depth[ray] = (float)(-zc);
+    }
   }
 }
 
@@ -226,11 +246,13 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(const float* __restr
 
 using namespace avr;
 
-extern "C" int avr_composite_fwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
-                                 float infinity, float* rgb, float* dist, float* weights, void* stream) {
+static int composite_fwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
+                         float infinity, float* rgb, float* dist, float* weights, const float* ro, const float* rd,
+                         const double* depth_row, float* depth, void* stream) {
   AVR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples <= 1024, "avr_composite_fwd: n_samples must be in [1,1024]");
   if (n_rays == 0) return AVR_OK;
   AVR_REQUIRE(z && field && rgb && dist, "avr_composite_fwd: null pointer");
+  AVR_REQUIRE(!depth || (ro && rd && depth_row), "avr_composite_fwd_depth: null ro / rd / depth_row");
   const size_t shm = (size_t)kCompWaves * (n_samples + 64) * sizeof(float);
   const unsigned grid = (unsigned)((n_rays + kCompWaves - 1) / kCompWaves);
   const float4* f4 = reinterpret_cast<const float4*>(field);
@@ -238,7 +260,7 @@ extern "C" int avr_composite_fwd(const float* z, const float* field, int64_t n_r
 #define AVR_COMP_K(KK)                                                                                          \
   case KK:                                                                                                      \
     composite_fwd_kernel<KK><<<grid, 64 * kCompWaves, shm, st>>>(z, f4, n_rays, n_samples, white_back, infinity, \
-                                                                 rgb, dist, weights);                           \
+                                                                 rgb, dist, weights, ro, rd, depth_row, depth); \
     break;
   switch ((n_samples + 63) / 64) {
     AVR_COMP_K(1) AVR_COMP_K(2) AVR_COMP_K(3) AVR_COMP_K(4) AVR_COMP_K(5) AVR_COMP_K(6) AVR_COMP_K(7) AVR_COMP_K(8)
@@ -247,6 +269,21 @@ extern "C" int avr_composite_fwd(const float* z, const float* field, int64_t n_r
   }
 #undef AVR_COMP_K
   return check_launch("composite_fwd_kernel");
+}
+
+extern "C" int avr_composite_fwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
+                                 float infinity, float* rgb, float* dist, float* weights, void* stream) {
+  return composite_fwd(z, field, n_rays, n_samples, white_back, infinity, rgb, dist, weights, nullptr, nullptr,
+                       nullptr, nullptr, stream);
+}
+
+extern "C" int avr_composite_fwd_depth(const float* z, const float* field, int64_t n_rays, int n_samples,
+                                       int white_back, float infinity, const float* ro, const float* rd,
+                                       const double* depth_row, float* rgb, float* dist, float* weights, float* depth,
+                                       void* stream) {
+  AVR_REQUIRE(n_rays == 0 || depth, "avr_composite_fwd_depth: null depth");
+  return composite_fwd(z, field, n_rays, n_samples, white_back, infinity, rgb, dist, weights, ro, rd, depth_row,
+                       depth, stream);
 }
 
 extern "C" int avr_composite_bwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,

@@ -5,46 +5,6 @@
 
 namespace avr {
 
-// Gauss-Jordan inverse with partial pivoting in fp64 (torch.inverse is an LU
-// solve; fp64 here keeps the fp32-rounded results at the oracle's values).
-template <int N>
-__device__ __forceinline__ void invert(double (&a)[N][N], double (&inv)[N][N]) {
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int j = 0; j < N; ++j) inv[i][j] = (i == j) ? 1.0 : 0.0;
-#pragma unroll
-  for (int c = 0; c < N; ++c) {
-    int p = c;
-    double best = fabs(a[c][c]);
-#pragma unroll
-    for (int r = c + 1; r < N; ++r) {
-      const double v = fabs(a[r][c]);
-      if (v > best) { best = v; p = r; }
-    }
-#pragma unroll
-    for (int r = c + 1; r < N; ++r) {  // swap rows c and p (branch-free on the unrolled index)
-      if (r == p) {
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-          double t = a[c][j]; a[c][j] = a[r][j]; a[r][j] = t;
-          t = inv[c][j]; inv[c][j] = inv[r][j]; inv[r][j] = t;
-        }
-      }
-    }
-    const double d = 1.0 / a[c][c];
-#pragma unroll
-    for (int j = 0; j < N; ++j) { a[c][j] *= d; inv[c][j] *= d; }
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-      if (r == c) continue;
-      const double f = a[r][c];
-#pragma unroll
-      for (int j = 0; j < N; ++j) { a[r][j] -= f * a[c][j]; inv[r][j] -= f * inv[c][j]; }
-    }
-  }
-}
-
 __global__ void __launch_bounds__(256) world_rays_kernel(const float* __restrict__ x_pix,
                                                          const float* __restrict__ K,
                                                          const float* __restrict__ c2w, int64_t sb_stride,

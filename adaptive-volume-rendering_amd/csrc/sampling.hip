@@ -15,14 +15,17 @@
 
 namespace avr {
 
-constexpr uint32_t kStreamCoarse = 0x1001u, kStreamU = 0x2002u, kStreamU2 = 0x3003u, kStreamDepth = 0x4004u;
+// Philox streams: coarse noise; the fine pass's (u, u2) pair (one block per fine
+// sample: u = .x, u2 = .y); the depth samples' normals.
+constexpr uint32_t kStreamCoarse = 0x1001u, kStreamFine = 0x2002u, kStreamDepth = 0x4004u;
 
 // Four consecutive samples per thread: one Philox4x32 block gives all four
 // uniforms (the same values philox_uniform draws one at a time), one 16-B store.
-__device__ __forceinline__ float coarse_z(float near_, float span, int s, int n, float u) {
+template <bool POW2>
+__device__ __forceinline__ float coarse_z(float near_, float span, int s, int n, float u, float inv_n) {
   // z = (near + span*step) + (u*span)/n   (two separate einsums, renderers.py:13-14)
-  const float step = fdiv((float)s, (float)n);
-  return fadd(fadd(near_, fmul(span, step)), fdiv(fmul(u, span), (float)n));
+  const float step = div_count<POW2>((float)s, (float)n, inv_n);
+  return fadd(fadd(near_, fmul(span, step)), div_count<POW2>(fmul(u, span), (float)n, inv_n));
 }
 
 // near + span * (s / n) depends on s only: each workgroup tabulates it once in
@@ -30,6 +33,7 @@ __device__ __forceinline__ float coarse_z(float near_, float span, int s, int n,
 // one IEEE division. 32-bit index arithmetic when the sample count allows.
 constexpr int kCoarseTab = 1024;
 
+template <bool POW2>
 __global__ void __launch_bounds__(256) sample_coarse_kernel(float near_, float far_, int64_t n_rays, int n,
                                                             const float* __restrict__ noise, uint64_t seed,
                                                             uint64_t offset, const int64_t* __restrict__ ray_ids,
@@ -38,8 +42,10 @@ __global__ void __launch_bounds__(256) sample_coarse_kernel(float near_, float f
   const int nq = (n + 3) >> 2;                           // 4-sample blocks per ray
   const float span = fsub(far_, near_);
   const bool tab = n <= kCoarseTab;
+  const float inv_n = 1.0f / (float)n;                   // exact when POW2 (the only case it is used)
   if (tab)
-    for (int s = threadIdx.x; s < n; s += blockDim.x) base_tab[s] = fadd(near_, fmul(span, fdiv((float)s, (float)n)));
+    for (int s = threadIdx.x; s < n; s += blockDim.x)
+      base_tab[s] = fadd(near_, fmul(span, div_count<POW2>((float)s, (float)n, inv_n)));
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = n_rays * nq;
@@ -67,7 +73,8 @@ __global__ void __launch_bounds__(256) sample_coarse_kernel(float near_, float f
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int s = 4 * q + k;
-    o[k] = tab ? fadd(base_tab[s < n ? s : 0], fdiv(fmul(u[k], span), (float)n)) : coarse_z(near_, span, s, n, u[k]);
+    o[k] = tab ? fadd(base_tab[s < n ? s : 0], div_count<POW2>(fmul(u[k], span), (float)n, inv_n))
+               : coarse_z<POW2>(near_, span, s, n, u[k], inv_n);
   }
   float* zr = z + r * n + 4 * q;
   if ((n & 3) == 0) {
@@ -92,9 +99,102 @@ __global__ void __launch_bounds__(256) sample_coarse_rays_kernel(const float* __
   const int s = (int)(i - r * n);
   const float nr = near_[r];
   const float span = fsub(far_[r], nr);
-  const float step = fdiv((float)s, (float)n);
   const float u = noise ? noise[i] : philox_uniform(seed, offset + (uint64_t)r, (uint32_t)s, kStreamCoarse);
-  z[i] = fadd(fadd(nr, fmul(span, step)), fdiv(fmul(u, span), (float)n));
+  z[i] = coarse_z<false>(nr, span, s, n, u, 0.f);
+}
+
+// get_world_rays (utils.py:315-336) + sample_coarse (renderers.py:4-24) in one
+// launch, plus each ray's depth row for the composite epilogue. A workgroup
+// owns kRaysPerBlock consecutive rays: first one thread per ray builds ro, rd
+// (and, if asked, row 2 of inverse(cam2world) in fp64: depth = -(row . [x, 1]),
+// utils.py:358-361), then the workgroup writes the rays' z in 4-sample quads,
+// consecutive threads on consecutive quads (coalesced 16-B stores).
+constexpr int kRaysPerBlock = 64;
+
+template <bool POW2>
+__global__ void __launch_bounds__(256) rays_coarse_kernel(
+    const float* __restrict__ x_pix, const float* __restrict__ K, const float* __restrict__ c2w, int64_t sb_stride,
+    int64_t ray_stride, int64_t n_sb, int64_t n_rays, float near_, float far_, int n, const float* __restrict__ noise,
+    uint64_t seed, uint64_t offset, const int64_t* __restrict__ ray_ids, float* __restrict__ ro,
+    float* __restrict__ rd, double* __restrict__ depth_row, float* __restrict__ z) {
+  __shared__ float base_tab[kCoarseTab];
+  const int64_t total = n_sb * n_rays;
+  const int64_t r0 = (int64_t)blockIdx.x * kRaysPerBlock;
+  const float span = fsub(far_, near_);
+  const float inv_n = 1.0f / (float)n;
+  const bool tab = n <= kCoarseTab;
+  if (tab)
+    for (int s = threadIdx.x; s < n; s += blockDim.x)
+      base_tab[s] = fadd(near_, fmul(span, div_count<POW2>((float)s, (float)n, inv_n)));
+  if (threadIdx.x < kRaysPerBlock && r0 + threadIdx.x < total) {
+    const int64_t i = r0 + threadIdx.x;
+    const int64_t sb = i / n_rays, r = i - sb * n_rays;
+    double k[3][3], ki[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) k[a][b] = (double)K[sb * 9 + a * 3 + b];
+    invert<3>(k, ki);
+    const double hx = x_pix[2 * i], hy = x_pix[2 * i + 1];
+    float cam[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const double kf0 = (double)(float)ki[a][0], kf1 = (double)(float)ki[a][1], kf2 = (double)(float)ki[a][2];
+      cam[a] = (float)(kf0 * hx + kf1 * hy + kf2);
+    }
+    cam[0] = (-cam[0]) * -1.0f;   // unproject: x negated, then scaled by z = -1 (utils.py:262-265)
+    cam[1] = cam[1] * -1.0f;
+    cam[2] = cam[2] * -1.0f;
+    const float nrm = (float)sqrt((double)cam[0] * cam[0] + (double)cam[1] * cam[1] + (double)cam[2] * cam[2]);
+    const float d0 = fdiv(cam[0], nrm), d1 = fdiv(cam[1], nrm), d2 = fdiv(cam[2], nrm);
+    const float* T = c2w + sb * sb_stride + r * ray_stride;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      rd[3 * i + a] = (float)((double)T[4 * a] * d0 + (double)T[4 * a + 1] * d1 + (double)T[4 * a + 2] * d2);
+      ro[3 * i + a] = T[4 * a + 3];
+    }
+    if (depth_row) {
+      double m[4][4], inv[4][4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[p][q] = (double)T[4 * p + q];
+      invert<4>(m, inv);
+      reinterpret_cast<double4*>(depth_row)[i] = make_double4(inv[2][0], inv[2][1], inv[2][2], inv[2][3]);
+    }
+  }
+  __syncthreads();   // base_tab
+  const int nq = (n + 3) >> 2;
+  const int64_t nr_blk = total - r0 < kRaysPerBlock ? total - r0 : kRaysPerBlock;
+  const int items = (int)nr_blk * nq;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int rl = it / nq, q = it - rl * nq;
+    const int64_t ray = r0 + rl;
+    float u[4];
+    if (noise) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[k] = 4 * q + k < n ? noise[ray * n + 4 * q + k] : 0.f;
+    } else {
+      const uint64_t key = offset + (uint64_t)(ray_ids ? ray_ids[ray] : ray);
+      const float4 v = philox_uniform4(seed, key, (uint32_t)q, kStreamCoarse);
+      u[0] = v.x; u[1] = v.y; u[2] = v.z; u[3] = v.w;
+    }
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int s = 4 * q + k;
+      o[k] = tab ? fadd(base_tab[s < n ? s : 0], div_count<POW2>(fmul(u[k], span), (float)n, inv_n))
+                 : coarse_z<POW2>(near_, span, s, n, u[k], inv_n);
+    }
+    float* zr = z + ray * n + 4 * q;
+    if ((n & 3) == 0) {
+      *reinterpret_cast<float4*>(zr) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (4 * q + k < n) zr[k] = o[k];
+    }
+  }
 }
 
 // torch-CPU fp32 row sum (ATen vectorised reduction): four 8-lane accumulators
@@ -156,13 +256,14 @@ __device__ __forceinline__ int count_below(const float* L, int n, float x) {
   return lo;
 }
 
-// Ascending bitonic sort of one float per lane across the wave (64 values).
+// Ascending bitonic sort of one float per lane across the wave (64 values);
+// partners through lane_xor (DPP / permlane swaps, no LDS round trips).
 __device__ __forceinline__ float wave_sort64(float v, int lane) {
 #pragma unroll
   for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      const float o = __shfl_xor(v, j, 64);
+      const float o = lane_xor(v, j, lane);
       const bool up = (lane & k) == 0, lower = (lane & j) == 0;
       v = (lower == up) ? fminf(v, o) : fmaxf(v, o);
     }
@@ -170,24 +271,41 @@ __device__ __forceinline__ float wave_sort64(float v, int lane) {
   return v;
 }
 
+// count_below over the sorted list L[0..n) starting from a guess g of the
+// answer: when L[g-2] and L[g+2] bracket x (checked), a 2-step search of the
+// window; otherwise the full binary search. Exact either way.
+template <bool LT>
+__device__ __forceinline__ int count_below_near(const float* L, int n, float x, int g) {
+  const int lo = g - 2 < 0 ? 0 : (g - 2 > n ? n : g - 2);
+  const int hi = g + 2 > n ? n : (g + 2 < lo ? lo : g + 2);
+  const bool below_lo = lo == 0 || (LT ? L[lo - 1] < x : L[lo - 1] <= x);   // every index < lo counts
+  const bool above_hi = hi == n || !(LT ? L[hi] < x : L[hi] <= x);          // no index >= hi counts
+  if (below_lo && above_hi) return lo + count_below<LT>(L + lo, hi - lo, x);
+  return count_below<LT>(L, n, x);
+}
+
+constexpr int kMaxK = kMaxCoarse / 64;   // coarse samples per lane
+
 // One wave per ray; no block barriers (each wave owns its LDS slice).
 //   1) w' = w + 1e-5, s = torch-CPU cascade sum (bit-exact);
-//   2) pdf = w'/s (IEEE), cdf = [0, fp64 prefix sum]: lane l sums its K
-//      consecutive entries sequentially, one DPP exclusive scan joins the lanes
-//      (these fp64 partial sums of fp32 terms are exact: order cannot change a bit);
+//   2) pdf = w'/s (IEEE, once per entry), cdf = [0, fp64 prefix sum]: lane l
+//      sums its K consecutive entries sequentially, one DPP exclusive scan
+//      joins the lanes (these fp64 partial sums of fp32 terms are exact:
+//      order cannot change a bit);
 //   3) idx = #{cdf <= u} - 1 (binary search), z = near + (far-near)*((idx+u2)/Nc);
 //   4) depth samples clamp(randn * std, near, far) (quirk Q6);
 //   5) values-only sort of [z_coarse | z_fine | z_depth]: when z_coarse is
 //      ascending (stratified: always, barring fp32 ties) and Nf, Nd <= 64, the
 //      fine and depth lists are sorted in registers and the three sorted lists
 //      merged by rank (own index + counts below in the other lists, ties broken
-//      coarse < fine < depth); otherwise a wave-local bitonic sort.
+//      coarse < fine < depth; a fine value's count in the coarse list starts
+//      from its stratified bin); otherwise a wave-local bitonic sort.
+template <bool POW2>
 __global__ void __launch_bounds__(256) sample_fine_kernel(
     const float* __restrict__ weights, const float* __restrict__ z_coarse, float near_, float far_, int64_t n_rays,
     int Nc, int Nf, int Nd, float depth_std, const float* __restrict__ u_in, const float* __restrict__ u2_in,
     const float* __restrict__ nd_in, uint64_t seed, uint64_t offset, const int64_t* __restrict__ ray_ids, int sort_n,
-    float* __restrict__ z_sorted,
-    int32_t* __restrict__ idx_out, float* __restrict__ z_fine_out) {
+    float* __restrict__ z_sorted, int32_t* __restrict__ idx_out, float* __restrict__ z_fine_out) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t ray = (int64_t)blockIdx.x * kFineWaves + wid;
@@ -199,6 +317,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
   float* obuf = sbuf + sort_n;
   const float span = fsub(far_, near_);
   const uint64_t key = offset + (uint64_t)(ray_ids ? ray_ids[ray] : ray);   // Philox counter of this ray
+  const float inv_nc = 1.0f / (float)Nc;
 
   // 1) + 2)
   const float* w = weights + ray * Nc;
@@ -214,14 +333,19 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
   const float s = cascade_sum_wave(cdf + 1, Nc, lane, scratch);
   {
     const int K = (Nc + 63) >> 6, k0 = K * lane;
+    float pv[kMaxK];
     double part = 0.0;
-    for (int k = 0; k < K; ++k)
-      if (k0 + k < Nc) part += (double)fdiv(cdf[1 + k0 + k], s);
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) {
+      pv[k] = (k < K && k0 + k < Nc) ? fdiv(cdf[1 + k0 + k], s) : 0.f;
+      part += (double)pv[k];
+    }
     double run = wave_excl_sum_dpp(part);
     wave_sync();   // every pdf read before any cdf write
-    for (int k = 0; k < K; ++k)
-      if (k0 + k < Nc) {
-        run += (double)fdiv(cdf[1 + k0 + k], s);
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k)
+      if (k < K && k0 + k < Nc) {
+        run += (double)pv[k];
         cdf[1 + k0 + k] = (float)run;
       }
     if (lane == 0) cdf[0] = 0.f;
@@ -231,11 +355,18 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
   // 3) importance samples
   float zf_mine = FLT_MAX;
   for (int f = lane; f < Nf; f += 64) {
-    const float u = u_in ? u_in[ray * Nf + f] : philox_uniform(seed, key, f, kStreamU);
-    const float u2 = u2_in ? u2_in[ray * Nf + f] : philox_uniform(seed, key, f, kStreamU2);
+    float u, u2;
+    if (u_in) {
+      u = u_in[ray * Nf + f];
+      u2 = u2_in[ray * Nf + f];
+    } else {
+      const float4 v = philox_uniform4(seed, key, (uint32_t)f, kStreamFine);
+      u = v.x;
+      u2 = v.y;
+    }
     const int cnt = count_below<false>(cdf, Nc + 1, u);   // #{cdf <= u}
     const int idx = cnt > 0 ? cnt - 1 : 0;
-    const float steps = fdiv(fadd((float)idx, u2), (float)Nc);
+    const float steps = div_count<POW2>(fadd((float)idx, u2), (float)Nc, inv_nc);
     const float zf = fadd(near_, fmul(span, steps));
     if (idx_out) idx_out[ray * Nf + f] = idx;
     if (z_fine_out) z_fine_out[ray * Nf + f] = zf;
@@ -267,7 +398,12 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
       const float x = A[k];
       obuf[k + count_below<true>(B, Nf, x) + count_below<true>(D, Nd, x)] = x;
     }
-    if (lane < Nf) obuf[lane + count_below<false>(A, Nc, bf) + count_below<true>(D, Nd, bf)] = bf;
+    if (lane < Nf) {
+      // stratified coarse lists put #{A <= bf} within a step of bf's bin
+      const float t = fmul(fsub(bf, near_), (float)Nc / span);
+      const int g = t > 0.f ? (t < (float)Nc ? (int)t : Nc) : 0;
+      obuf[lane + count_below_near<false>(A, Nc, bf, g) + count_below<true>(D, Nd, bf)] = bf;
+    }
     if (lane < Nd) obuf[lane + count_below<false>(A, Nc, bd) + count_below<false>(B, Nf, bd)] = bd;
     wave_sync();
     for (int k = lane; k < Ntot; k += 64) out[k] = obuf[k];
@@ -301,10 +437,32 @@ extern "C" int avr_sample_coarse(float near_, float far_, int64_t n_rays, int n_
   if (n == 0) return AVR_OK;
   AVR_REQUIRE(z, "avr_sample_coarse: null output");
   const int64_t threads = n_rays * ((n_samples + 3) / 4);
-  sample_coarse_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, as_stream(stream)>>>(near_, far_, n_rays,
-                                                                                       n_samples, noise, seed,
-                                                                                       offset, ray_ids, z);
+  const unsigned grid = (unsigned)((threads + 255) / 256);
+  if ((n_samples & (n_samples - 1)) == 0)
+    sample_coarse_kernel<true><<<grid, 256, 0, as_stream(stream)>>>(near_, far_, n_rays, n_samples, noise, seed,
+                                                                   offset, ray_ids, z);
+  else
+    sample_coarse_kernel<false><<<grid, 256, 0, as_stream(stream)>>>(near_, far_, n_rays, n_samples, noise, seed,
+                                                                    offset, ray_ids, z);
   return check_launch("sample_coarse_kernel");
+}
+
+extern "C" int avr_rays_sample_coarse(const float* x_pix, const float* K, const float* c2w, int64_t c2w_sb_stride,
+                                      int64_t c2w_ray_stride, int64_t n_sb, int64_t n_rays, float near_, float far_,
+                                      int n_samples, const float* noise, uint64_t seed, uint64_t offset,
+                                      const int64_t* ray_ids, float* ro, float* rd, double* depth_row, float* z,
+                                      void* stream) {
+  AVR_REQUIRE(n_sb >= 0 && n_rays >= 0 && n_samples > 0, "avr_rays_sample_coarse: bad sizes");
+  const int64_t total = n_sb * n_rays;
+  if (total == 0) return AVR_OK;
+  AVR_REQUIRE(x_pix && K && c2w && ro && rd && z, "avr_rays_sample_coarse: null pointer");
+  const int64_t blocks = (total + kRaysPerBlock - 1) / kRaysPerBlock;
+  AVR_REQUIRE(blocks < (1ll << 31), "avr_rays_sample_coarse: too many rays");
+  auto* kern = (n_samples & (n_samples - 1)) == 0 ? rays_coarse_kernel<true> : rays_coarse_kernel<false>;
+  kern<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(x_pix, K, c2w, c2w_sb_stride, c2w_ray_stride, n_sb, n_rays,
+                                                        near_, far_, n_samples, noise, seed, offset, ray_ids, ro, rd,
+                                                        depth_row, z);
+  return check_launch("rays_coarse_kernel");
 }
 
 extern "C" int avr_sample_coarse_rays(const float* near_, const float* far_, int64_t n_rays, int n_samples,
@@ -337,7 +495,8 @@ extern "C" int avr_sample_fine(const float* weights, const float* z_coarse, floa
   while (sort_n < ntot) sort_n <<= 1;
   const unsigned grid = (unsigned)((n_rays + kFineWaves - 1) / kFineWaves);
   const size_t shm = (size_t)kFineWaves * fine_wave_floats(n_coarse, sort_n, ntot) * sizeof(float);
-  sample_fine_kernel<<<grid, 64 * kFineWaves, shm, as_stream(stream)>>>(
+  auto* kern = (n_coarse & (n_coarse - 1)) == 0 ? sample_fine_kernel<true> : sample_fine_kernel<false>;
+  kern<<<grid, 64 * kFineWaves, shm, as_stream(stream)>>>(
       weights, z_coarse, near_, far_, n_rays, n_coarse, n_importance, n_depth, depth_std, u, u2, noise_depth, seed,
       offset, ray_ids, sort_n, z_sorted, idx, z_fine);
   return check_launch("sample_fine_kernel");

@@ -138,6 +138,16 @@ class HbmKernelTimer:
             w, zc = a[0], a[1]
             return w.numel() * 4 + zc.numel() * 4 + out[0].numel() * 4, f"Nc={zc.shape[1]}, out {out[0].shape[1]}"
 
+        def rays_coarse_bytes(a, k, out):
+            R, N = out[2].shape
+            return R * (8 + 24 + 4 * N + (32 if out[3] is not None else 0)), f"N={N}, depth rows"
+
+        def composite_depth_bytes(a, k, out):
+            R, N = a[0].shape
+            return R * (N * (4 + 16) + 16 + 24 + 32 + 4), f"N={N}, + depth"
+
+        self._wrap("rays_sample_coarse", "rays_coarse_kernel", rays_coarse_bytes)
+        self._wrap("composite_depth", "composite_fwd_kernel", composite_depth_bytes)
         self._wrap("world_rays", "world_rays_kernel", lambda a, k, out: (a[0].shape[0] * a[0].shape[1] * 32, ""))
         self._wrap("sample_coarse", "sample_coarse_kernel", lambda a, k, out: (out.numel() * 4, f"N={out.shape[1]}"))
         self._wrap("composite_fwd", "composite_fwd_kernel", composite_bytes)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 4
+#define AVR_ABI_VERSION 5
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -73,6 +73,18 @@ int avr_depth_from_world(const float* ro, const float* rd, const float* dist, co
 int avr_sample_coarse(float near_, float far_, int64_t n_rays, int n_samples, const float* noise,
                       uint64_t seed, uint64_t offset, const int64_t* ray_ids, float* z, void* stream);
 
+/* get_world_rays + sample_coarse in one launch (utils.py:315-336,
+ * renderers.py:4-24; the renderer's stage order): the inputs of
+ * avr_world_rays, then near / far / n_samples / noise / seed / offset /
+ * ray_ids of avr_sample_coarse -> ro, rd (n_sb, n_rays, 3), z (n_sb * n_rays,
+ * n_samples), and, if depth_row is not NULL, row 2 of inverse(cam2world) per
+ * ray in fp64 (n_sb * n_rays, 4 doubles) for avr_composite_fwd_depth.
+ * Outputs equal avr_world_rays + avr_sample_coarse bit for bit.               */
+int avr_rays_sample_coarse(const float* x_pix, const float* K, const float* c2w, int64_t c2w_sb_stride,
+                           int64_t c2w_ray_stride, int64_t n_sb, int64_t n_rays, float near_, float far_, int n_samples,
+                           const float* noise, uint64_t seed, uint64_t offset, const int64_t* ray_ids, float* ro,
+                           float* rd, double* depth_row, float* z, void* stream);
+
 /* sample_coarse with per-ray near/far (n_rays) — AdaptiveVolumeRenderer's band
  * around the raymarched distance (renderers.py:492-493).                        */
 int avr_sample_coarse_rays(const float* near_, const float* far_, int64_t n_rays, int n_samples,
@@ -102,6 +114,14 @@ int avr_sample_fine(const float* weights, const float* z_coarse, float near_, fl
  * N <= 1024.                                                                   */
 int avr_composite_fwd(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
                       float infinity, float* rgb, float* dist, float* weights, void* stream);
+
+/* avr_composite_fwd + depth_from_world(ro + rd * dist, cam2world) in the
+ * epilogue (renderers.py:274-275, utils.py:358-361) from the depth rows of
+ * avr_rays_sample_coarse: depth (n_rays), equal to avr_depth_from_world bit
+ * for bit. ro, rd (n_rays, 3).                                                 */
+int avr_composite_fwd_depth(const float* z, const float* field, int64_t n_rays, int n_samples, int white_back,
+                            float infinity, const float* ro, const float* rd, const double* depth_row, float* rgb,
+                            float* dist, float* weights, float* depth, void* stream);
 
 /* Gradient of volume_integral (autograd of renderers.py:78-112).
  *   grad_rgb (n_rays,3), grad_dist (n_rays) or NULL, grad_weights (n_rays,N)

@@ -423,3 +423,62 @@ def test_field_x3_tracks_fp32_at_scale(golden):
     d = (a - b).abs()
     assert float(d[:, :3].max()) < 2e-5, float(d[:, :3].max())
     assert float((d[:, 3] / a[:, 3].abs().clamp_min(1.0)).max()) < 1e-4
+
+
+# ----------------------------------------------------------------- fused stage kernels
+@pytest.mark.parametrize("n,noise,per_ray", [(128, False, False), (37, True, True), (192, False, True)])
+def test_rays_sample_coarse_equals_separate_kernels(n, noise, per_ray):
+    """avr_rays_sample_coarse (ray generation + stratified z + depth rows in one
+    launch) equals avr_world_rays + avr_sample_coarse bit for bit, and the
+    composite epilogue's depth equals avr_depth_from_world bit for bit."""
+    from avr import ops
+    from oracle import synth
+    SB, R = 2, 777
+    g = torch.Generator().manual_seed(n)
+    x_pix = torch.rand(SB, R, 2, generator=g).to(DEV)
+    K = T(np.stack([synth.default_intrinsics(), synth.default_intrinsics() * 1.1]).astype(np.float32))
+    K[1, 2, 2] = 1.0
+    if per_ray:
+        c2w = T(np.stack([synth.orbit_cam2world(0.1 + 0.01 * i) for i in range(SB * R)]).astype(np.float32))
+        c2w = c2w.reshape(SB, R, 4, 4)
+    else:
+        c2w = T(synth.orbit_cam2world(0.7)).reshape(1, 1, 4, 4).expand(SB, R, 4, 4)
+    nz = torch.rand(SB, R, n, generator=g).to(DEV) if noise else None
+    ids = torch.randperm(10 * SB * R, generator=g)[:SB * R].to(DEV)
+    with torch.no_grad():
+        ro, rd, info = ops.world_rays(x_pix, K, c2w)
+        z = ops.sample_coarse(0.8, 1.8, SB * R, n, DEV, noise=nz, seed=5, offset=3, ray_ids=ids)
+        ro2, rd2, z2, drow, _ = ops.rays_sample_coarse(x_pix, K, c2w, 0.8, 1.8, n, noise=nz, seed=5, offset=3,
+                                                       ray_ids=ids, want_depth_row=True)
+        assert torch.equal(ro, ro2) and torch.equal(rd, rd2) and torch.equal(z, z2)
+        field = torch.cat([torch.rand(SB * R, n, 3, device=DEV), 3 * torch.rand(SB * R, n, 1, device=DEV)], -1)
+        rgb, dist, w = ops.composite_fwd(z, field, True)
+        depth = ops.depth_from_world(ro, rd, dist.reshape(SB, R), info)
+        rgb2, dist2, w2, depth2 = ops.composite_depth(z, field, ro, rd, drow, True, want_weights=True)
+    assert torch.equal(rgb, rgb2) and torch.equal(dist, dist2) and torch.equal(w, w2)
+    assert torch.equal(depth.reshape(-1), depth2)
+
+
+def test_sample_fine_philox_pairs():
+    """In-kernel Philox for the fine pass (one block per fine sample: u, u2):
+    deterministic per (seed, ray id), uniform, independent of the batch
+    layout, and the merged output is the sorted union (numpy sort)."""
+    from avr import ops
+    R, Nc, Nf = 4096, 128, 64
+    w = torch.rand(R, Nc, device=DEV) ** 4
+    zc = ops.sample_coarse(0.8, 1.8, R, Nc, DEV, seed=1)
+    zs, idx, zf = ops.sample_fine(w, zc, 0.8, 1.8, Nf, 0, 0.0, seed=9, want_idx=True, want_fine=True)
+    zs2, idx2, zf2 = ops.sample_fine(w, zc, 0.8, 1.8, Nf, 0, 0.0, seed=9, want_idx=True, want_fine=True)
+    assert torch.equal(zs, zs2) and torch.equal(idx, idx2)
+    _, _, zf3 = ops.sample_fine(w, zc, 0.8, 1.8, Nf, 0, 0.0, seed=10, want_fine=True)
+    assert not torch.equal(zf, zf3)
+    # rays 100..199 alone, keyed by their ids, draw the same samples
+    ids = torch.arange(100, 200, device=DEV)
+    _, _, zf4 = ops.sample_fine(w[100:200].contiguous(), zc[100:200].contiguous(), 0.8, 1.8, Nf, 0, 0.0, seed=9,
+                                want_fine=True, ray_ids=ids)
+    assert torch.equal(zf4, zf[100:200])
+    ref = np.sort(np.concatenate([to_np(zc), to_np(zf)], -1), -1)
+    np.testing.assert_array_equal(to_np(zs), ref)
+    # u2 ~ U[0,1): the position of z_fine inside its coarse bin
+    frac = to_np(zf - 0.8) * Nc - to_np(idx).astype(np.float32)
+    assert frac.min() > -1e-3 and frac.max() < 1 + 1e-3 and abs(frac.mean() - 0.5) < 5e-3
