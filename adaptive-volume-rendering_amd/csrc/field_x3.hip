@@ -467,6 +467,60 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     AVR_STAMP(9 + 5 * (b & 3));
   }
 
+  if constexpr (TWO) {
+    // ---- lin_out(relu(h)) without publishing X: every wave multiplies its own 64
+    // features (its 2 K-chunks) into a partial 4 x 64 output under a wave-local split
+    // scale, the partials meet in LDS (the dead dedup area of the tail) and waves 0-3
+    // sum them in wave order for samples 16w + j.
+    const uint4* wo = P16 + L.x3_out / 4 + lane;
+    FragX3 Aw[2];
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) Aw[cc] = load_frag(wo + 2 * 64 * (2 * wid + cc));
+    const float f = 1.0f / S_h;
+    const float mxw = max_relu_affine<FT, false>(h, f, bz);
+    const float s_w = pow2_scale_for(mxw);
+    floatx4 part[4];
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      part[sg] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        uint2 h0, l0, h1, l1;
+        split4(relu_affine<false>(h[2 * cc][sg], f, bz[0]), s_w, h0, l0);
+        split4(relu_affine<false>(h[2 * cc + 1][sg], f, bz[0]), s_w, h1, l1);
+        const half8 bh = __builtin_bit_cast(half8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+        const half8 bl = __builtin_bit_cast(half8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+        part[sg] = mfma32h(Aw[cc].hi, bh, part[sg]);
+        part[sg] = mfma32h(Aw[cc].hi, bl, part[sg]);
+        part[sg] = mfma32h(Aw[cc].lo, bh, part[sg]);
+      }
+    }
+    const float un = 1.0f / (layer_scale(a.packed, L, 1) * s_w);
+    float4* pbuf = reinterpret_cast<float4*>(tail);   // [wave][sample] (r, g, b, sigma) partials: 8 KiB
+    if (g == 0) {
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        const floatx4 o = part[sg] * un;
+        pbuf[wid * 64 + 16 * sg + j] = make_float4(o.x, o.y, o.z, o.w);
+      }
+    }
+    lds_barrier();
+    AVR_STAMP(25);
+    if (wid >= 4) return;
+    const int s = 16 * wid + j;
+    const int64_t m = base + s;
+    if (g == 0 && m < a.M) {
+      float4 o = *reinterpret_cast<const float4*>(a.packed + L.b_out);
+#pragma unroll
+      for (int v = 0; v < NW; ++v) {
+        const float4 p = pbuf[v * 64 + s];
+        o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
+      }
+      AVR_STAMP(26);
+      a.out[roff + m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
+    }
+    return;
+  }
   // ---- lin_out(relu(h)): waves 0-3 compute the 16-row output tile for samples 16w + j.
   // (a quarter of lin_out's A fragments are loaded ahead of the publish, the rest after)
   FragX3 Ao[KC];
