@@ -10,7 +10,7 @@
 // The contraction runs over the ROW index of both operands, so the MFMA
 // operands are k-strided in memory: each workgroup stages 32-sample chunks of
 // its 128-column G and X slices in LDS as row-major fp16 hi/lo images
-// (XOR-swizzled 256-B rows) and reads the A and B fragments of
+// (padded 288-B rows) and reads the A and B fragments of
 // v_mfma_f32_16x16x32_f16 with gfx950's transposing ds_read_b64_tr_b16.
 // Products are W-split x3 (Gh.Xh + Gh.Xl + Gl.Xh, fp32 accumulate) under
 // per-layer power-of-two scales from the max |G| / |X| the producing kernels
@@ -27,7 +27,8 @@ namespace avr {
 constexpr int kDwTile = 256;                 // output tile (o x i) per workgroup
 constexpr int kDwWT = 8;                     // 16 x 16 MFMA tiles per wave and dimension (128 x 128 per wave)
 constexpr int kDwK = 32;
-constexpr int kDwHalf = kDwK * 256;          // bytes of one 128-column half image (32 rows x 256 B)
+constexpr int kDwRow = 256 + 32;             // bytes per row of a 128-column half image (padded: 9 x 32 B)
+constexpr int kDwHalf = kDwK * kDwRow;       // one 128-column half image (32 rows)
 constexpr int kDwImg = 2 * kDwHalf;          // one fp16 image of 256 columns
 constexpr int kDwStage = 4 * kDwImg;         // G hi, G lo, X hi, X lo
 
@@ -53,23 +54,29 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
 typedef __attribute__((address_space(3))) char lds_char;
 
-// byte offset of 16-B chunk ch (0..15) of row r in a 256-B-row image (XOR swizzle:
-// conflict-free transposed reads, cdna_hip_programming.md T10 image (b)); a
-// 256-column image is two such 128-column halves
-__device__ __forceinline__ int img_off(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
-__device__ __forceinline__ int img_off_col(int r, int col) { return kDwHalf * (col >> 7) + img_off(r, (col & 127) >> 3); }
+// byte offset of column col of row r in a 256-column image (two 128-column
+// halves of padded 288-B rows: 8 consecutive rows start in 8 different 32-B
+// bank groups, so the transposed reads below are conflict-free with no swizzle
+// and a fragment's address is affine in its column: one lane base + an immediate)
+__device__ __forceinline__ int img_off_col(int r, int col) { return kDwHalf * (col >> 7) + kDwRow * r + 2 * (col & 127); }
 
-// MFMA operand fragment of 16 columns col0 .. col0+15 of an image: lane l
-// (g = l >> 4, i = l & 15) gets column col0 + i, rows 8g .. 8g+7 (element j =
-// row 8g + j, the natural k order of v_mfma_f32_16x16x32_f16 for A and B).
-__device__ __forceinline__ half8 tr_frag(const lds_char* img_full, int col0_full, int lane) {
-  const lds_char* img = img_full + kDwHalf * (col0_full >> 7);
-  const int col0 = col0_full & 127;
+// Lane base of the transposed operand reads: lane l (g = l >> 4, i = l & 15,
+// q = i >> 2, p = i & 3) supplies row 4g + q, columns 4p .. 4p+3 of a 16-column
+// block; the second read takes row 16 + 4g + q.
+__device__ __forceinline__ int tr_base(int lane) {
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int ch = (col0 >> 3) + (p >> 1), sub = 8 * (p & 1);
+  return kDwRow * (4 * g + q) + 8 * p;
+}
+
+// MFMA operand fragment of 16 columns col0 .. col0+15 of an image (col0 a
+// compile-time multiple of 16 after unrolling): lane l gets column col0 + (l & 15),
+// K rows {4g .. 4g+3, 16+4g .. 16+4g+3} (g = l >> 4). The same K permutation on
+// both operands leaves every product sum unchanged.
+__device__ __forceinline__ half8 tr_frag(const lds_char* img_full, int col0_full, int base) {
+  const lds_char* img = img_full + kDwHalf * (col0_full >> 7) + 2 * (col0_full & 127) + base;
   typedef __attribute__((address_space(3))) short4_t lds_short4;
-  const short4_t r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(img + img_off(8 * g + q, ch) + sub));
-  const short4_t r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(img + img_off(8 * g + 4 + q, ch) + sub));
+  const short4_t r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)img);
+  const short4_t r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(img + 16 * kDwRow));
   const short4_t both[2] = {r0, r1};
   return __builtin_bit_cast(half8, both);
 }
@@ -126,6 +133,7 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
   };
 
   const int wo = wid >> 1, wi = wid & 1;
+  const int trb = tr_base(lane);
   floatx4 acc[kDwWT][kDwWT];
 #pragma unroll
   for (int t = 0; t < kDwWT; ++t)
@@ -135,7 +143,7 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
   // Row group u of chunk c (registers gv / xv) -> LDS stage c & 1, split into fp16 hi / lo.
   const auto put = [&](int c, const floatx4 (&gv)[NU], const floatx4 (&xv)[NU], int u) {
     lds_char* st = lds + (c & 1) * kDwStage;
-    const int r = rb + 4 * u, off = img_off_col(r, 4 * cc) + 8 * (cc & 1);
+    const int r = rb + 4 * u, off = img_off_col(r, 4 * cc);
     uint2 hi, lo;
     split4(gv[u], sG, hi, lo);
     *(lds_u32x2*)(st + off) = u32x2{hi.x, hi.y};
@@ -157,18 +165,18 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
     half8 bh[kDwWT], bl[kDwWT];
 #pragma unroll
     for (int u = 0; u < kDwWT; ++u) {
-      bh[u] = tr_frag(st + 2 * kDwImg, 128 * wi + 16 * u, lane);
-      bl[u] = tr_frag(st + 3 * kDwImg, 128 * wi + 16 * u, lane);
+      bh[u] = tr_frag(st + 2 * kDwImg, 128 * wi + 16 * u, trb);
+      bl[u] = tr_frag(st + 3 * kDwImg, 128 * wi + 16 * u, trb);
     }
     // A fragments one row tile ahead: row tile t + 1's transposed reads are in
     // flight while row tile t's 24 MFMAs issue
-    half8 ah = tr_frag(st, 128 * wo, lane), al = tr_frag(st + kDwImg, 128 * wo, lane);
+    half8 ah = tr_frag(st, 128 * wo, trb), al = tr_frag(st + kDwImg, 128 * wo, trb);
 #pragma unroll
     for (int t = 0; t < kDwWT; ++t) {
       half8 ahn = ah, aln = al;
       if (t + 1 < kDwWT) {
-        ahn = tr_frag(st, 128 * wo + 16 * (t + 1), lane);
-        aln = tr_frag(st + kDwImg, 128 * wo + 16 * (t + 1), lane);
+        ahn = tr_frag(st, 128 * wo + 16 * (t + 1), trb);
+        aln = tr_frag(st + kDwImg, 128 * wo + 16 * (t + 1), trb);
       }
 #pragma unroll
       for (int u = 0; u < kDwWT; ++u) {
