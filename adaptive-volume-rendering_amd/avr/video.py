@@ -23,20 +23,20 @@ def get_opencv_pixel_coordinates(y_resolution, x_resolution):
 
 
 def get_R(x, y, z):
-    """utils.py:464-479: look-at rotation (camera at (x, y, z), target origin,
-    up (0, 0, -1)), returned as (1, 3, 3) with the axes as columns."""
-    camera_position = torch.tensor([x, y, z], dtype=torch.float32).reshape(1, 3)
-    at = torch.zeros(1, 3)
-    up = torch.tensor([0.0, 0.0, -1.0]).reshape(1, 3)
-    z_axis = F.normalize(at - camera_position, eps=1e-5)
-    x_axis = F.normalize(torch.cross(up, z_axis, dim=1), eps=1e-5)
-    y_axis = F.normalize(torch.cross(z_axis, x_axis, dim=1), eps=1e-5)
-    is_close = torch.isclose(x_axis, torch.tensor(0.0), atol=5e-3).all(dim=1, keepdim=True)
-    if is_close.any():
-        replacement = F.normalize(torch.cross(y_axis, z_axis, dim=1), eps=1e-5)
-        x_axis = torch.where(is_close, replacement, x_axis)
-    R = torch.cat((x_axis[:, None, :], y_axis[:, None, :], z_axis[:, None, :]), dim=1)
-    return R.transpose(1, 2)
+    """Look-at rotation of a camera at (x, y, z) aimed at the origin, with the
+    scene's (0, 0, -1) reference direction (utils.py:464-479): (1, 3, 3) whose
+    columns are the camera's x, y and viewing axes. When the viewing axis is
+    (anti)parallel to the reference direction, x is rebuilt from y and the
+    viewing axis, as the reference does."""
+    eye = torch.tensor([[float(x), float(y), float(z)]], dtype=torch.float32)
+    ref_dir = torch.tensor([[0.0, 0.0, -1.0]])
+    view = F.normalize(torch.zeros(1, 3) - eye, eps=1e-5)
+    cam_x = F.normalize(torch.cross(ref_dir, view, dim=1), eps=1e-5)
+    cam_y = F.normalize(torch.cross(view, cam_x, dim=1), eps=1e-5)
+    degenerate = torch.isclose(cam_x, torch.tensor(0.0), atol=5e-3).all(dim=1, keepdim=True)
+    if bool(degenerate.any()):
+        cam_x = torch.where(degenerate, F.normalize(torch.cross(cam_y, view, dim=1), eps=1e-5), cam_x)
+    return torch.stack([cam_x, cam_y, view], dim=2)
 
 
 def orbit_cam2world(num_frames, radius, z_height=0.4):
