@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -86,6 +86,10 @@ _SIGS = {
                            c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p],
     "avr_field_fwd_points": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
                              c_void_p, i64, c_void_p, c_void_p],
+    "avr_field_fwd_rays_batch": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p],
+    "avr_field_fwd_points_batch": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, i64, c_void_p, c_void_p],
     "avr_field_train_sizes": [ctypes.POINTER(FieldDims), c_int, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)],
     "avr_field_bwd_packed_floats": [ctypes.POINTER(FieldDims), ctypes.POINTER(i64)],
     "avr_field_pack_bwd": [ctypes.POINTER(FieldDims), ctypes.POINTER(ResnetFCWeights), c_void_p, c_void_p],

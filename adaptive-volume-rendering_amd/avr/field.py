@@ -213,11 +213,47 @@ class FusedField:
              ptr(table), ptr(ro), ptr(rd), ptr(z), R, N, ptr(out), stream_of(z))
         return out
 
+    def forward_rays_batch(self, ro, rd, z, coarse):
+        """SB scenes at once: ro, rd (SB, R, 3), z (SB*R, N) -> (SB*R*N, 4); one x3
+        launch per group of up to AVR_MAX_SCENES scenes (avr_field_fwd_rays_batch)."""
+        SB, R, _ = ro.shape
+        N = z.shape[-1]
+        ro = ro.to(F32).contiguous()
+        rd = rd.to(F32).contiguous()
+        z = z.to(F32).reshape(SB * R, N).contiguous()
+        require_device(ro, rd, z)
+        out = torch.empty(SB * R * N, 4, device=z.device, dtype=F32)
+        if self.precision != "x3":     # the fp32 kernel is single-scene
+            for b in range(SB):
+                out[b * R * N:(b + 1) * R * N] = self.forward_rays(ro[b], rd[b], z[b * R:(b + 1) * R], coarse, sb=b)
+            return out
+        entry = self.packed(coarse)
+        tables = self.tables_batch(coarse, SB)
+        entry.dims.precision = _lib.FIELD_X3
+        for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
+            n = min(_lib.AVR_MAX_SCENES, SB - g0)
+            views = (ViewDesc * n)(*[self.view(sb) for sb in range(g0, g0 + n)])
+            call("avr_field_fwd_rays_batch", ctypes.byref(entry.dims), views, n, ptr(entry.packed), ptr(tables[g0]),
+                 ptr(ro[g0]), ptr(rd[g0]), ptr(z[g0 * R]), R, N, ptr(out[g0 * R * N]), stream_of(z))
+        return out
+
     def forward_points(self, xyz, viewdirs, coarse):
         """The rf(xyz (SB,B,3), viewdirs, coarse) protocol -> (SB, B, 4)."""
         SB, B, _ = xyz.shape
         out = torch.empty(SB, B, 4, device=xyz.device, dtype=F32)
         entry = self.packed(coarse)
+        if SB > 1 and self.precision == "x3":   # one launch per group of scenes
+            p = xyz.to(F32).contiguous()
+            v = viewdirs.reshape(SB, B, 3).to(F32).contiguous()
+            require_device(p, v)
+            tables = self.tables_batch(coarse, SB)
+            entry.dims.precision = _lib.FIELD_X3
+            for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
+                n = min(_lib.AVR_MAX_SCENES, SB - g0)
+                views = (ViewDesc * n)(*[self.view(sb) for sb in range(g0, g0 + n)])
+                call("avr_field_fwd_points_batch", ctypes.byref(entry.dims), views, n, ptr(entry.packed),
+                     ptr(tables[g0]), ptr(p[g0]), ptr(v[g0]), B, ptr(out[g0]), stream_of(p))
+            return out
         for sb in range(SB):
             p = xyz[sb].to(F32).contiguous()
             v = viewdirs.reshape(SB, B, 3)[sb].to(F32).contiguous()

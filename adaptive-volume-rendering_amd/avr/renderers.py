@@ -199,8 +199,7 @@ class VolumeRenderer(nn.Module):
                 fusedf = radiance_field.fused()
                 if SB == 1:
                     return fusedf.forward_rays(ro[0], rd[0], z, coarse).reshape(SB * R, n, 4)
-                outs = [fusedf.forward_rays(ro[b], rd[b], z.reshape(SB, R, n)[b], coarse, sb=b) for b in range(SB)]
-                return torch.cat(outs, 0).reshape(SB * R, n, 4)
+                return fusedf.forward_rays_batch(ro, rd, z, coarse).reshape(SB * R, n, 4)   # one launch per 16 scenes
             pts, vd = ops.points(ro.reshape(SB * R, 3), rd.reshape(SB * R, 3), z)
             out = radiance_field(pts.reshape(SB, -1, 3), viewdirs=vd.reshape(SB, -1, 3), coarse=coarse)
             return out.reshape(SB * R, n, 4)

@@ -587,6 +587,55 @@ extern "C" int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_des
   return dispatch_field(dims, a, as_stream(stream));
 }
 
+// Several scenes in one launch (x3 path): scene s's samples are rows s * per_scene .. of the inputs, its lin_z
+// tables at tables + s * max(n_lin_z, 1) * H*W * d_hidden (FusedField.tables_batch), its view views[s].
+static int field_batch(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes, const float* packed,
+                       const float* tables, FieldArgs* a, int64_t per_scene, const char* what) {
+  AVR_REQUIRE(views && n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES, "%s: 1..%d scenes per call", what,
+              AVR_MAX_SCENES);
+  AVR_REQUIRE(dims && dims->precision == AVR_FIELD_X3, "%s: the multi-scene launch is x3 only", what);
+  int rc = field_common(dims, views, packed, tables, a);
+  if (rc) return rc;
+  for (int s = 0; s < n_scenes; ++s) {
+    AVR_REQUIRE(views[s].latent_h == views[0].latent_h && views[s].latent_w == views[0].latent_w,
+                "%s: scenes need latent maps of one size", what);
+    view_from_desc(&views[s], &a->views[s]);
+  }
+  a->M = per_scene;
+  a->n_scenes = n_scenes;
+  a->blocks_per_scene = (per_scene + kX3Samples - 1) / kX3Samples;
+  a->table_scene_stride = (int64_t)(dims->n_lin_z > 0 ? dims->n_lin_z : 1) * a->table_stride;
+  return AVR_OK;
+}
+
+extern "C" int avr_field_fwd_rays_batch(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
+                                        const float* packed, const float* tables, const float* ro, const float* rd,
+                                        const float* z, int64_t n_rays, int n_samples, float* out, void* stream) {
+  FieldArgs a{};
+  AVR_REQUIRE(n_rays >= 0 && n_samples > 0, "avr_field_fwd_rays_batch: bad sizes");
+  int rc = field_batch(dims, views, n_scenes, packed, tables, &a, n_rays * n_samples, "avr_field_fwd_rays_batch");
+  if (rc) return rc;
+  AVR_REQUIRE(n_rays == 0 || (ro && rd && z && out), "avr_field_fwd_rays_batch: null pointer");
+  a.ro = ro; a.rd = rd; a.z = z; a.n_samples = n_samples;
+  a.out = reinterpret_cast<float4*>(out);
+  if (a.M == 0) return AVR_OK;
+  return dispatch_field_x3(dims->d_hidden, a, as_stream(stream));
+}
+
+extern "C" int avr_field_fwd_points_batch(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
+                                          const float* packed, const float* tables, const float* xyz,
+                                          const float* viewdirs, int64_t n_points, float* out, void* stream) {
+  FieldArgs a{};
+  AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points_batch: bad size");
+  int rc = field_batch(dims, views, n_scenes, packed, tables, &a, n_points, "avr_field_fwd_points_batch");
+  if (rc) return rc;
+  AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && out), "avr_field_fwd_points_batch: null pointer");
+  a.xyz = xyz; a.vd = viewdirs; a.n_samples = 1;
+  a.out = reinterpret_cast<float4*>(out);
+  if (a.M == 0) return AVR_OK;
+  return dispatch_field_x3(dims->d_hidden, a, as_stream(stream));
+}
+
 extern "C" int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
                                     const float* table, const float* xyz, const float* viewdirs, int64_t n_points,
                                     float* out, void* stream) {

@@ -192,6 +192,30 @@ __device__ __forceinline__ SampleGeom sample_geom(const FieldArgs& a, int64_t mm
   return s;
 }
 
+// sample_geom for scene `scene` of a multi-scene launch: its samples are rows
+// roff .. roff + M of the z / xyz arrays (roff = scene * M), its rays rows
+// roff / n_samples onward, viewed from v (that scene's source view).
+__device__ __forceinline__ SampleGeom sample_geom_scene(const FieldArgs& a, const View& v, int64_t roff, int64_t mm) {
+  float x0, x1, x2, d0, d1, d2;
+  const int64_t g = roff + mm;
+  if (a.z) {
+    const int64_t r = g / a.n_samples;
+    const float zz = a.z[g];
+    d0 = a.rd[3 * r]; d1 = a.rd[3 * r + 1]; d2 = a.rd[3 * r + 2];
+    x0 = fadd(a.ro[3 * r], fmul(d0, zz));      // ros + rds * z (renderers.py:171, :260)
+    x1 = fadd(a.ro[3 * r + 1], fmul(d1, zz));
+    x2 = fadd(a.ro[3 * r + 2], fmul(d2, zz));
+  } else {
+    x0 = a.xyz[3 * g]; x1 = a.xyz[3 * g + 1]; x2 = a.xyz[3 * g + 2];
+    d0 = a.vd[3 * g]; d1 = a.vd[3 * g + 1]; d2 = a.vd[3 * g + 2];
+  }
+  SampleGeom s;
+  s.xr[0] = dot3(v.R + 0, x0, x1, x2); s.xr[1] = dot3(v.R + 3, x0, x1, x2); s.xr[2] = dot3(v.R + 6, x0, x1, x2);
+  s.vr[0] = dot3(v.R + 0, d0, d1, d2); s.vr[1] = dot3(v.R + 3, d0, d1, d2); s.vr[2] = dot3(v.R + 6, d0, d1, d2);
+  s.bl = bilinear_from_rot(v, s.xr);
+  return s;
+}
+
 // World point -> bilinear corners of the source-view latent (models.py:753-760, :260-273).
 __device__ __forceinline__ Bilinear bilinear_at(const View& v, float x0, float x1, float x2) {
   const float xr[3] = {dot3(v.R + 0, x0, x1, x2), dot3(v.R + 3, x0, x1, x2), dot3(v.R + 6, x0, x1, x2)};

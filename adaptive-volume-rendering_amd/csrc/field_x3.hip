@@ -256,14 +256,16 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   const int g = lane >> 4, j = lane & 15;
   const int gg = g + 4 * (wid >> 2);               // prologue: sub-lane of sample 16 (wid & 3) + j
   // SAVE: one training launch covers every scene of the batch (scene of this workgroup, its rows)
+  // (inference over several scenes in one launch likewise: n_scenes > 1)
+  const bool multi = SAVE || a.n_scenes > 1;
   int scene = 0;
   int64_t lblk = blockIdx.x;
-  if (SAVE) {
+  if (multi) {
     scene = (int)(blockIdx.x / a.blocks_per_scene);
     lblk = blockIdx.x - (int64_t)scene * a.blocks_per_scene;
   }
   const int64_t base = lblk * kX3Samples;
-  const int64_t roff = SAVE ? (int64_t)scene * a.M : 0;
+  const int64_t roff = (int64_t)scene * a.M;
   const Layout& L = a.L;
   const uint4* P16 = reinterpret_cast<const uint4*>(a.packed);  // 16-B units
 
@@ -284,7 +286,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     const int64_t m = base + s;
     const int64_t mm = m < a.M ? m : a.M - 1;
     const SampleGeom geo = SAVE ? sample_geom_pts(a.views[scene], a.xyz + 3 * roff, a.vd + 3 * roff, mm)
-                                : sample_geom(a, mm);
+                                : sample_geom_scene(a, multi ? a.views[scene] : a.v, roff, mm);
     if (g == 0 && wid < 4) {
       *reinterpret_cast<int4*>(tail->tex + 4 * s) = make_int4(geo.bl.tex[0], geo.bl.tex[1], geo.bl.tex[2], geo.bl.tex[3]);
       *reinterpret_cast<float4*>(tail->w + 4 * s) = make_float4(geo.bl.w[0], geo.bl.w[1], geo.bl.w[2], geo.bl.w[3]);
@@ -373,7 +375,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   // 8 waves: block 0's lin_z stage rows that do not overlap lin_in's X are DMA'd before the lin_in GEMM
   constexpr bool PRE0 = TWO;
   if (PRE0 && a.n_lin_z > 0 && D <= P::CAP && D > P::IN_ROWS0) {
-    stage_rows<HID, NW>(stage, a.table, tail, P::IN_ROWS0, D - P::IN_ROWS0, P::RS, lane, wid, P::IN_ROWS0);
+    stage_rows<HID, NW>(stage, a.table + scene * a.table_scene_stride, tail, P::IN_ROWS0, D - P::IN_ROWS0, P::RS, lane, wid, P::IN_ROWS0);
     p0 = P::IN_ROWS0;
     p1 = D;
   }
@@ -384,7 +386,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     // + lin_z[b](interp latent) (models.py ResnetFC: x = x + lin_z[b](z) before block b)
     // (fused with the fc_0 input prep: v = relu(h), mx)
     if (b < a.n_lin_z) lds_barrier();  // every wave is done reading X (the stage aliases it)
-    const float* table = a.table + b * a.table_stride + (SAVE ? scene * a.table_scene_stride : 0);
+    const float* table = a.table + b * a.table_stride + scene * a.table_scene_stride;
     if (b < a.n_lin_z && D <= P::CAP) {
       if (p0 > 0) stage_rows<HID, NW>(stage, table, tail, 0, p0, P::RS, lane, wid, 0);
       if (p1 < D) stage_rows<HID, NW>(stage, table, tail, p1, D - p1, P::RS, lane, wid, p1);
@@ -574,7 +576,8 @@ static int launch_x3(const FieldArgs& a, hipStream_t s) {
       return fail(AVR_E_HIP, "field_x3_kernel: cannot set dynamic LDS to %zu", shm);
     attr = true;
   }
-  const int64_t blocks = SAVE ? a.blocks_per_scene * a.n_scenes : (a.M + kX3Samples - 1) / kX3Samples;
+  const int64_t blocks = (SAVE || a.n_scenes > 1) ? a.blocks_per_scene * a.n_scenes
+                                                  : (a.M + kX3Samples - 1) / kX3Samples;
   AVR_REQUIRE(blocks < (1ll << 31), "field: too many points");
   field_x3_kernel<FT, NW, SAVE><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("field_x3_kernel");

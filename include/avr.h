@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 5
+#define AVR_ABI_VERSION 6
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -214,6 +214,20 @@ int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_desc* view, co
 int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
                          const float* table, const float* xyz, const float* viewdirs, int64_t n_points,
                          float* out, void* stream);
+
+/* Several scenes (<= AVR_MAX_SCENES) in one launch, x3 path only: scene s has
+ * its own view views[s] (host array) and lin_z tables (tables + s *
+ * max(n_lin_z, 1) * H*W * d_hidden: the per-scene tables back to back), and
+ * its samples at rows s * n_rays * n_samples (rays: ro / rd rows s * n_rays)
+ * or s * n_points (points) of the inputs and of out. The same results as one
+ * avr_field_fwd_rays / _points call per scene (the VolumeRenderer's SB > 1
+ * batches, renderers.py:171-174 over models.py:739-863 per object).           */
+int avr_field_fwd_rays_batch(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
+                             const float* packed, const float* tables, const float* ro, const float* rd,
+                             const float* z, int64_t n_rays, int n_samples, float* out, void* stream);
+int avr_field_fwd_points_batch(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
+                               const float* packed, const float* tables, const float* xyz, const float* viewdirs,
+                               int64_t n_points, float* out, void* stream);
 
 /* ---------------------------------------------------------- field training
  * Autograd of NewPixelNeRFNet.forward for train.py:108-114 (loss.backward()

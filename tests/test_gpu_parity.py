@@ -482,3 +482,33 @@ def test_sample_fine_philox_pairs():
     # u2 ~ U[0,1): the position of z_fine inside its coarse bin
     frac = to_np(zf - 0.8) * Nc - to_np(idx).astype(np.float32)
     assert frac.min() > -1e-3 and frac.max() < 1 + 1e-3 and abs(frac.mean() - 0.5) < 5e-3
+
+
+@pytest.mark.parametrize("SB", [3, 17])
+def test_multi_scene_field_launch_equals_per_scene(SB):
+    """avr_field_fwd_rays_batch / _points_batch (up to 16 scenes per launch, each
+    with its own latent, pose and tables) equal one launch per scene bit for
+    bit; the renderer's SB > 1 fused path uses them."""
+    from avr.scene import synthetic_scene
+    net = synthetic_scene(DEV)
+    g = torch.Generator().manual_seed(SB)
+    lat = torch.randn(SB, net.d_latent, 64, 64, generator=g).to(DEV)
+    net.encoder.set_latent(lat)
+    net.num_objs = SB
+    poses = net.poses.repeat(SB, 1, 1)
+    poses[:, 0, 3] += 0.03 * torch.arange(SB, device=DEV, dtype=torch.float32)
+    net.poses = poses
+    net.focal, net.c = net.focal.repeat(SB, 1), net.c.repeat(SB, 1)
+    R, N = 100, 37
+    ro = (torch.rand(SB, R, 3, generator=g) * 0.2 + torch.tensor([0.3, -1.1, 0.5])).to(DEV)
+    rd = torch.nn.functional.normalize(-ro + 0.3 * torch.randn(SB, R, 3, generator=g).to(DEV), dim=-1)
+    z = torch.sort(0.8 + torch.rand(SB * R, N, generator=g), -1)[0].to(DEV)
+    f = net.fused()
+    with torch.no_grad():
+        batch = f.forward_rays_batch(ro, rd, z, False)
+        loop = torch.cat([f.forward_rays(ro[b], rd[b], z[b * R:(b + 1) * R], False, sb=b) for b in range(SB)])
+        assert torch.equal(batch, loop)
+        xyz = ro[..., None, :] + rd[..., None, :] * z.reshape(SB, R, N, 1)
+        vd = rd[..., None, :].expand(SB, R, N, 3)
+        pts = net(xyz.reshape(SB, -1, 3), coarse=False, viewdirs=vd.reshape(SB, -1, 3))
+    torch.testing.assert_close(pts.reshape(-1, 4), batch, atol=0, rtol=0)
