@@ -186,14 +186,35 @@ class HbmKernelTimer:
         e.synchronize()
         return s.elapsed_time(e) * 1e3 / reps
 
-    def report(self, reps=20):
+    def report(self, reps=20, achievable=None):
         res = []
         for label, (fn, a, k, nb) in self.calls.items():
             us = self._replay_us(fn, a, k, reps)
             gbs = nb / (us * 1e-6) / 1e9
             res.append({"kernel": label, "avg_us": round(us, 2), "bytes_per_launch": int(nb),
                         "achieved_GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)})
+            if achievable:
+                res[-1]["frac_of_achievable"] = round(gbs / achievable, 4)
         return res
+
+
+def achievable_hbm_gbs(device, nbytes=1 << 31, reps=5):
+    """the HBM bandwidth a plain device copy reaches on this box
+    (read + write bytes / time, 2 GiB buffers, HIP events)."""
+    src = torch.empty(nbytes // 4, device=device, dtype=torch.float32).fill_(1.0)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e.record()
+    e.synchronize()
+    gbs = 2 * nbytes * reps / (s.elapsed_time(e) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return gbs
 
 
 def cpu_share():
@@ -465,8 +486,9 @@ def main():
     ap.add_argument("--precision", choices=["x3", "fp32"], default="x3",
                     help="field MFMA path: split-fp16 (3 products, fp32 accumulate) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", type=int, choices=[3, 4, 5], default=None,
-                    help="BASELINE config (default: 3 on one GPU, 5 on more): 3 = 65536 random rays per GPU (weak "
+    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=None,
+                    help="BASELINE config (default: 3 on one GPU, 5 on more): 2 = the coarse pass only (65536 "
+                         "rays x 128 samples: rays, stratified z, field, composite); 3 = 65536 random rays per GPU (weak "
                          "scaling); 5 = 4 orbit views of 800x800 per step for the whole job, dealt to the ranks in "
                          "64-ray tiles (strong scaling, avr.parallel.render_sharded); 4 = one 800x800 frame per "
                          "step with fine-pass early termination at T_stop 1e-5")
@@ -556,6 +578,12 @@ def main():
                 else:
                     rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
                 return rgb_f
+            if config == 2:   # BASELINE configs[1]: the coarse pass alone
+                ro, rd, zc, _, _ = avr.ops.rays_sample_coarse(x_pix, K, c2w, 0.8, 1.8, args.n_coarse, seed=rend.seed)
+                rgb_c, _, _ = avr.ops.composite(zc, fused.forward_rays(ro[0], rd[0], zc, True), True,
+                                                want_weights=False)
+                rend.last_path, rend.last_fine_samples = "fused", 0
+                return rgb_c
             rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
             if world > 1:
                 local = torch.cat([rgb_c.reshape(-1), rgb_f.reshape(-1), depth.reshape(-1)])
@@ -591,7 +619,7 @@ def main():
     # whole-job rays: config 5 renders a fixed 4 x 800 x 800 per step over all ranks (strong scaling)
     rays_total = (R if config == 5 else R * world) * args.steps
     value = rays_total / elapsed
-    samples_per_ray = args.n_coarse + args.n_coarse + args.n_fine
+    samples_per_ray = args.n_coarse if config == 2 else args.n_coarse + args.n_coarse + args.n_fine
     fps = field_flops_per_sample()
     field_launches = len(timer.events)
     achieved_tflops = timer.samples * fps / (field_ms * 1e-3) / 1e12
@@ -614,12 +642,14 @@ def main():
         "scaling": "strong" if config == 5 else "weak",
         "vs_baseline": None,
         "dtype": "fp32" if args.precision == "fp32" else "fp32 (field products as 3 fp16 MFMA terms)",
-        "data": ("synthetic rays (x_pix ~ U[0,1)^2, orbit pose)" if config == 3 else
+        "data": ("synthetic rays (x_pix ~ U[0,1)^2, orbit pose)" if config in (2, 3) else
                  "synthetic rays (get_opencv_pixel_coordinates 800x800 grid, orbit poses)")
                 + ", random-init default.conf field, random 512x64x64 latent",
         "config": {"workload": (f"BASELINE config 3: {R} rays/GPU x ({args.n_coarse} coarse + {args.n_fine} fine, "
                                 "n_fine_depth 0), conf/default.conf PixelNeRF field (3x512 ResnetFC, d_latent 512)")
                    if config == 3 else
+                   (f"BASELINE config 2: {R} rays/GPU x {args.n_coarse} coarse samples, coarse pass only (rays, "
+                    "stratified z, field, composite), conf/default.conf PixelNeRF field") if config == 2 else
                    (f"BASELINE config 4: 800x800 frame ({R} rays)/GPU x ({args.n_coarse} coarse + {args.n_fine} "
                     f"fine), fine-pass early termination T_stop 1e-5, sigma bias {args.sigma_bias}, "
                     "conf/default.conf PixelNeRF field") if config == 4 else
@@ -642,8 +672,11 @@ def main():
             "field_share_of_step": round(field_ms / (elapsed * 1e3), 4),
         },
     }
-    # the renderer's HBM-bound kernels (the metric's "achieved HBM GB/s vs roofline"), HIP events per launch
-    line["hbm_kernels"] = hbm.report()
+    # the renderer's HBM-bound kernels (the metric's "achieved HBM GB/s vs roofline"), HIP events per launch,
+    # against the 8 TB/s peak and against what a device copy reaches on this box
+    ach = achievable_hbm_gbs(device)
+    line["hbm_achievable_GBs"] = round(ach, 1)
+    line["hbm_kernels"] = hbm.report(achievable=ach)
     pmc = os.path.join(REPO, "profiles", "field_pmc.json")
     if os.path.exists(pmc):
         # not measured in this run: the committed rocprofv3 --pmc pass over this bench (TCC_EA0 read/write
