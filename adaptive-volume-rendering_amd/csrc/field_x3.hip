@@ -424,9 +424,11 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       floatx4 bv[FT];
       load_bias<FT, true>(bv, a.packed + L.b_fc0[b], wid, g);
       mx = max_relu_affine<FT, true>(t, 1.0f / S_t, bv);
+      if (b == 1) AVR_STAMP(20);
       floatx4 bb[FT];
       load_bias<FT, true>(bb, a.packed + L.b_fc1[b], wid, g);
       prefetch_a<FT, NPF>(A0, W1, lane);
+      if (b == 1) AVR_STAMP(21);
       s_x = publish_affine<FT, NW, true>(X16, t, 1.0f / S_t, bv, mx, red, wid, lane, g, j);
       AVR_STAMP(8 + 5 * (b & 3));
       // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)

@@ -49,9 +49,12 @@ have4 = (w4[:, 0] != 0).mean() > 0.99
 names = {0: "start", 27: "sample_geom", 28: "dedup texels", 1: "PE sines", 2: "publish X0", 3: "lin_in init",
          4: "lin_in gemm"}
 for b in range(4):
+    if b == 3:
+        continue
     names.update({5 + 5 * b: f"b{b} lin_z interp", 6 + 5 * b: f"b{b} prep+publish h", 7 + 5 * b: f"b{b} fc0 gemm",
                   8 + 5 * b: f"b{b} prep+publish t", 9 + 5 * b: f"b{b} fc1 init+gemm"})
-names.update({25: "lin_out prep+publish", 26: "lin_out gemm", 29: "b2 stage issue", 30: "b2 stage wait"})
+names.update({25: "lin_out prep+publish", 26: "lin_out gemm", 29: "b2 stage issue", 30: "b2 stage wait",
+              20: "b1 t max pass", 21: "b1 bias/prefetch issue"})
 used = [k for k in names if (st[:, k] != 0).mean() > 0.99]
 used.sort(key=lambda k: np.median(st[:, k] - st[:, 0]))
 print(f"kernel {t0.elapsed_time(t1):.2f} ms for {R * N} samples, {blocks} blocks")
