@@ -69,6 +69,13 @@ __device__ __forceinline__ void invert(double (&a)[N][N], double (&inv)[N][N]) {
   }
 }
 
+// per-lane select by a wave-uniform lane mask (bit l set: lane l takes `set`)
+__device__ __forceinline__ float mask_select(uint64_t m, float clear, float set) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(clear), "v"(set), "s"(m));
+  return r;
+}
+
 // ------------------------------------------------------------------ Philox4x32-10
 // Counter-based RNG for in-kernel noise (no noise bytes read from HBM).
 __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
@@ -125,20 +132,20 @@ __device__ __forceinline__ float lane_xor(float v, int J, int lane) {
     case 4: {
       const int up = __builtin_amdgcn_update_dpp(b, b, 0x104, 0xf, 0xf, false);   // row_shl:4 (lane + 4)
       const int dn = __builtin_amdgcn_update_dpp(b, b, 0x114, 0xf, 0xf, false);   // row_shr:4 (lane - 4)
-      return __int_as_float((lane & 4) ? dn : up);
+      return mask_select(0xF0F0F0F0F0F0F0F0ull, __int_as_float(up), __int_as_float(dn));   // lane & 4
     }
     case 8: {
       const int up = __builtin_amdgcn_update_dpp(b, b, 0x108, 0xf, 0xf, false);
       const int dn = __builtin_amdgcn_update_dpp(b, b, 0x118, 0xf, 0xf, false);
-      return __int_as_float((lane & 8) ? dn : up);
+      return mask_select(0xFF00FF00FF00FF00ull, __int_as_float(up), __int_as_float(dn));
     }
     case 16: {
       const auto r = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
-      return __uint_as_float((lane & 16) ? r[0] : r[1]);
+      return mask_select(0xFFFF0000FFFF0000ull, __uint_as_float(r[1]), __uint_as_float(r[0]));
     }
     default: {
       const auto r = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
-      return __uint_as_float((lane & 32) ? r[0] : r[1]);
+      return mask_select(0xFFFFFFFF00000000ull, __uint_as_float(r[1]), __uint_as_float(r[0]));
     }
   }
 }

@@ -105,10 +105,12 @@ __global__ void __launch_bounds__(256) sample_coarse_rays_kernel(const float* __
 
 // get_world_rays (utils.py:315-336) + sample_coarse (renderers.py:4-24) in one
 // launch, plus each ray's depth row for the composite epilogue. A workgroup
-// owns kRaysPerBlock consecutive rays: first one thread per ray builds ro, rd
-// (and, if asked, row 2 of inverse(cam2world) in fp64: depth = -(row . [x, 1]),
-// utils.py:358-361), then the workgroup writes the rays' z in 4-sample quads,
-// consecutive threads on consecutive quads (coalesced 16-B stores).
+// owns kRaysPerBlock consecutive rays: wave 0 builds ro, rd with one lane per
+// ray (and, if asked, row 2 of inverse(cam2world) in fp64: depth = -(row .
+// [x, 1]), utils.py:358-361) while waves 1-3 write the rays' z in 4-sample
+// quads, consecutive threads on consecutive quads (coalesced 16-B stores): z
+// does not depend on the geometry, so the fp64 latency of wave 0 overlaps the
+// z stores instead of preceding them.
 constexpr int kRaysPerBlock = 64;
 
 template <bool POW2>
@@ -126,7 +128,9 @@ __global__ void __launch_bounds__(256) rays_coarse_kernel(
   if (tab)
     for (int s = threadIdx.x; s < n; s += blockDim.x)
       base_tab[s] = fadd(near_, fmul(span, div_count<POW2>((float)s, (float)n, inv_n)));
-  if (threadIdx.x < kRaysPerBlock && r0 + threadIdx.x < total) {
+  __syncthreads();   // base_tab
+  if (threadIdx.x < kRaysPerBlock) {
+    if (r0 + threadIdx.x >= total) return;
     const int64_t i = r0 + threadIdx.x;
     const int64_t sb = i / n_rays, r = i - sb * n_rays;
     double k[3][3], ki[3][3];
@@ -162,13 +166,14 @@ __global__ void __launch_bounds__(256) rays_coarse_kernel(
       invert<4>(m, inv);
       reinterpret_cast<double4*>(depth_row)[i] = make_double4(inv[2][0], inv[2][1], inv[2][2], inv[2][3]);
     }
+    return;
   }
-  __syncthreads();   // base_tab
   const int nq = (n + 3) >> 2;
+  const int lg_nq = POW2 && n >= 4 ? __builtin_ctz((unsigned)nq) : 0;   // nq a power of two too
   const int64_t nr_blk = total - r0 < kRaysPerBlock ? total - r0 : kRaysPerBlock;
   const int items = (int)nr_blk * nq;
-  for (int it = threadIdx.x; it < items; it += blockDim.x) {
-    const int rl = it / nq, q = it - rl * nq;
+  for (int it = threadIdx.x - kRaysPerBlock; it < items; it += blockDim.x - kRaysPerBlock) {
+    const int rl = POW2 && n >= 4 ? it >> lg_nq : it / nq, q = it - rl * nq;
     const int64_t ray = r0 + rl;
     float u[4];
     if (noise) {
@@ -231,6 +236,28 @@ __device__ float cascade_sum_wave(const float* x, int N, int lane, float* scratc
 }
 
 constexpr int kMaxCoarse = 256;
+constexpr int kMaxK = kMaxCoarse / 64;   // coarse samples per lane
+
+// cascade_sum_wave for N a multiple of 64 from registers: lane l holds
+// x[l + 64m], m < K = N/64. Same additions in the same order: lane l < 32
+// sums x[32i + l] over i (x[l + 64m], then lane l+32's x[l + 32 + 64m]), lane
+// l < 8 adds the partials of lanes l+8, l+16, l+24, and the 8 lane sums are
+// added in lane order. No LDS round trips or wave barriers.
+__device__ __forceinline__ float cascade_sum_regs(const float (&x)[kMaxK], int K, int lane) {
+  float p = 0.f;
+#pragma unroll
+  for (int m = 0; m < kMaxK; ++m)
+    if (m < K) {
+      p = fadd(p, x[m]);
+      p = fadd(p, lane_xor(x[m], 32, lane));
+    }
+  const float q8 = lane_xor(p, 8, lane);
+  const float a = fadd(fadd(fadd(p, q8), lane_xor(p, 16, lane)), lane_xor(q8, 16, lane));
+  float s = 0.f;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) s = fadd(s, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), l)));
+  return s;
+}
 constexpr int kMaxSort = 512;
 constexpr int kFineWaves = 4;
 
@@ -242,34 +269,67 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-// #{L[i] < x} (LT) or #{L[i] <= x} over the sorted LDS list L[0..n); n is wave-uniform.
+// #{L[i] < x} (LT) or #{L[i] <= x} over the sorted LDS list L[0..n). The
+// probe sequence depends on n only (base += half when L[base + half - 1]
+// passes): a uniform n keeps the loop scalar and the lanes converged.
 template <bool LT>
 __device__ __forceinline__ int count_below(const float* L, int n, float x) {
-  int lo = 0;
-  while (n > 0) {
-    const int half = n >> 1;
-    const float v = L[lo + half];
-    const bool go = LT ? (v < x) : (v <= x);
-    lo = go ? lo + half + 1 : lo;
-    n = go ? n - half - 1 : half;
+  if (n <= 0) return 0;
+  int base = 0;
+  for (int len = n; len > 1;) {
+    const int half = len >> 1;
+    const float v = L[base + half - 1];
+    base = (LT ? v < x : v <= x) ? base + half : base;
+    len -= half;
   }
-  return lo;
+  const float v = L[base];
+  return base + ((LT ? v < x : v <= x) ? 1 : 0);
+}
+
+// lanes of a bitonic stage (k, j) that keep the minimum: ((l & k) == 0) == ((l & j) == 0)
+__host__ __device__ constexpr uint64_t bitonic_min_lanes(int k, int j) {
+  uint64_t m = 0;
+  for (int l = 0; l < 64; ++l)
+    if (((l & k) == 0) == ((l & j) == 0)) m |= 1ull << l;
+  return m;
+}
+
+// partner value of lane l ^ J for the sort: quad-permute DPP (J = 1, 2; left
+// to the compiler to fold into the min/max), a ds_swizzle xor within 32 lanes
+// (J = 4, 8, 16: LDS crossbar, no memory traffic, one instruction instead of
+// two DPP rows and a select), the permlane32 swap for J = 32
+template <int J>
+__device__ __forceinline__ float sort_partner(float v, int lane) {
+  const int b = __float_as_int(v);
+  if constexpr (J == 1) return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0xB1, 0xf, 0xf, false));
+  else if constexpr (J == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0x4E, 0xf, 0xf, false));
+  else if constexpr (J <= 16) return __int_as_float(__builtin_amdgcn_ds_swizzle(b, 0x1F | (J << 10)));
+  else return lane_xor(v, J, lane);
+}
+
+template <int K, int J>
+__device__ __forceinline__ float bitonic_stages(float v, int lane) {
+  // keep v where (v < o) == (lane keeps the minimum), else o: one compare
+  // (into a lane mask), a scalar xnor with the stage's constant, one select;
+  // equal values are interchangeable (values-only sort, no NaN, no -0)
+  const float o = sort_partner<J>(v, lane);
+  const uint64_t keep_v = ~(__ballot(v < o) ^ bitonic_min_lanes(K, J));
+  v = mask_select(keep_v, o, v);
+  if constexpr (J > 1) return bitonic_stages<K, J / 2>(v, lane);
+  else return v;
+}
+
+template <int K>
+__device__ __forceinline__ float bitonic_from(float v, int lane) {
+  v = bitonic_stages<K, K / 2>(v, lane);
+  if constexpr (K < 64) return bitonic_from<2 * K>(v, lane);
+  else return v;
 }
 
 // Ascending bitonic sort of one float per lane across the wave (64 values);
-// partners through lane_xor (DPP / permlane swaps, no LDS round trips).
-__device__ __forceinline__ float wave_sort64(float v, int lane) {
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const float o = lane_xor(v, j, lane);
-      const bool up = (lane & k) == 0, lower = (lane & j) == 0;
-      v = (lower == up) ? fminf(v, o) : fmaxf(v, o);
-    }
-  }
-  return v;
-}
+// partners through lane_xor (DPP / permlane swaps, no LDS round trips), the
+// min/max choice by a constant lane mask.
+__device__ __forceinline__ float wave_sort64(float v, int lane) { return bitonic_from<2>(v, lane); }
 
 // count_below over the sorted list L[0..n) starting from a guess g of the
 // answer: when L[g-2] and L[g+2] bracket x (checked), a 2-step search of the
@@ -283,8 +343,6 @@ __device__ __forceinline__ int count_below_near(const float* L, int n, float x, 
   if (below_lo && above_hi) return lo + count_below<LT>(L + lo, hi - lo, x);
   return count_below<LT>(L, n, x);
 }
-
-constexpr int kMaxK = kMaxCoarse / 64;   // coarse samples per lane
 
 // One wave per ray; no block barriers (each wave owns its LDS slice).
 //   1) w' = w + 1e-5, s = torch-CPU cascade sum (bit-exact);
@@ -300,16 +358,19 @@ constexpr int kMaxK = kMaxCoarse / 64;   // coarse samples per lane
 //      merged by rank (own index + counts below in the other lists, ties broken
 //      coarse < fine < depth; a fine value's count in the coarse list starts
 //      from its stratified bin); otherwise a wave-local bitonic sort.
-template <bool POW2>
+// NC, NF, ND > 0: the sample counts as compile-time constants (the renderer's
+// 128 -> 64 shape: loops unrolled, no loop or exec-mask bookkeeping); 0: runtime.
+template <bool POW2, int NC = 0, int NF = 0, int ND = 0>
 __global__ void __launch_bounds__(256) sample_fine_kernel(
     const float* __restrict__ weights, const float* __restrict__ z_coarse, float near_, float far_, int64_t n_rays,
-    int Nc, int Nf, int Nd, float depth_std, const float* __restrict__ u_in, const float* __restrict__ u2_in,
+    int Nc_, int Nf_, int Nd_, float depth_std, const float* __restrict__ u_in, const float* __restrict__ u2_in,
     const float* __restrict__ nd_in, uint64_t seed, uint64_t offset, const int64_t* __restrict__ ray_ids, int sort_n,
     float* __restrict__ z_sorted, int32_t* __restrict__ idx_out, float* __restrict__ z_fine_out) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t ray = (int64_t)blockIdx.x * kFineWaves + wid;
   if (ray >= n_rays) return;  // wave-uniform
+  const int Nc = NC ? NC : Nc_, Nf = NC ? NF : Nf_, Nd = NC ? ND : Nd_;
   const int Ntot = Nc + Nf + Nd;
   float* cdf = lds + (size_t)wid * fine_wave_floats(Nc, sort_n, Ntot);   // [0 .. Nc]
   float* scratch = cdf + Nc + 1;
@@ -323,14 +384,27 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
   const float* w = weights + ray * Nc;
   const float* zc = z_coarse + ray * Nc;
   bool coarse_sorted = true;
-  for (int k = lane; k < Nc; k += 64) {
-    cdf[1 + k] = fadd(w[k], 1e-5f);
-    sbuf[k] = zc[k];
+  float xr[kMaxK];
+#pragma unroll
+  for (int m = 0; m < kMaxK; ++m) {
+    const int k = lane + 64 * m;
+    xr[m] = 0.f;
+    if (k < Nc) {
+      xr[m] = fadd(w[k], 1e-5f);
+      cdf[1 + k] = xr[m];
+      sbuf[k] = zc[k];
+    }
   }
-  wave_sync();
+  float s;
+  if ((Nc & 63) == 0) {
+    s = cascade_sum_regs(xr, Nc >> 6, lane);
+    wave_sync();
+  } else {
+    wave_sync();
+    s = cascade_sum_wave(cdf + 1, Nc, lane, scratch);
+  }
   for (int k = lane; k + 1 < Nc; k += 64) coarse_sorted &= sbuf[k] <= sbuf[k + 1];
   coarse_sorted = __all(coarse_sorted);
-  const float s = cascade_sum_wave(cdf + 1, Nc, lane, scratch);
   {
     const int K = (Nc + 63) >> 6, k0 = K * lane;
     float pv[kMaxK];
@@ -384,6 +458,35 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
 
   // 5) sort
   float* out = z_sorted + ray * Ntot;
+  if (coarse_sorted && Nf <= 64 && Nd == 0) {
+    // two lists: the fine values take slots lane + #{A <= bf} (increasing in
+    // lane); the coarse values fill the other slots in order. A slot's list
+    // index = the number of fine slots before it (ballot + mbcnt) or the rest.
+    const float* A = sbuf;
+    float* B = sbuf + Nc;
+    int* marks = reinterpret_cast<int*>(obuf);
+    for (int k = lane; k < Ntot; k += 64) marks[k] = 0;
+    const float bf = wave_sort64(zf_mine, lane);
+    wave_sync();   // the unsorted fine list is read by nobody past this point
+    if (lane < Nf) {
+      B[lane] = bf;
+      const float t = fmul(fsub(bf, near_), (float)Nc / span);
+      const int g = t > 0.f ? (t < (float)Nc ? (int)t : Nc) : 0;
+      marks[lane + count_below_near<false>(A, Nc, bf, g)] = 1;
+    }
+    wave_sync();
+    int base = 0;
+    for (int s0 = 0; s0 < Ntot; s0 += 64) {
+      const int k = s0 + lane;
+      const bool fine = k < Ntot && marks[k] != 0;
+      const uint64_t mask = __ballot(fine);
+      const int before = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+      if (k < Ntot) out[k] = fine ? B[before] : A[k - before];
+      base += __popcll(mask);
+    }
+    return;
+  }
   if (coarse_sorted && Nf <= 64 && Nd <= 64) {
     const float* A = sbuf;
     float* B = sbuf + Nc;
@@ -496,6 +599,7 @@ extern "C" int avr_sample_fine(const float* weights, const float* z_coarse, floa
   const unsigned grid = (unsigned)((n_rays + kFineWaves - 1) / kFineWaves);
   const size_t shm = (size_t)kFineWaves * fine_wave_floats(n_coarse, sort_n, ntot) * sizeof(float);
   auto* kern = (n_coarse & (n_coarse - 1)) == 0 ? sample_fine_kernel<true> : sample_fine_kernel<false>;
+  if (n_coarse == 128 && n_importance == 64 && n_depth == 0) kern = sample_fine_kernel<true, 128, 64, 0>;
   kern<<<grid, 64 * kFineWaves, shm, as_stream(stream)>>>(
       weights, z_coarse, near_, far_, n_rays, n_coarse, n_importance, n_depth, depth_std, u, u2, noise_depth, seed,
       offset, ray_ids, sort_n, z_sorted, idx, z_fine);

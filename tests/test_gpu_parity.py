@@ -115,7 +115,8 @@ def test_sample_fine_bit_exact(golden, case):
     np.testing.assert_array_equal(to_np(zs), np.sort(np.concatenate([zc, g[f"{case}_z"][0]], -1), -1))
 
 
-@pytest.mark.parametrize("Nc,Nf,Nd", [(64, 32, 16), (128, 64, 0), (32, 16, 8), (256, 128, 64), (200, 37, 5)])
+@pytest.mark.parametrize("Nc,Nf,Nd", [(64, 32, 16), (128, 64, 0), (32, 16, 8), (256, 128, 64), (200, 37, 5),
+                                      (64, 64, 0), (192, 17, 0), (256, 64, 0), (96, 33, 0), (100, 1, 0)])
 def test_sample_fine_vs_oracle(Nc, Nf, Nd):
     """Indices bit-exact vs the oracle on weights produced by a volume integral,
     odd sizes included; the sorted merge equals numpy's sort."""
@@ -167,6 +168,23 @@ def test_sample_coarse_ragged_bit_exact(N):
     u_n = (zp - (0.8 + torch.arange(N, device=DEV) / N)) * N
     u_64 = (z64 - (0.8 + torch.arange(64, device=DEV) / 64)) * 64
     torch.testing.assert_close(u_n, u_64[:, :N], atol=2e-5, rtol=0)
+
+
+def test_sample_fine_merge_ties():
+    """Coarse values equal to fine values (n_depth 0: the two-list slot merge):
+    every slot filled once, the output equals numpy's sort."""
+    from avr import ops
+    R, Nc, Nf = 500, 128, 64
+    rng = np.random.default_rng(9)
+    zc = np.sort(rng.uniform(0.8, 1.8, (R, Nc)).astype(np.float32), -1)
+    w = rng.random((R, Nc), dtype=np.float32)
+    u, u2 = rng.random((R, Nf), dtype=np.float32), rng.random((R, Nf), dtype=np.float32)
+    _, _, zf = ops.sample_fine(T(w), T(zc), 0.8, 1.8, Nf, 0, 0.0, u=T(u), u2=T(u2), want_fine=True)
+    zf = to_np(zf)
+    zc2 = np.sort(np.concatenate([zc[:, : Nc - 16], zf[:, :16]], -1), -1)      # 16 exact ties per ray
+    zs, _, zf2 = ops.sample_fine(T(w), T(zc2), 0.8, 1.8, Nf, 0, 0.0, u=T(u), u2=T(u2), want_fine=True)
+    np.testing.assert_array_equal(to_np(zf2), zf)
+    np.testing.assert_array_equal(to_np(zs), np.sort(np.concatenate([zc2, zf], -1), -1))
 
 
 def test_sample_fine_unsorted_coarse_fallback():
