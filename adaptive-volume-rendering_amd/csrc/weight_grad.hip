@@ -110,26 +110,22 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
   const int xcol = i0 + 4 * cc < D.I ? i0 + 4 * cc : 0;
   floatx4 bsum = {0.f, 0.f, 0.f, 0.f};
   constexpr int NU = kDwK / 4;   // rows per thread and chunk
-  const auto load = [&](int c, floatx4 (&gv)[NU], floatx4 (&xv)[NU]) {
+  // Rows of chunk c that exist: rows past the K-range's end (its ragged last
+  // chunk, and the chunks past it that the branch-free pipeline below also
+  // loads) read row k1 - 1 and contribute G = 0. `last` is wave-uniform.
+  const auto chunk_last = [&](int c) -> int {
+    const int64_t n = k1 - 1 - (k0 + (int64_t)kDwK * c);
+    return n < kDwK - 1 ? (int)n : kDwK - 1;
+  };
+  floatx4 gn[NU], xn[NU];
+  // row group u (row rb + 4u) of chunk c -> registers (no branches: the
+  // pipeline's loads stay in flight across the MFMAs that follow them)
+  const auto load_u = [&](int c, int u) {
     const int64_t row0 = k0 + (int64_t)kDwK * c;
-    const float* gb = D.g + row0 * D.ldg;
-    const float* xb = D.x + row0 * D.ldx;
-    if (row0 + kDwK <= k1) {
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        gv[u] = *reinterpret_cast<const floatx4*>(gb + (unsigned)((rb + 4 * u) * ldg + gcol));
-        xv[u] = *reinterpret_cast<const floatx4*>(xb + (unsigned)((rb + 4 * u) * ldx + xcol));
-      }
-    } else {   // the K-range's ragged last chunk: rows past k1 read row k1 - 1, G zeroed
-      const int last = (int)(k1 - 1 - row0);
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const int r = rb + 4 * u < last ? rb + 4 * u : last;
-        gv[u] = *reinterpret_cast<const floatx4*>(gb + (unsigned)(r * ldg + gcol));
-        xv[u] = *reinterpret_cast<const floatx4*>(xb + (unsigned)(r * ldx + xcol));
-        if (rb + 4 * u > last) gv[u] = floatx4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
+    const int last = chunk_last(c);
+    const int r = rb + 4 * u < last ? rb + 4 * u : last;
+    gn[u] = *reinterpret_cast<const floatx4*>(D.g + row0 * D.ldg + (r * ldg + gcol));
+    xn[u] = *reinterpret_cast<const floatx4*>(D.x + row0 * D.ldx + (r * ldx + xcol));
   };
 
   const int wo = wid >> 1, wi = wid & 1;
@@ -140,36 +136,37 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
 #pragma unroll
     for (int u = 0; u < kDwWT; ++u) acc[t][u] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // Row group u of chunk c (registers gv / xv) -> LDS stage c & 1, split into fp16 hi / lo.
-  const auto put = [&](int c, const floatx4 (&gv)[NU], const floatx4 (&xv)[NU], int u) {
+  // Row group u of chunk c (registers gn / xn) -> LDS stage c & 1, split into
+  // fp16 hi / lo; G of rows past the K-range as 0 (also out of the bias sum).
+  const auto put = [&](int c, int u) {
     lds_char* st = lds + (c & 1) * kDwStage;
     const int r = rb + 4 * u, off = img_off_col(r, 4 * cc);
+    const floatx4 g = r > chunk_last(c) ? floatx4{0.f, 0.f, 0.f, 0.f} : gn[u];
     uint2 hi, lo;
-    split4(gv[u], sG, hi, lo);
+    split4(g, sG, hi, lo);
     *(lds_u32x2*)(st + off) = u32x2{hi.x, hi.y};
     *(lds_u32x2*)(st + kDwImg + off) = u32x2{lo.x, lo.y};
-    split4(xv[u], sX, hi, lo);
+    split4(xn[u], sX, hi, lo);
     *(lds_u32x2*)(st + 2 * kDwImg + off) = u32x2{hi.x, hi.y};
     *(lds_u32x2*)(st + 3 * kDwImg + off) = u32x2{lo.x, lo.y};
-    if (bias) bsum += gv[u];
+    if (bias) bsum += g;
   };
 
-  // Chunk c: MFMAs on stage c & 1, with chunk c + 1 (registers gn / xn, loaded
-  // during chunk c - 1) split into stage (c + 1) & 1 between them, then gn / xn
-  // reloaded with chunk c + 2; one barrier. Stage (c + 1) & 1 was last read in
-  // chunk c - 1, which every wave finished before that chunk's barrier.
-  floatx4 gn[NU], xn[NU];
+  // Chunk c: MFMAs on stage c & 1; during the second half of the row tiles,
+  // row group u of chunk c + 1 (registers, loaded one chunk earlier) is split
+  // into stage (c + 1) & 1 and its registers reloaded with chunk c + 2 at
+  // once, so a chunk of loads is always in flight; one barrier. Stage (c + 1) & 1
+  // was last read in chunk c - 1, which every wave finished before that
+  // chunk's barrier. Scheduling barriers keep each row tile's fragment reads
+  // next to its MFMAs (hoisting them all would exhaust the VGPRs).
   const auto step = [&](int c) {
     const lds_char* st = lds + (c & 1) * kDwStage;
-    const bool next = c + 1 < nch;
     half8 bh[kDwWT], bl[kDwWT];
 #pragma unroll
     for (int u = 0; u < kDwWT; ++u) {
       bh[u] = tr_frag(st + 2 * kDwImg, 128 * wi + 16 * u, trb);
       bl[u] = tr_frag(st + 3 * kDwImg, 128 * wi + 16 * u, trb);
     }
-    // A fragments one row tile ahead: row tile t + 1's transposed reads are in
-    // flight while row tile t's 24 MFMAs issue
     half8 ah = tr_frag(st, 128 * wo, trb), al = tr_frag(st + kDwImg, 128 * wo, trb);
 #pragma unroll
     for (int t = 0; t < kDwWT; ++t) {
@@ -184,24 +181,27 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
         acc[t][u] = mfma32h(ah, bl[u], acc[t][u]);
         acc[t][u] = mfma32h(al, bh[u], acc[t][u]);
       }
-      // chunk c + 1's loads were issued at the end of chunk c - 1: split them in
-      // the second half of the MFMAs, when they have landed
-      if (next && t >= kDwWT / 2) {
-        put(c + 1, gn, xn, 2 * (t - kDwWT / 2));
-        put(c + 1, gn, xn, 2 * (t - kDwWT / 2) + 1);
+      if (t >= kDwWT / 2) {   // chunks past nch: harmless (rows clamped, G = 0, stage never read)
+        const int u = 2 * (t - kDwWT / 2);
+        put(c + 1, u);
+        put(c + 1, u + 1);
+        load_u(c + 2, u);
+        load_u(c + 2, u + 1);
       }
+      __builtin_amdgcn_sched_barrier(0);
       ah = ahn;
       al = aln;
     }
-    if (c + 2 < nch) load(c + 2, gn, xn);
     __syncthreads();
   };
 
   if (nch > 0) {
-    load(0, gn, xn);
 #pragma unroll
-    for (int u = 0; u < NU; ++u) put(0, gn, xn, u);
-    if (nch > 1) load(1, gn, xn);
+    for (int u = 0; u < NU; ++u) load_u(0, u);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) put(0, u);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) load_u(1, u);
     __syncthreads();
   }
   for (int c = 0; c < nch; ++c) step(c);
