@@ -25,7 +25,6 @@
 namespace avr {
 
 constexpr int kDwTile = 256;                 // output tile (o x i) per workgroup
-constexpr int kDwWT = 8;                     // 16 x 16 MFMA tiles per wave and dimension (128 x 128 per wave)
 constexpr int kDwK = 32;
 constexpr int kDwRow = 256 + 32;             // bytes per row of a 128-column half image (padded: 9 x 32 B)
 constexpr int kDwHalf = kDwK * kDwRow;       // one 128-column half image (32 rows)
@@ -81,7 +80,15 @@ __device__ __forceinline__ half8 tr_frag(const lds_char* img_full, int col0_full
   return __builtin_bit_cast(half8, both);
 }
 
-__global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
+// NW = 4: one wave per SIMD, 128 x 128 per wave (512 registers: the
+// accumulators fill the AGPRs). NW = 8: two waves per SIMD, 128 x 64 per wave
+// (256 registers), so one wave's MFMAs run while the other waits on LDS or
+// the barrier.
+template <int NW>
+__global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
+  constexpr int WI = NW / 2;                 // waves across the 256 input columns
+  constexpr int TO = 8, TI = 16 / WI;        // 16 x 16 MFMA tiles per wave: output rows x input columns
+  constexpr int NU = kDwK / NW;              // staged rows per thread and chunk
   extern __shared__ float lds_f[];
   lds_char* lds = (lds_char*)lds_f;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -100,7 +107,7 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
   const float sG = pow2_scale_for(__uint_as_float(*D.gmax)), sX = pow2_scale_for(__uint_as_float(*D.xmax));
   const bool bias = D.bpart && it == 0;
 
-  // staging: thread -> 4-column group cc, rows rb + 4u of each 32-row chunk.
+  // staging: thread -> 4-column group cc, rows rb + NW u of each 32-row chunk.
   // Columns past O / I read column 0 instead (finite values whose products
   // land in output rows / columns that are never stored), so every load is
   // unconditional: a uniform chunk base (SGPRs) plus a 32-bit lane offset.
@@ -109,7 +116,6 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
   const int gcol = o0 + 4 * cc < D.O ? o0 + 4 * cc : 0;
   const int xcol = i0 + 4 * cc < D.I ? i0 + 4 * cc : 0;
   floatx4 bsum = {0.f, 0.f, 0.f, 0.f};
-  constexpr int NU = kDwK / 4;   // rows per thread and chunk
   // Rows of chunk c that exist: rows past the K-range's end (its ragged last
   // chunk, and the chunks past it that the branch-free pipeline below also
   // loads) read row k1 - 1 and contribute G = 0. `last` is wave-uniform.
@@ -118,29 +124,29 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
     return n < kDwK - 1 ? (int)n : kDwK - 1;
   };
   floatx4 gn[NU], xn[NU];
-  // row group u (row rb + 4u) of chunk c -> registers (no branches: the
+  // row group u (row rb + NW u) of chunk c -> registers (no branches: the
   // pipeline's loads stay in flight across the MFMAs that follow them)
   const auto load_u = [&](int c, int u) {
     const int64_t row0 = k0 + (int64_t)kDwK * c;
     const int last = chunk_last(c);
-    const int r = rb + 4 * u < last ? rb + 4 * u : last;
+    const int r = rb + NW * u < last ? rb + NW * u : last;
     gn[u] = *reinterpret_cast<const floatx4*>(D.g + row0 * D.ldg + (r * ldg + gcol));
     xn[u] = *reinterpret_cast<const floatx4*>(D.x + row0 * D.ldx + (r * ldx + xcol));
   };
 
-  const int wo = wid >> 1, wi = wid & 1;
+  const int wo = wid / WI, wi = wid % WI;
   const int trb = tr_base(lane);
-  floatx4 acc[kDwWT][kDwWT];
+  floatx4 acc[TO][TI];
 #pragma unroll
-  for (int t = 0; t < kDwWT; ++t)
+  for (int t = 0; t < TO; ++t)
 #pragma unroll
-    for (int u = 0; u < kDwWT; ++u) acc[t][u] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < TI; ++u) acc[t][u] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // Row group u of chunk c (registers gn / xn) -> LDS stage c & 1, split into
   // fp16 hi / lo; G of rows past the K-range as 0 (also out of the bias sum).
   const auto put = [&](int c, int u) {
     lds_char* st = lds + (c & 1) * kDwStage;
-    const int r = rb + 4 * u, off = img_off_col(r, 4 * cc);
+    const int r = rb + NW * u, off = img_off_col(r, 4 * cc);
     const floatx4 g = r > chunk_last(c) ? floatx4{0.f, 0.f, 0.f, 0.f} : gn[u];
     uint2 hi, lo;
     split4(g, sG, hi, lo);
@@ -152,47 +158,49 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
     if (bias) bsum += g;
   };
 
-  // Chunk c: MFMAs on stage c & 1; during the second half of the row tiles,
-  // row group u of chunk c + 1 (registers, loaded one chunk earlier) is split
-  // into stage (c + 1) & 1 and its registers reloaded with chunk c + 2 at
-  // once, so a chunk of loads is always in flight; one barrier. Stage (c + 1) & 1
-  // was last read in chunk c - 1, which every wave finished before that
-  // chunk's barrier. Scheduling barriers keep each row tile's fragment reads
-  // next to its MFMAs (hoisting them all would exhaust the VGPRs).
+  // Chunk c: the loads of chunk c + 2 are issued first (their registers were
+  // split into LDS at the end of chunk c - 1), then the MFMAs on stage c & 1,
+  // one barrier, and chunk c + 2 is split into stage c & 1, which nobody reads
+  // any more; chunk c + 1 (stage (c + 1) & 1, split at the end of chunk c - 1)
+  // was made visible by that barrier. A chunk's loads have the whole MFMA phase
+  // to land. Chunks past nch are harmless (rows clamped, G = 0, never read).
+  // Scheduling barriers keep each row tile's fragment reads next to its MFMAs.
   const auto step = [&](int c) {
     const lds_char* st = lds + (c & 1) * kDwStage;
-    half8 bh[kDwWT], bl[kDwWT];
 #pragma unroll
-    for (int u = 0; u < kDwWT; ++u) {
-      bh[u] = tr_frag(st + 2 * kDwImg, 128 * wi + 16 * u, trb);
-      bl[u] = tr_frag(st + 3 * kDwImg, 128 * wi + 16 * u, trb);
+    for (int u = 0; u < NU; ++u) load_u(c + 2, u);
+    half8 bh[TI], bl[TI];
+#pragma unroll
+    for (int u = 0; u < TI; ++u) {
+      bh[u] = tr_frag(st + 2 * kDwImg, (256 / WI) * wi + 16 * u, trb);
+      bl[u] = tr_frag(st + 3 * kDwImg, (256 / WI) * wi + 16 * u, trb);
     }
     half8 ah = tr_frag(st, 128 * wo, trb), al = tr_frag(st + kDwImg, 128 * wo, trb);
 #pragma unroll
-    for (int t = 0; t < kDwWT; ++t) {
+    for (int t = 0; t < TO; ++t) {
       half8 ahn = ah, aln = al;
-      if (t + 1 < kDwWT) {
+      if (t + 1 < TO) {
         ahn = tr_frag(st, 128 * wo + 16 * (t + 1), trb);
         aln = tr_frag(st + kDwImg, 128 * wo + 16 * (t + 1), trb);
       }
+#ifndef AVR_WGRAD_NO_MFMA   // diagnostic build: the staging pipeline alone
 #pragma unroll
-      for (int u = 0; u < kDwWT; ++u) {
+      for (int u = 0; u < TI; ++u) {
         acc[t][u] = mfma32h(ah, bh[u], acc[t][u]);
         acc[t][u] = mfma32h(ah, bl[u], acc[t][u]);
         acc[t][u] = mfma32h(al, bh[u], acc[t][u]);
       }
-      if (t >= kDwWT / 2) {   // chunks past nch: harmless (rows clamped, G = 0, stage never read)
-        const int u = 2 * (t - kDwWT / 2);
-        put(c + 1, u);
-        put(c + 1, u + 1);
-        load_u(c + 2, u);
-        load_u(c + 2, u + 1);
-      }
+#else
+      acc[t][0][0] += __builtin_bit_cast(floatx4, ah)[0] + __builtin_bit_cast(floatx4, al)[1] +
+                      __builtin_bit_cast(floatx4, bh[t % TI])[2] + __builtin_bit_cast(floatx4, bl[t % TI])[3];
+#endif
       __builtin_amdgcn_sched_barrier(0);
       ah = ahn;
       al = aln;
     }
     __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NU; ++u) put(c + 2, u);
   };
 
   if (nch > 0) {
@@ -202,6 +210,8 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
     for (int u = 0; u < NU; ++u) put(0, u);
 #pragma unroll
     for (int u = 0; u < NU; ++u) load_u(1, u);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) put(1, u);
     __syncthreads();
   }
   for (int c = 0; c < nch; ++c) step(c);
@@ -210,26 +220,26 @@ __global__ void __launch_bounds__(256, 1) weight_grad_kernel(DwArgs a) {
   const float inv = (1.0f / sG) * (1.0f / sX);
   float* part = D.part + (int64_t)krange * D.O * D.I;
 #pragma unroll
-  for (int t = 0; t < kDwWT; ++t)
+  for (int t = 0; t < TO; ++t)
 #pragma unroll
-    for (int u = 0; u < kDwWT; ++u) {
-      const int i = i0 + 128 * wi + 16 * u + (lane & 15);
+    for (int u = 0; u < TI; ++u) {
+      const int i = i0 + (256 / WI) * wi + 16 * u + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = o0 + 128 * wo + 16 * t + 4 * (lane >> 4) + r;
         if (o < D.O && i < D.I) part[(int64_t)o * D.I + i] = acc[t][u][r] * inv;
       }
     }
-  // ---- partial db: the 8 row groups' column sums through LDS
+  // ---- partial db: the NW row groups' column sums through LDS
   if (bias) {
     __syncthreads();
-    float* red = lds_f;   // [4][256]
+    float* red = lds_f;   // [NW][256]
     *reinterpret_cast<floatx4*>(red + rb * kDwTile + 4 * cc) = bsum;
     __syncthreads();
     if (threadIdx.x < kDwTile && o0 + (int)threadIdx.x < D.O) {
       float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) s += red[q * kDwTile + threadIdx.x];
+      for (int q = 0; q < NW; ++q) s += red[q * kDwTile + threadIdx.x];
       D.bpart[(int64_t)krange * D.O + o0 + threadIdx.x] = s;
     }
   }
@@ -269,13 +279,18 @@ extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int
   a.tiles = tiles;
   const int64_t blocks = (int64_t)tiles * n_split;
   AVR_REQUIRE(blocks < (1ll << 31), "avr_weight_grads: too many tiles");
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess)
+  static int waves = 0;
+  if (!waves) {
+    const char* e = getenv("AVR_WGRAD_WAVES");
+    waves = (e && atoi(e) == 4) ? 4 : 8;
+    const void* k = waves == 4 ? reinterpret_cast<const void*>(&weight_grad_kernel<4>)
+                               : reinterpret_cast<const void*>(&weight_grad_kernel<8>);
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess)
       return fail(AVR_E_HIP, "weight_grad_kernel: cannot set dynamic LDS");
-    attr = true;
   }
-  weight_grad_kernel<<<(unsigned)blocks, 256, 2 * kDwStage, as_stream(stream)>>>(a);
+  if (waves == 4)
+    weight_grad_kernel<4><<<(unsigned)blocks, 256, 2 * kDwStage, as_stream(stream)>>>(a);
+  else
+    weight_grad_kernel<8><<<(unsigned)blocks, 512, 2 * kDwStage, as_stream(stream)>>>(a);
   return check_launch("weight_grad_kernel");
 }

@@ -1,10 +1,11 @@
 #!/bin/bash
-# Board power and clocks sampled once a second while the C3 bench runs (is the field kernel power-capped?).
+# Board power and clocks sampled once a second while the C3 bench (or $CMD) runs: is the kernel power-capped?
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/power; mkdir -p $OUT
-timeout -k 10 300 python bench.py --steps ${STEPS:-30} --warmup 2 --no-cpu-baseline > $OUT/bench.log 2>&1 &
+# CMD: the workload to sample (default: the C3 bench)
+timeout -k 10 300 ${CMD:-python bench.py --steps ${STEPS:-30} --warmup 2 --no-cpu-baseline} > $OUT/bench.log 2>&1 &
 pid=$!
 for i in $(seq 240); do
   echo "== t=$i" >> $OUT/smi.log
