@@ -279,16 +279,17 @@ extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int
   a.tiles = tiles;
   const int64_t blocks = (int64_t)tiles * n_split;
   AVR_REQUIRE(blocks < (1ll << 31), "avr_weight_grads: too many tiles");
-  static int waves = 0;
-  if (!waves) {
-    const char* e = getenv("AVR_WGRAD_WAVES");
-    waves = (e && atoi(e) == 4) ? 4 : 8;
-    const void* k = waves == 4 ? reinterpret_cast<const void*>(&weight_grad_kernel<4>)
-                               : reinterpret_cast<const void*>(&weight_grad_kernel<8>);
-    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess)
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel<4>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel<8>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess)
       return fail(AVR_E_HIP, "weight_grad_kernel: cannot set dynamic LDS");
+    attr = true;
   }
-  if (waves == 4)
+  const char* e = getenv("AVR_WGRAD_WAVES");   // 8 (default) or 4, read per call
+  if (e && atoi(e) == 4)
     weight_grad_kernel<4><<<(unsigned)blocks, 256, 2 * kDwStage, as_stream(stream)>>>(a);
   else
     weight_grad_kernel<8><<<(unsigned)blocks, 512, 2 * kDwStage, as_stream(stream)>>>(a);
