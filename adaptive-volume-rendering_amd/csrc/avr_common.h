@@ -229,14 +229,30 @@ __device__ __forceinline__ double wave_excl_prod_dpp(double v, double& total) {
   return dpp_d<kDppWaveShr1>(incl, 1.0);
 }
 
-// Exclusive sum scan of doubles (lane 0 gets 0).
-__device__ __forceinline__ double wave_excl_sum_dpp(double v) {
-  const double incl = wave_incl_scan_dpp(v, 0.0, [](double a, double b) { return a + b; });
-  return dpp_d<kDppWaveShr1>(incl, 0.0);
+// dpp_d with identity 0 for the shifts (row_shr, wave_shr) that name a lane for
+// every destination or none: bound_ctrl zero-fills the lanes without a source,
+// so no old value has to be materialised first.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d0(double v) {
+  const unsigned long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, true);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-__device__ __forceinline__ double wave_total_sum_dpp(double v) {
-  return readlane_d(wave_incl_scan_dpp(v, 0.0, [](double a, double b) { return a + b; }), 63);
+__device__ __forceinline__ double wave_incl_sum_dpp(double v) {
+  v += dpp_d0<kDppRowShr1>(v);
+  v += dpp_d0<kDppRowShr2>(v);
+  v += dpp_d0<kDppRowShr4>(v);
+  v += dpp_d0<kDppRowShr8>(v);
+  v += dpp_d<kDppRowBcast15, 0xa>(v, 0.0);
+  v += dpp_d<kDppRowBcast31, 0xc>(v, 0.0);
+  return v;
 }
+
+// Exclusive sum scan of doubles (lane 0 gets 0).
+__device__ __forceinline__ double wave_excl_sum_dpp(double v) { return dpp_d0<kDppWaveShr1>(wave_incl_sum_dpp(v)); }
+
+__device__ __forceinline__ double wave_total_sum_dpp(double v) { return readlane_d(wave_incl_sum_dpp(v), 63); }
 
 }  // namespace avr

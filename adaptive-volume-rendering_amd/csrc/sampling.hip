@@ -470,7 +470,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
     wave_sync();   // the unsorted fine list is read by nobody past this point
     if (lane < Nf) {
       B[lane] = bf;
-      const float t = fmul(fsub(bf, near_), (float)Nc / span);
+      const float t = (bf - near_) * ((float)Nc * __builtin_amdgcn_rcpf(span));   // a guess: verified below
       const int g = t > 0.f ? (t < (float)Nc ? (int)t : Nc) : 0;
       marks[lane + count_below_near<false>(A, Nc, bf, g)] = 1;
     }
@@ -503,7 +503,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
     }
     if (lane < Nf) {
       // stratified coarse lists put #{A <= bf} within a step of bf's bin
-      const float t = fmul(fsub(bf, near_), (float)Nc / span);
+      const float t = (bf - near_) * ((float)Nc * __builtin_amdgcn_rcpf(span));   // a guess: verified below
       const int g = t > 0.f ? (t < (float)Nc ? (int)t : Nc) : 0;
       obuf[lane + count_below_near<false>(A, Nc, bf, g) + count_below<true>(D, Nd, bf)] = bf;
     }
