@@ -396,7 +396,11 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       __syncthreads();
       AVR_STAMP(30);
       mx = 0.f;
+#ifndef AVR_DIAG_NO_BLEND   // timing-only diagnostic: the lin_z blend skipped (wrong results)
       blend_stage<FT, true, !TWO>(h, v, mx, stage, tail, 0, D, P::RS, S_h, 1.0f / S_h, wid, g, j);
+#else
+      mx = max_relu_affine<FT, false>(h, 1.0f / S_h, bz);
+#endif
       mx = wave_max(mx);
     } else {
       for (int lo = 0; b < a.n_lin_z && lo < D; lo += P::CAP) {   // more distinct texels than the stage holds
