@@ -8,7 +8,9 @@
 //   pdf = w'/s (IEEE), cdf = [0, fp64 prefix sum] (wave scan; the fp64 partial
 //   sums of these fp32 terms are exact, so the scan order cannot change a bit),
 //   idx = #{cdf <= u} - 1 by binary search, z = near + (far-near)*((idx+u2)/Nc),
-//   then a bitonic sort of [z_coarse | z_fine | z_depth] padded to 2^k with +inf.
+//   then the values-only merge of [z_coarse | z_fine | z_depth] (register
+//   bitonic sorts of the short lists + slot ranks; a wave-local bitonic sort of
+//   the list padded to 2^k with +inf when z_coarse is not ascending).
 #include <float.h>
 
 #include "avr_common.h"
@@ -357,7 +359,9 @@ __device__ __forceinline__ int count_below_near(const float* L, int n, float x, 
 //      fine and depth lists are sorted in registers and the three sorted lists
 //      merged by rank (own index + counts below in the other lists, ties broken
 //      coarse < fine < depth; a fine value's count in the coarse list starts
-//      from its stratified bin); otherwise a wave-local bitonic sort.
+//      from its stratified bin; with no depth samples, the coarse values fill
+//      the slots the fine values leave, in order); otherwise a wave-local
+//      bitonic sort.
 // NC, NF, ND > 0: the sample counts as compile-time constants (the renderer's
 // 128 -> 64 shape: loops unrolled, no loop or exec-mask bookkeeping); 0: runtime.
 template <bool POW2, int NC = 0, int NF = 0, int ND = 0>
