@@ -672,6 +672,13 @@ def main():
             "field_share_of_step": round(field_ms / (elapsed * 1e3), 4),
         },
     }
+    if args.precision == "x3":
+        # context, not the contract's peak: back-to-back 16x16x32 fp16 MFMAs with random operands are held by
+        # the board's power limit to ~1.87 PFLOP/s (1.32 kW, 1.85-1.95 GHz; profiles/r02_mfma_power_probe.txt)
+        pl = 1868.0 / 3.0
+        line["roofline"]["power_limited_peak"] = {
+            "value": round(pl, 1), "unit": "TFLOP/s", "frac": round(achieved_tflops / pl, 4),
+            "source": "profiles/r02_mfma_power_probe.txt (scripts/probe/mfma_probe.hip, random fp16 operands) / 3"}
     # the renderer's HBM-bound kernels (the metric's "achieved HBM GB/s vs roofline"), HIP events per launch,
     # against the 8 TB/s peak and against what a device copy reaches on this box
     ach = achievable_hbm_gbs(device)
