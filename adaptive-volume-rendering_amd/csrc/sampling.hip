@@ -333,16 +333,22 @@ __device__ __forceinline__ float bitonic_from(float v, int lane) {
 // min/max choice by a constant lane mask.
 __device__ __forceinline__ float wave_sort64(float v, int lane) { return bitonic_from<2>(v, lane); }
 
-// count_below over the sorted list L[0..n) starting from a guess g of the
-// answer: when L[g-2] and L[g+2] bracket x (checked), a 2-step search of the
-// window; otherwise the full binary search. Exact either way.
+// count_below over the sorted list L[0..n) from a guess g of the answer: when
+// L[g-2] and L[g+2] bracket x (checked), the count is g - 1 plus the entries
+// of the window [g-1, g+2) that pass — five independent reads instead of a
+// dependent search chain; otherwise the full binary search. Exact either way.
 template <bool LT>
 __device__ __forceinline__ int count_below_near(const float* L, int n, float x, int g) {
-  const int lo = g - 2 < 0 ? 0 : (g - 2 > n ? n : g - 2);
+  const auto pass = [&](float v) { return LT ? v < x : v <= x; };
+  const int lo = g - 1 < 0 ? 0 : (g - 1 > n ? n : g - 1);
   const int hi = g + 2 > n ? n : (g + 2 < lo ? lo : g + 2);
-  const bool below_lo = lo == 0 || (LT ? L[lo - 1] < x : L[lo - 1] <= x);   // every index < lo counts
-  const bool above_hi = hi == n || !(LT ? L[hi] < x : L[hi] <= x);          // no index >= hi counts
-  if (below_lo && above_hi) return lo + count_below<LT>(L + lo, hi - lo, x);
+  const int last = n - 1;
+  const float before = L[lo > 0 ? lo - 1 : 0], after = L[hi < n ? hi : last];
+  const float w0 = L[lo < last ? lo : last], w1 = L[lo + 1 < last ? lo + 1 : last], w2 = L[lo + 2 < last ? lo + 2 : last];
+  const bool below_lo = lo == 0 || pass(before);   // every index < lo counts
+  const bool above_hi = hi == n || !pass(after);   // no index >= hi counts
+  const int c = lo + (lo < hi && pass(w0)) + (lo + 1 < hi && pass(w1)) + (lo + 2 < hi && pass(w2));
+  if (below_lo && above_hi) return c;
   return count_below<LT>(L, n, x);
 }
 
@@ -371,7 +377,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
     const float* __restrict__ nd_in, uint64_t seed, uint64_t offset, const int64_t* __restrict__ ray_ids, int sort_n,
     float* __restrict__ z_sorted, int32_t* __restrict__ idx_out, float* __restrict__ z_fine_out) {
   extern __shared__ float lds[];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wid, ray: scalars
   const int64_t ray = (int64_t)blockIdx.x * kFineWaves + wid;
   if (ray >= n_rays) return;  // wave-uniform
   const int Nc = NC ? NC : Nc_, Nf = NC ? NF : Nf_, Nd = NC ? ND : Nd_;
