@@ -394,15 +394,26 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
   const float* w = weights + ray * Nc;
   const float* zc = z_coarse + ray * Nc;
   bool coarse_sorted = true;
+  float wv[kMaxK], zv[kMaxK];
+#pragma unroll
+  for (int m = 0; m < kMaxK; ++m) {
+    const int k = lane + 64 * m;
+    wv[m] = k < Nc ? w[k] : 0.f;
+    zv[m] = k < Nc ? zc[k] : 0.f;
+  }
+  // the in-kernel (u, u2) draw of this lane's fine sample does not depend on
+  // the weights: it runs while their loads are in flight (one sample per lane)
+  float4 draw = {0.f, 0.f, 0.f, 0.f};
+  if (!u_in && Nf <= 64 && lane < Nf) draw = philox_uniform4(seed, key, (uint32_t)lane, kStreamFine);
   float xr[kMaxK];
 #pragma unroll
   for (int m = 0; m < kMaxK; ++m) {
     const int k = lane + 64 * m;
     xr[m] = 0.f;
     if (k < Nc) {
-      xr[m] = fadd(w[k], 1e-5f);
+      xr[m] = fadd(wv[m], 1e-5f);
       cdf[1 + k] = xr[m];
-      sbuf[k] = zc[k];
+      sbuf[k] = zv[m];
     }
   }
   float s;
@@ -444,7 +455,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
       u = u_in[ray * Nf + f];
       u2 = u2_in[ray * Nf + f];
     } else {
-      const float4 v = philox_uniform4(seed, key, (uint32_t)f, kStreamFine);
+      const float4 v = Nf <= 64 ? draw : philox_uniform4(seed, key, (uint32_t)f, kStreamFine);
       u = v.x;
       u2 = v.y;
     }
