@@ -107,8 +107,8 @@ __global__ void __launch_bounds__(256) sample_coarse_rays_kernel(const float* __
 
 // get_world_rays (utils.py:315-336) + sample_coarse (renderers.py:4-24) in one
 // launch, plus each ray's depth row for the composite epilogue. A workgroup
-// owns kRaysPerBlock consecutive rays: wave 0 builds ro, rd with one lane per
-// ray (and, if asked, row 2 of inverse(cam2world) in fp64: depth = -(row .
+// owns kRaysPerBlock (64) consecutive rays: wave 0 builds ro, rd with one lane
+// per ray (and, if asked, row 2 of inverse(cam2world) in fp64: depth = -(row .
 // [x, 1]), utils.py:358-361) while waves 1-3 write the rays' z in 4-sample
 // quads, consecutive threads on consecutive quads (coalesced 16-B stores): z
 // does not depend on the geometry, so the fp64 latency of wave 0 overlaps the
@@ -126,13 +126,16 @@ __global__ void __launch_bounds__(256) rays_coarse_kernel(
   const int64_t r0 = (int64_t)blockIdx.x * kRaysPerBlock;
   const float span = fsub(far_, near_);
   const float inv_n = 1.0f / (float)n;
-  const bool tab = n <= kCoarseTab;
-  if (tab)
+  // a power-of-two count computes near + span * (s / n) directly (an exact
+  // scaling, no table and no barrier); otherwise the table saves a division
+  const bool tab = !POW2 && n <= kCoarseTab;
+  if (tab) {
     for (int s = threadIdx.x; s < n; s += blockDim.x)
       base_tab[s] = fadd(near_, fmul(span, div_count<POW2>((float)s, (float)n, inv_n)));
-  __syncthreads();   // base_tab
-  if (threadIdx.x < kRaysPerBlock) {
-    if (r0 + threadIdx.x >= total) return;
+    __syncthreads();   // base_tab
+  }
+  if (threadIdx.x < 64) {   // wave 0: the rays' geometry, one lane per ray
+    if (threadIdx.x >= kRaysPerBlock || r0 + threadIdx.x >= total) return;
     const int64_t i = r0 + threadIdx.x;
     const int64_t sb = i / n_rays, r = i - sb * n_rays;
     double k[3][3], ki[3][3];
@@ -174,7 +177,7 @@ __global__ void __launch_bounds__(256) rays_coarse_kernel(
   const int lg_nq = POW2 && n >= 4 ? __builtin_ctz((unsigned)nq) : 0;   // nq a power of two too
   const int64_t nr_blk = total - r0 < kRaysPerBlock ? total - r0 : kRaysPerBlock;
   const int items = (int)nr_blk * nq;
-  for (int it = threadIdx.x - kRaysPerBlock; it < items; it += blockDim.x - kRaysPerBlock) {
+  for (int it = threadIdx.x - 64; it < items; it += blockDim.x - 64) {   // waves 1-3: z
     const int rl = POW2 && n >= 4 ? it >> lg_nq : it / nq, q = it - rl * nq;
     const int64_t ray = r0 + rl;
     float u[4];
