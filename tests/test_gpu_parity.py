@@ -170,6 +170,29 @@ def test_sample_coarse_ragged_bit_exact(N):
     torch.testing.assert_close(u_n, u_64[:, :N], atol=2e-5, rtol=0)
 
 
+@pytest.mark.parametrize("R", [1, 3, 1001])
+@pytest.mark.parametrize("Nc,Nf,Nd", [(128, 64, 0), (64, 32, 16)])
+def test_sample_fine_partial_workgroup(R, Nc, Nf, Nd):
+    """Ray counts that leave the last workgroup (4 rays) partly empty, for the
+    compile-time-size path (128 -> 64) and the runtime one: indices, fine z and
+    the merge bit-exact against the oracle."""
+    from avr import ops
+    rng = np.random.default_rng(R + Nc)
+    zc = np.sort(rng.uniform(0.8, 1.8, (R, Nc)).astype(np.float32), -1)
+    w = rng.random((R, Nc), dtype=np.float32)
+    u, u2 = rng.random((R, Nf), dtype=np.float32), rng.random((R, Nf), dtype=np.float32)
+    nd = rng.normal(0, 1, (R, Nd)).astype(np.float32)
+    zs, idx, zf = ops.sample_fine(T(w), T(zc), 0.8, 1.8, Nf, Nd, 0.01, u=T(u), u2=T(u2), noise_depth=T(nd),
+                                  want_idx=True, want_fine=True)
+    oz, oidx = O.sample_fine(np.full((1, R), 0.8, np.float32), np.full((1, R), 1.8, np.float32), Nf, w[None, ..., None],
+                             u[None], u2[None], return_idx=True)
+    np.testing.assert_array_equal(to_np(idx), oidx[0])
+    np.testing.assert_array_equal(to_np(zf), oz[0])
+    od = np.clip(O.sample_depth(np.zeros((1, R, 1), np.float32), Nd, 0.01, nd[None]), np.float32(0.8),
+                 np.float32(1.8))[0]
+    np.testing.assert_array_equal(to_np(zs), np.sort(np.concatenate([zc, oz[0], od], -1), -1))
+
+
 def test_sample_fine_merge_ties():
     """Coarse values equal to fine values (n_depth 0: the two-list slot merge):
     every slot filled once, the output equals numpy's sort."""
