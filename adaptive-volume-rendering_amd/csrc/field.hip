@@ -141,7 +141,9 @@ __global__ void pack_x3_kernel(const float* __restrict__ W, int out_dim, int in_
 // acc[ot] += sum_t sum_r A(ot,t,r) B(t,r); A from packed global [t][ot][lane]
 // through a P-deep register ring that runs ahead across t iterations, B from
 // the wave's LDS slab [t][lane].
-template <int NT, int P>
+// NTOT: output tiles per K tile in the packed layout (NT < NTOT: this call
+// computes the NT tiles starting at W, a slice of them)
+template <int NT, int P, int NTOT = NT>
 __device__ __forceinline__ void gemm_tiles(floatx4 (&acc)[NT], const floatx4* __restrict__ W, int KT,
                                            const floatx4* slab, int lane) {
   static_assert(NT % P == 0 && P % 2 == 0, "ring must divide the tile count");
@@ -151,8 +153,8 @@ __device__ __forceinline__ void gemm_tiles(floatx4 (&acc)[NT], const floatx4* __
   for (int p = 0; p < P; ++p) ring[p] = wl[p * 64];
   for (int t = 0; t < KT; ++t) {
     const floatx4 bv = slab[t * 64 + lane];
-    const floatx4* cur = wl + (int64_t)t * NT * 64;
-    const floatx4* nxt = wl + (int64_t)(t + 1 < KT ? t + 1 : t) * NT * 64;
+    const floatx4* cur = wl + (int64_t)t * NTOT * 64;
+    const floatx4* nxt = wl + (int64_t)(t + 1 < KT ? t + 1 : t) * NTOT * 64;
 #pragma unroll
     for (int ot = 0; ot < NT; ot += 2) {
       const floatx4 a0 = ring[ot % P];
@@ -301,6 +303,42 @@ __global__ void __launch_bounds__(256, 1) latent_table_kernel(const float* __res
   }
 }
 
+// The same table with the output tiles split over the workgroup's waves
+// (NT >= 8): a workgroup owns 16 texels, their latent columns are staged in
+// LDS once (32 KB at d_latent 512) and wave w computes output tiles
+// [w NT/4, (w+1) NT/4). Four times the workgroups of latent_table_kernel at a
+// quarter of the LDS each, so a 4096-texel table fills the chip.
+template <int NT>
+__global__ void __launch_bounds__(256) latent_table_split_kernel(const float* __restrict__ packed, Layout L,
+                                                                 const float* __restrict__ latent, int HW,
+                                                                 float* __restrict__ table) {
+  constexpr int NWT = NT / kFieldWaves;          // output tiles per wave
+  constexpr int P = NWT >= 16 ? 16 : NWT;
+  extern __shared__ floatx4 lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y;
+  const int64_t texel = (int64_t)blockIdx.x * kSPW + j;
+  const bool valid = texel < HW;
+  const int64_t tx = valid ? texel : HW - 1;
+  for (int t = wid; t < L.KTl; t += kFieldWaves) {
+    const int c0 = 16 * t + 4 * g;
+    lds[t * 64 + lane] = floatx4{latent[(int64_t)c0 * HW + tx], latent[(int64_t)(c0 + 1) * HW + tx],
+                                 latent[(int64_t)(c0 + 2) * HW + tx], latent[(int64_t)(c0 + 3) * HW + tx]};
+  }
+  __syncthreads();
+  floatx4 acc[NWT];
+#pragma unroll
+  for (int ot = 0; ot < NWT; ++ot) acc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+  gemm_tiles<NWT, P, NT>(acc, reinterpret_cast<const floatx4*>(packed + L.lin_z[b]) + NWT * wid * 64, L.KTl, lds,
+                         lane);
+  if (valid) {
+    float* dst = table + ((int64_t)b * HW + texel) * (NT * 16) + 16 * NWT * wid + 4 * g;
+#pragma unroll
+    for (int ot = 0; ot < NWT; ++ot) *reinterpret_cast<floatx4*>(dst + 16 * ot) = acc[ot];
+  }
+}
+
 // ----------------------------------------------------------------- host side
 static int pack_linear(const float* W, int out_dim, int in_dim, int NTo, int KTi, float* dst, hipStream_t s) {
   AVR_REQUIRE(W, "avr_field_pack: null weight tensor");
@@ -350,6 +388,15 @@ static int launch_field(const FieldArgs& a, hipStream_t s) {
 template <int NT>
 static int launch_table(const float* packed, const Layout& L, const float* latent, int HW, int n_lin_z,
                         float* table, hipStream_t s) {
+  if constexpr (NT >= 8) {
+    const size_t shm = (size_t)L.KTl * 64 * sizeof(floatx4);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&latent_table_split_kernel<NT>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
+      return fail(AVR_E_HIP, "latent_table_split_kernel: cannot set dynamic LDS to %zu", shm);
+    dim3 grid((HW + kSPW - 1) / kSPW, n_lin_z);
+    latent_table_split_kernel<NT><<<grid, 64 * kFieldWaves, shm, s>>>(packed, L, latent, HW, table);
+    return check_launch("latent_table_split_kernel");
+  }
   const size_t shm = (size_t)kFieldWaves * L.KTl * 64 * sizeof(floatx4);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&latent_table_kernel<NT>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
