@@ -100,15 +100,6 @@ __global__ void pack_bias_kernel(const float* __restrict__ a, const float* __res
   dst[i] = (i < n) ? (b ? fadd(a[i], b[i]) : a[i]) : 0.f;
 }
 
-// max|W| of one layer as float bits (atomicMax on non-negative floats = on their bits)
-__global__ void absmax_kernel(const float* __restrict__ W, int64_t n, unsigned* __restrict__ out) {
-  float m = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(W[i]));
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
-}
 
 // x3 fragments: dst[((c*FTt + ft)*2 + {0, 1})*512 + 8l + e] = (hi, lo) of
 // (a tile's 64 hi lanes, then its 64 lo lanes: each 16-B-per-lane load of one
@@ -116,11 +107,9 @@ __global__ void absmax_kernel(const float* __restrict__ W, int64_t n, unsigned* 
 // W[16ft + (l&15)][32c + (e<4 ? 4g+e : 16+4g+e-4)] * s_w, g = l>>4, with
 // s_w = 2^(14 - ceil-exponent of max|W|) from the layer's header word.
 // (rs, cs) = element strides of W's rows / columns: (in_dim, 1) for W, (1, ld) for W^T.
-__global__ void pack_x3_kernel(const float* __restrict__ W, int out_dim, int in_dim, int64_t rs, int64_t cs, int KC,
-                               int FTt, const unsigned* __restrict__ maxbits, _Float16* __restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n = (int64_t)KC * FTt * 64 * 8;
-  if (i >= n) return;
+__device__ __forceinline__ void pack_x3_elem(const float* __restrict__ W, int out_dim, int in_dim, int64_t rs,
+                                             int64_t cs, int FTt, const unsigned* __restrict__ maxbits,
+                                             _Float16* __restrict__ dst, int64_t i) {
   const int e = (int)(i & 7);
   const int l = (int)((i >> 3) & 63);
   const int64_t blk = i >> 9;
@@ -135,6 +124,38 @@ __global__ void pack_x3_kernel(const float* __restrict__ W, int out_dim, int in_
   const int64_t base = ((int64_t)c * FTt + ft) * 2 * 64 * 8 + l * 8;
   dst[base + e] = hi;
   dst[base + 64 * 8 + e] = lo;
+}
+
+// Every layer of a pack in two launches (max |W| of each layer, then its
+// fragments; blockIdx.y = layer) instead of two per layer: the weight pack
+// runs in every training step.
+struct X3PackJob {
+  const float* W;
+  unsigned* maxbits;
+  _Float16* dst;
+  int64_t rs, cs, nw, n;
+  int out_dim, in_dim, FTt;
+};
+struct X3PackBatch {
+  X3PackJob j[kX3MaxLayers];
+  int count;
+};
+
+// max|W| of each layer as float bits (atomicMax on non-negative floats = on their bits)
+__global__ void absmax_batch_kernel(X3PackBatch b) {
+  const X3PackJob& J = b.j[blockIdx.y];
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < J.nw; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(J.W[i]));
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(J.maxbits, __float_as_uint(m));
+}
+
+__global__ void pack_x3_batch_kernel(X3PackBatch b) {
+  const X3PackJob& J = b.j[blockIdx.y];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < J.n; i += (int64_t)gridDim.x * blockDim.x)
+    pack_x3_elem(J.W, J.out_dim, J.in_dim, J.rs, J.cs, J.FTt, J.maxbits, J.dst, i);
 }
 
 // ----------------------------------------------------------------- fp32 MFMA tiles
@@ -347,19 +368,40 @@ static int pack_linear(const float* W, int out_dim, int in_dim, int NTo, int KTi
   return check_launch("pack_linear_kernel");
 }
 
-static int pack_x3(const float* W, int out_dim, int in_dim, int KC, int FTt, unsigned* maxbits, float* dst,
-                   hipStream_t s, bool transpose = false) {
+// one layer into a batch (W is (out_dim, in_dim) row-major; transpose: (in_dim,
+// out_dim), and the fragments hold W^T)
+static int add_x3(X3PackBatch& bt, const float* W, int out_dim, int in_dim, int KC, int FTt, unsigned* maxbits,
+                  float* dst, bool transpose = false) {
   AVR_REQUIRE(W, "avr_field_pack: null weight tensor");
-  const int64_t nw = (int64_t)out_dim * in_dim;
-  absmax_kernel<<<(unsigned)((nw + 255) / 256 < 256 ? (nw + 255) / 256 : 256), 256, 0, s>>>(W, nw, maxbits);
-  int rc = check_launch("absmax_kernel");
+  AVR_REQUIRE(bt.count < kX3MaxLayers, "avr_field_pack: too many layers");
+  X3PackJob& J = bt.j[bt.count++];
+  J.W = W;
+  J.maxbits = maxbits;
+  J.dst = reinterpret_cast<_Float16*>(dst);
+  J.rs = transpose ? 1 : in_dim;
+  J.cs = transpose ? out_dim : 1;
+  J.nw = (int64_t)out_dim * in_dim;
+  J.n = (int64_t)KC * FTt * 64 * 8;
+  J.out_dim = out_dim;
+  J.in_dim = in_dim;
+  J.FTt = FTt;
+  return AVR_OK;
+}
+
+static int run_x3(const X3PackBatch& bt, hipStream_t s) {
+  if (bt.count == 0) return AVR_OK;
+  int64_t nw = 0, n = 0;
+  for (int k = 0; k < bt.count; ++k) {
+    nw = bt.j[k].nw > nw ? bt.j[k].nw : nw;
+    n = bt.j[k].n > n ? bt.j[k].n : n;
+  }
+  const unsigned ga = (unsigned)((nw + 255) / 256 < 256 ? (nw + 255) / 256 : 256);
+  absmax_batch_kernel<<<dim3(ga, bt.count), 256, 0, s>>>(bt);
+  int rc = check_launch("absmax_batch_kernel");
   if (rc) return rc;
-  const int64_t n = (int64_t)KC * FTt * 64 * 8;
-  // transpose: W is (in_dim, out_dim) row-major and the fragments hold W^T
-  const int64_t rs = transpose ? 1 : in_dim, cs = transpose ? out_dim : 1;
-  pack_x3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(W, out_dim, in_dim, rs, cs, KC, FTt, maxbits,
-                                                            reinterpret_cast<_Float16*>(dst));
-  return check_launch("pack_x3_kernel");
+  const unsigned gp = (unsigned)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024);
+  pack_x3_batch_kernel<<<dim3(gp, bt.count), 256, 0, s>>>(bt);
+  return check_launch("pack_x3_batch_kernel");
 }
 
 static int pack_bias(const float* a, const float* b, int n, int n_pad, float* dst, hipStream_t s) {
@@ -486,13 +528,14 @@ extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_wei
   unsigned* hdr = reinterpret_cast<unsigned*>(packed + L.x3_hdr);
   if (hipMemsetAsync(hdr, 0, 64 * sizeof(float), s) != hipSuccess) return fail(AVR_E_HIP, "avr_field_pack: memset");
   const int KC = H / 32;
-  if ((rc = pack_x3(w->lin_in_w, H, dims->d_in, kX3InChunks, NT, hdr + 0, packed + L.x3_in, s))) return rc;
-  if ((rc = pack_x3(w->lin_out_w, 4, H, KC, 1, hdr + 1, packed + L.x3_out, s))) return rc;
+  X3PackBatch bt{};
+  if ((rc = add_x3(bt, w->lin_in_w, H, dims->d_in, kX3InChunks, NT, hdr + 0, packed + L.x3_in))) return rc;
+  if ((rc = add_x3(bt, w->lin_out_w, 4, H, KC, 1, hdr + 1, packed + L.x3_out))) return rc;
   for (int b = 0; b < dims->n_blocks; ++b) {
-    if ((rc = pack_x3(w->fc0_w[b], H, H, KC, NT, hdr + 2 + 2 * b, packed + L.x3_fc0[b], s))) return rc;
-    if ((rc = pack_x3(w->fc1_w[b], H, H, KC, NT, hdr + 3 + 2 * b, packed + L.x3_fc1[b], s))) return rc;
+    if ((rc = add_x3(bt, w->fc0_w[b], H, H, KC, NT, hdr + 2 + 2 * b, packed + L.x3_fc0[b]))) return rc;
+    if ((rc = add_x3(bt, w->fc1_w[b], H, H, KC, NT, hdr + 3 + 2 * b, packed + L.x3_fc1[b]))) return rc;
   }
-  return AVR_OK;
+  return run_x3(bt, s);
 }
 
 extern "C" int avr_field_bwd_packed_floats(const avr_field_dims* dims, int64_t* n_floats) {
@@ -518,11 +561,12 @@ extern "C" int avr_field_pack_bwd(const avr_field_dims* dims, const avr_resnetfc
   unsigned* hdr = reinterpret_cast<unsigned*>(packed_bwd);
   if (hipMemsetAsync(hdr, 0, 64 * sizeof(float), s) != hipSuccess) return fail(AVR_E_HIP, "avr_field_pack_bwd: memset");
   const int H = dims->d_hidden, KC = H / 32, NT = H / 16;
+  X3PackBatch bt{};
   for (int b = 0; b < dims->n_blocks; ++b) {
-    if ((rc = pack_x3(w->fc0_w[b], H, H, KC, NT, hdr + 2 + 2 * b, packed_bwd + LB.fc0t[b], s, true))) return rc;
-    if ((rc = pack_x3(w->fc1_w[b], H, H, KC, NT, hdr + 3 + 2 * b, packed_bwd + LB.fc1t[b], s, true))) return rc;
+    if ((rc = add_x3(bt, w->fc0_w[b], H, H, KC, NT, hdr + 2 + 2 * b, packed_bwd + LB.fc0t[b], true))) return rc;
+    if ((rc = add_x3(bt, w->fc1_w[b], H, H, KC, NT, hdr + 3 + 2 * b, packed_bwd + LB.fc1t[b], true))) return rc;
   }
-  return AVR_OK;
+  return run_x3(bt, s);
 }
 
 extern "C" int avr_field_train_sizes(const avr_field_dims* dims, int n_scenes, int64_t n_points, int64_t* act_floats,
