@@ -142,14 +142,19 @@ struct X3PackBatch {
 };
 
 // max|W| of each layer as float bits (atomicMax on non-negative floats = on their bits)
+// (one atomic per workgroup: a few dozen per layer, not one per wave)
 __global__ void absmax_batch_kernel(X3PackBatch b) {
+  __shared__ float wm[4];
   const X3PackJob& J = b.j[blockIdx.y];
   float m = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < J.nw; i += (int64_t)gridDim.x * blockDim.x)
     m = fmaxf(m, fabsf(J.W[i]));
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(J.maxbits, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(J.maxbits, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
 }
 
 __global__ void pack_x3_batch_kernel(X3PackBatch b) {
@@ -395,7 +400,7 @@ static int run_x3(const X3PackBatch& bt, hipStream_t s) {
     nw = bt.j[k].nw > nw ? bt.j[k].nw : nw;
     n = bt.j[k].n > n ? bt.j[k].n : n;
   }
-  const unsigned ga = (unsigned)((nw + 255) / 256 < 256 ? (nw + 255) / 256 : 256);
+  const unsigned ga = (unsigned)((nw + 4095) / 4096 < 64 ? (nw + 4095) / 4096 : 64);   // >= 16 values per thread
   absmax_batch_kernel<<<dim3(ga, bt.count), 256, 0, s>>>(bt);
   int rc = check_launch("absmax_batch_kernel");
   if (rc) return rc;
