@@ -506,7 +506,7 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
       const uint64_t mask = __ballot(fine);
       const int before = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-      if (k < Ntot) out[k] = fine ? B[before] : A[k - before];
+      if (k < Ntot) out[k] = sbuf[fine ? Nc + before : k - before];   // B[before] or A[k - before]: one read
       base += __popcll(mask);
     }
     return;
