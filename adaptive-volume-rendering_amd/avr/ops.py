@@ -425,3 +425,14 @@ def latent_features(view, latent_chw, xyz, out=None):
     require_device(lat, xyz, out)
     call("avr_latent_features", ctypes.byref(view), ptr(lat), C, ptr(xyz), n, ptr(out), stream_of(xyz))
     return out
+
+
+def stream_copy(src, dst):
+    """dst <- src (same byte size, 16-B aligned): the streaming copy kernel
+    bench.py uses as its achievable-HBM yardstick (avr_stream_copy)."""
+    require_device(src, dst)
+    nb = src.numel() * src.element_size()
+    if nb != dst.numel() * dst.element_size():
+        raise _lib.AVRError("stream_copy: size mismatch")
+    call("avr_stream_copy", ptr(src), ptr(dst), nb, stream_of(src))
+    return dst

@@ -38,18 +38,23 @@ def broadcast_scene(net, src=0, group=None):
 
 
 def _takes_ray_ids(fn):
+    """True when fn names both `ray_ids` and `n_rays_total` as parameters (a
+    bare **kwargs does not count: it may forward to something that does not
+    take them)."""
     try:
         params = inspect.signature(fn).parameters
     except (TypeError, ValueError):
         return False
-    return "ray_ids" in params or any(p.kind == p.VAR_KEYWORD for p in params.values())
+    return "ray_ids" in params and "n_rays_total" in params
 
 
-def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None):
+def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None, pass_ray_ids=None):
     """render_fn(cam2world, intrinsics, x_pix[, ray_ids=, n_rays_total=]) ->
     (rgb_c, rgb_f, depth, depth) on this rank's tiles; returns the full-frame
-    outputs on every rank. A render_fn that accepts `ray_ids` (a
-    VolumeRenderer call) gets the frame-wide index of each of its rays.
+    outputs on every rank. The frame-wide index of each of the rank's rays is
+    passed as `ray_ids` (with `n_rays_total`) when pass_ray_ids is True, or,
+    by default (None), when render_fn declares both parameters (a
+    VolumeRenderer call: its Philox draws then match the single-GPU frame).
     cam2world (SB,R,4,4) may be a stride-0 expand; x_pix (SB,R,2)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -59,7 +64,7 @@ def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None)
     c2w_local = cam2world if cam2world.shape[1] == 1 else cam2world[:, idx]
     if c2w_local.shape[1] == 1 and idx.numel() != 1:
         c2w_local = c2w_local.expand(SB, idx.numel(), 4, 4)
-    if _takes_ray_ids(render_fn):
+    if pass_ray_ids if pass_ray_ids is not None else _takes_ray_ids(render_fn):
         # frame-wide ray indices: the renderer's Philox draws then match the single-GPU render of the frame
         rgb_c, rgb_f, depth, _ = render_fn(c2w_local, intrinsics, x_pix[:, idx].contiguous(), ray_ids=idx,
                                            n_rays_total=R)

@@ -98,7 +98,8 @@ def main(argv=None):
             if dist is None:
                 return rend(c2w, K, x_pix, net)
             if isinstance(rend, VolumeRenderer):   # Philox keyed by frame-wide ray ids
-                return render_sharded(lambda c, k, x, **ids: rend(c, k, x, net, **ids), c2w, K, x_pix)
+                return render_sharded(lambda c, k, x, **ids: rend(c, k, x, net, **ids), c2w, K, x_pix,
+                                      pass_ray_ids=True)
             return render_sharded(lambda c, k, x: rend(c, k, x, net), c2w, K, x_pix)
 
     for i in range(args.warmup):

@@ -155,12 +155,41 @@ class HbmKernelTimer:
         self._wrap("depth_from_world_fwd", "depth_kernel", lambda a, k, out: (a[0].shape[0] * a[0].shape[1] * 32, ""))
 
     @staticmethod
-    def _replay_us(fn, a, k, reps):
+    def _input_sets(a, k, min_bytes, max_sets):
+        """Copies of one launch's device inputs, enough sets that they span
+        min_bytes together (more than the 256 MB Infinity Cache, so replayed
+        launches read HBM, not MALL hits). Stride-0 views (a broadcast pose)
+        are shared, not materialised."""
+        def tensors(x):
+            return [t for t in x if isinstance(t, torch.Tensor) and t.is_cuda]
+        nb = sum(t.numel() * t.element_size() for t in tensors(list(a) + list(k.values())))
+        n = max(1, min(max_sets, -(-min_bytes // max(nb, 1))))
+
+        def clone(x):
+            if isinstance(x, torch.Tensor) and x.is_cuda and 0 not in x.stride():
+                return x.clone()
+            return x
+        sets = [(a, k)] + [(tuple(clone(x) for x in a), {kk: clone(v) for kk, v in k.items()}) for _ in range(n - 1)]
+        return sets, nb
+
+    @classmethod
+    def _replay_us(cls, fn, a, k, reps, min_bytes):
         """Average launch duration: `reps` launches captured in one HIP graph
-        (no host launch gaps between them), or plain back-to-back launches if
-        capture is refused."""
-        fn(*a, **k)
+        (no host launch gaps between them) cycling over input copies that span
+        min_bytes, every launch writing outputs of its own (kept alive during
+        the capture); plain back-to-back launches if capture is refused."""
+        sets, in_b = cls._input_sets(a, k, min_bytes, reps)
+        n_sets = len(sets)
+        keep = []
+
+        def launch(i):
+            aa, kk = sets[i % len(sets)]
+            keep.append(fn(*aa, **kk))
+
+        for i in range(len(sets)):
+            launch(i)
         torch.cuda.synchronize()
+        keep.clear()
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         try:
@@ -169,8 +198,8 @@ class HbmKernelTimer:
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 with torch.cuda.graph(g, stream=side):
-                    for _ in range(reps):
-                        fn(*a, **k)
+                    for i in range(reps):
+                        launch(i)
             torch.cuda.current_stream().wait_stream(side)
             g.replay()
             torch.cuda.synchronize()
@@ -178,43 +207,56 @@ class HbmKernelTimer:
             g.replay()
             e.record()
         except Exception:  # noqa: BLE001 -- capture refused: time plain launches
+            keep.clear()
             torch.cuda.synchronize()
             s.record()
-            for _ in range(reps):
-                fn(*a, **k)
+            for i in range(reps):
+                launch(i)
             e.record()
         e.synchronize()
-        return s.elapsed_time(e) * 1e3 / reps
+        us = s.elapsed_time(e) * 1e3 / reps
+        keep.clear()
+        del sets
+        torch.cuda.empty_cache()
+        return us, n_sets, in_b
 
-    def report(self, reps=20, achievable=None):
+    def report(self, reps=20, achievable=None, min_bytes=1 << 30):
         res = []
         for label, (fn, a, k, nb) in self.calls.items():
-            us = self._replay_us(fn, a, k, reps)
+            us, n_sets, in_b = self._replay_us(fn, a, k, reps, min_bytes)
             gbs = nb / (us * 1e-6) / 1e9
             res.append({"kernel": label, "avg_us": round(us, 2), "bytes_per_launch": int(nb),
-                        "achieved_GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)})
+                        "achieved_GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+                        "input_sets": n_sets, "input_bytes_rotated": int(n_sets * in_b)})
             if achievable:
                 res[-1]["frac_of_achievable"] = round(gbs / achievable, 4)
         return res
 
 
 def achievable_hbm_gbs(device, nbytes=1 << 31, reps=5):
-    """the HBM bandwidth a plain device copy reaches on this box
-    (read + write bytes / time, 2 GiB buffers, HIP events)."""
+    """the HBM bandwidth a streaming copy reaches on this box --
+    avr_stream_copy (16 B per lane, 4 loads in flight per lane; the kind of
+    float4 copy MI355X_MICROARCH.md measures at 6.29 TB/s) over 2 GiB buffers
+    (8x the Infinity Cache), read + write bytes / time, best of `reps` launches
+    timed one by one with HIP events."""
+    import avr
     src = torch.empty(nbytes // 4, device=device, dtype=torch.float32).fill_(1.0)
     dst = torch.empty_like(src)
-    dst.copy_(src)
+    avr.ops.stream_copy(src, dst)
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
+    best = None
     for _ in range(reps):
-        dst.copy_(src)
-    e.record()
-    e.synchronize()
-    gbs = 2 * nbytes * reps / (s.elapsed_time(e) * 1e-3) / 1e9
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        avr.ops.stream_copy(src, dst)
+        e.record()
+        e.synchronize()
+        ms = s.elapsed_time(e)
+        best = ms if best is None else min(best, ms)
+    assert bool((dst[:: 1 << 20] == 1.0).all())
     del src, dst
     torch.cuda.empty_cache()
-    return gbs
+    return 2 * nbytes / (best * 1e-3) / 1e9
 
 
 def cpu_share():
@@ -472,6 +514,175 @@ def run_standin(args, config, world, rank):
         dist.destroy_process_group()
 
 
+FIELD_KERNEL_SOURCES = ("csrc/field_x3.hip", "csrc/x3_gemm.h", "csrc/field_common.h")
+
+
+def field_kernel_hash():
+    """sha256[:16] of the x3 field kernel's sources (what a PMC profile was taken of)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in FIELD_KERNEL_SOURCES:
+        with open(os.path.join(REPO, "adaptive-volume-rendering_amd", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _run_killable(cmd, timeout, env):
+    """Run cmd in its own process group; on timeout kill the whole group."""
+    import signal
+    import subprocess
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                         start_new_session=True, cwd=REPO)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        return None, "", f"timed out after {timeout} s"
+    return p.returncode, out, err
+
+
+def pmc_traffic(args, timeout=240):
+    """The `roofline.traffic` leg, measured in this run: two rocprofv3 --pmc
+    passes (FETCH_SIZE; WRITE_SIZE + TCC_HIT/MISS -- counter groups that fit
+    one pass each, MI355X_MICROARCH.md) over a child `bench.py --pmc-child`
+    (the same C3 workload: one warm-up + one timed step), started BEFORE this
+    process touches the GPU. Per field_x3_kernel dispatch: L2->fabric bytes =
+    2 x FETCH_SIZE (gfx950 counts half of 16-B-per-lane reads) + WRITE_SIZE,
+    Infinity-Cache hits included. Returns (dict or None, note)."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    tmp = tempfile.mkdtemp(prefix="avr_pmc_", dir=os.environ.get("TMPDIR") or "/tmp")
+    env = dict(os.environ)
+    env.setdefault("TMPDIR", "/tmp")
+    per = {}
+    try:
+        for counters in (["FETCH_SIZE"], ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"]):
+            d = os.path.join(tmp, counters[0])
+            cmd = [prof, "--pmc", *counters, "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
+                   os.path.abspath(__file__), "--pmc-child", "--precision", args.precision,
+                   "--rays", str(args.rays), "--n-coarse", str(args.n_coarse), "--n-fine", str(args.n_fine)]
+            print(f"bench.py: rocprofv3 --pmc {' '.join(counters)} pass ...", file=sys.stderr, flush=True)
+            rc, _, err = _run_killable(cmd, timeout, env)
+            if rc != 0:
+                return None, f"rocprofv3 --pmc {counters[0]} pass failed ({rc}): {err.strip()[-300:]}"
+            rows = []
+            for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                with open(path) as fh:
+                    rows += [r for r in csv.DictReader(fh) if "field_x3_kernel" in r["Kernel_Name"]
+                             or "field_fwd_kernel" in r["Kernel_Name"]]
+            for c in counters:
+                vals = {}
+                for r in rows:
+                    if r["Counter_Name"] == c:
+                        vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+                if not vals:
+                    return None, f"no {c} rows for the field kernel"
+                per[c] = (sum(vals.values()) / len(vals), len(vals))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    fetch, n = per["FETCH_SIZE"]
+    write, _ = per["WRITE_SIZE"]
+    hit, miss = per["TCC_HIT_sum"][0], per["TCC_MISS_sum"][0]
+    return {"bytes_per_launch": int((2 * fetch + write) * 1024), "fetch_size_kb_raw": fetch, "write_size_kb": write,
+            "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None, "dispatches": n}, "ok"
+
+
+def time_steps(step, steps, warmup, world, device):
+    """W untimed steps, then K timed steps between barrier + synchronize on
+    both sides; the max over ranks. Returns (seconds, last output)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    return elapsed, out
+
+
+def frame_views(n_views, frame, device):
+    """BASELINE config 5's rays: n_views orbit views of a frame x frame
+    get_opencv_pixel_coordinates grid, one ray batch with a per-ray pose."""
+    from avr.video import get_opencv_pixel_coordinates
+    x_pix = get_opencv_pixel_coordinates(frame, frame).reshape(1, -1, 2).repeat(1, n_views, 1).to(device)
+    R = x_pix.shape[1]
+    c2w = torch.stack([orbit_c2w(2 * np.pi * v / n_views) for v in range(n_views)]).to(device)
+    c2w = c2w.repeat_interleave(R // n_views, 0).reshape(1, R, 4, 4)
+    return x_pix, c2w
+
+
+def config5_leg(args, net, fused, K, device):
+    """BASELINE config 5's workload (4 orbit views x 800x800 per step) on this
+    one GPU: the same renderer call each rank of `--gpus N` makes on its tiles,
+    so the driver's 1 -> N ratio compares one workload."""
+    from avr.renderers import VolumeRenderer
+    x_pix, c2w = frame_views(4, args.frame, device)
+    rend = VolumeRenderer(0.8, 1.8, args.n_coarse, args.n_fine, 0, 0.01, True)
+    rend.seed = 1234
+
+    def step():
+        fused._packed.clear()
+        with torch.no_grad():
+            return rend(c2w, K, x_pix, net)[1]
+
+    elapsed, out = time_steps(step, args.config5_steps, 1, 1, device)
+    assert rend.last_path == "fused" and bool(torch.isfinite(out).all())
+    R = x_pix.shape[1]
+    return {"value": round(R * args.config5_steps / elapsed, 1), "unit": "rays/s", "steps": args.config5_steps,
+            "warmup": 1, "ms_per_step": round(elapsed / args.config5_steps * 1e3, 3), "rays_per_step": R,
+            "scaling": "strong",
+            "workload": f"BASELINE config 5 on 1 GPU: 4 orbit views x {args.frame}x{args.frame} ({R} rays) per step "
+                        f"x ({args.n_coarse} coarse + {args.n_fine} fine), the per-rank renderer call of --gpus N"}
+
+
+def fp32_leg(args, net, fused, timer, K, c2w, x_pix, device):
+    """The strict-fp32 field (v_mfma_f32_16x16x4_f32) on the headline workload,
+    same box and process: a measured anchor for the x3 number."""
+    from avr.renderers import VolumeRenderer
+    rend = VolumeRenderer(0.8, 1.8, args.n_coarse, args.n_fine, 0, 0.01, True)
+    rend.seed = 1234
+    prev = net.field_precision
+    net.field_precision = "fp32"
+
+    def step():
+        fused._packed.clear()
+        with torch.no_grad():
+            return rend(c2w, K, x_pix, net)[1]
+
+    try:
+        step()
+        timer.reset()
+        elapsed, out = time_steps(step, args.fp32_steps, 0, 1, device)
+        field_ms = timer.total_ms()
+        ach = timer.samples * field_flops_per_sample() / (field_ms * 1e-3) / 1e12
+    finally:
+        net.field_precision = prev
+    R = x_pix.shape[1]
+    return {"value": round(R * args.fp32_steps / elapsed, 1), "unit": "rays/s", "steps": args.fp32_steps,
+            "warmup": 1, "ms_per_step": round(elapsed / args.fp32_steps * 1e3, 3), "dtype": "fp32",
+            "kernel": "field_fwd_kernel<32> (v_mfma_f32_16x16x4_f32)", "field_achieved_TFLOPs": round(ach, 2),
+            "field_frac_of_fp32_peak": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+            "avg_launch_ms": round(field_ms / max(len(timer.events), 1), 3)}
+
+
 def main():
     global dist
     ap = argparse.ArgumentParser()
@@ -486,6 +697,13 @@ def main():
     ap.add_argument("--precision", choices=["x3", "fp32"], default="x3",
                     help="field MFMA path: split-fp16 (3 products, fp32 accumulate) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic leg")
+    ap.add_argument("--no-legs", action="store_true", help="skip the config-5 and fp32 legs of the N=1 line")
+    ap.add_argument("--config5-steps", type=int, default=2, help="N=1: timed steps of the config-5 leg")
+    ap.add_argument("--fp32-steps", type=int, default=3, help="N=1: timed steps of the strict-fp32 leg")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the RCCL process group even at one rank (the N > 1 code path on one GPU)")
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=None,
                     help="BASELINE config (default: 3 on one GPU, 5 on more): 2 = the coarse pass only (65536 "
                          "rays x 128 samples: rays, stratified z, field, composite); 3 = 65536 random rays per GPU (weak "
@@ -497,10 +715,14 @@ def main():
                     help="density bias of the synthetic field (config 4: opacity of the scene)")
     ap.add_argument("--mode", choices=["render", "train"], default="render",
                     help="render: the headline inference metric; train: one train.py step per step (1 GPU)")
+    ap.add_argument("--conf", choices=["default", "default_mv"], default="default",
+                    help="--mode train: the field of conf/default.conf or conf/default_mv.conf (train.py:262)")
     ap.add_argument("--train-modes", default="hip,torch", help="--mode train: which autograd paths to time")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: stand-in renderer on gloo (tests the launcher and the config-5 sharding only)")
     args = ap.parse_args()
+    if args.pmc_child:
+        args.steps, args.warmup, args.no_cpu_baseline, args.no_pmc, args.no_legs = 1, 1, True, True, True
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
@@ -510,12 +732,19 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     config = args.config if args.config is not None else (3 if world == 1 else 5)
+    use_dist = world > 1 or args.dist
     if args.device == "cpu":
-        if world > 1:
+        if use_dist:
             import torch.distributed as dist
             dist.init_process_group("gloo")
         return run_standin(args, config, world, rank)
-    if world > 1:
+
+    # the traffic leg runs first: its profiled children use the GPU before this process does
+    pmc, pmc_note = None, "skipped"
+    if (world == 1 and args.mode == "render" and config == 3 and not args.no_pmc):
+        pmc, pmc_note = pmc_traffic(args)
+
+    if use_dist:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -538,6 +767,7 @@ def main():
     rend = VolumeRenderer(0.8, 1.8, args.n_coarse, args.n_fine, 0, 0.01, True)
     # config 5: one frame-wide Philox stream keyed by global ray ids (render_sharded); else a batch per rank
     rend.seed = 1234 if config == 5 else 1234 + rank
+    K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]], device=device)
     if config == 4:
         # one full 800x800 frame per step (get_opencv_pixel_coordinates grid), fine pass with early
         # termination at T_stop = 1e-5; with N GPUs each rank renders its own frame
@@ -549,32 +779,29 @@ def main():
         # BASELINE config 5: 4 views x 800x800 per step for the whole job; every rank renders its 64-ray tiles
         # of all 4 views and one all_gather assembles the frames (avr.parallel.render_sharded)
         # (one scene: the 4 views are one ray batch of 4 x 640 000 rays with a per-ray pose)
-        from avr.video import get_opencv_pixel_coordinates
-        n_views = 4
-        x_pix = get_opencv_pixel_coordinates(args.frame, args.frame).reshape(1, -1, 2).repeat(1, n_views, 1).to(device)
+        x_pix, c2w = frame_views(4, args.frame, device)
         R = x_pix.shape[1]
     else:
         R = args.rays
         g = torch.Generator(device="cpu").manual_seed(100 + rank)
         x_pix = torch.rand(1, R, 2, generator=g).to(device)
-    K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]], device=device)
     gathered = None
     if config == 5:
         from avr.parallel import render_sharded
-        c2w = torch.stack([orbit_c2w(2 * np.pi * v / n_views) for v in range(n_views)]).to(device)
-        c2w = c2w.repeat_interleave(R // n_views, 0).reshape(1, R, 4, 4)
     else:
         c2w = orbit_c2w(0.7 + 0.5 * rank).to(device).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
-        if world > 1:
+        if use_dist:
             gathered = torch.empty(world * R * 7, device=device)
+
+    def render_fn(c, k, x, ray_ids=None, n_rays_total=None):
+        return rend(c, k, x, net, ray_ids=ray_ids, n_rays_total=n_rays_total)
 
     def step():
         fused._packed.clear()       # per-scene prep inside the step: repack weights, rebuild lin_z tables
         with torch.no_grad():
             if config == 5:
-                if world > 1:
-                    rgb_c, rgb_f, depth, _ = render_sharded(lambda c, k, x, **ids: rend(c, k, x, net, **ids),
-                                                            c2w, K, x_pix)
+                if use_dist:
+                    rgb_c, rgb_f, depth, _ = render_sharded(render_fn, c2w, K, x_pix)
                 else:
                     rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
                 return rgb_f
@@ -585,7 +812,7 @@ def main():
                 rend.last_path, rend.last_fine_samples = "fused", 0
                 return rgb_c
             rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
-            if world > 1:
+            if use_dist:
                 local = torch.cat([rgb_c.reshape(-1), rgb_f.reshape(-1), depth.reshape(-1)])
                 dist.all_gather_into_tensor(gathered, local)
         return rgb_f
@@ -596,33 +823,36 @@ def main():
     torch.cuda.synchronize()
     timer.reset()
     hbm.on = True
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    fine_evaluated = 0
-    for _ in range(args.steps):
+    fine_evaluated = [0]
+
+    def counted_step():
         out = step()
-        fine_evaluated += rend.last_fine_samples
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        fine_evaluated[0] += rend.last_fine_samples
+        return out
+
+    elapsed, out = time_steps(counted_step, args.steps, 0, world if use_dist else 1, device)
+    hbm.on = False
     field_ms = timer.total_ms()
-    if world > 1:
-        t = torch.tensor([elapsed, field_ms], device=device, dtype=torch.float64)
+    field_launches = len(timer.events)
+    if use_dist:
+        t = torch.tensor([field_ms], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, field_ms = float(t[0]), float(t[1])
+        field_ms = float(t[0])
     assert bool(torch.isfinite(out).all())
+    if args.pmc_child:
+        return
 
     # whole-job rays: config 5 renders a fixed 4 x 800 x 800 per step over all ranks (strong scaling)
     rays_total = (R if config == 5 else R * world) * args.steps
     value = rays_total / elapsed
     samples_per_ray = args.n_coarse if config == 2 else args.n_coarse + args.n_coarse + args.n_fine
     fps = field_flops_per_sample()
-    field_launches = len(timer.events)
     achieved_tflops = timer.samples * fps / (field_ms * 1e-3) / 1e12
+    # compulsory bytes of an average field launch: z in + (r, g, b, sigma) out per sample, ro / rd
+    # per ray, the x3 weight blob (4 B per weight: fp16 hi + lo) and the three lin_z tables (fp32)
+    rays_per_launch = -(-R // world) if (config == 5 and use_dist) else R
+    alg_bytes = (timer.samples / max(field_launches, 1) * 20 + rays_per_launch * 24
+                 + 4 * (42 * 512 + 6 * 512 * 512 + 512 * 4) + 3 * 64 * 64 * 512 * 4)
     if args.precision == "x3":
         # each fp32-equivalent MAC is 3 fp16 MFMA MACs: the attainable fp32-equivalent peak is fp16 / 3
         peak, kname = FP16_MFMA_PEAK_TFLOPS / 3.0, ("field_x3_kernel<4,8> (8 waves; fused PE + lin_z interpolation + ResnetFC on "
@@ -656,7 +886,8 @@ def main():
                    (f"BASELINE config 5: 4 orbit views x 800x800 ({R} rays) per step over {world} GPU(s) in "
                     f"64-ray tiles x ({args.n_coarse} coarse + {args.n_fine} fine), conf/default.conf PixelNeRF field"),
                    "rays_per_gpu": R if config != 5 else -(-R // world), "n_coarse": args.n_coarse, "n_fine": args.n_fine,
-                   "field_samples_per_ray": samples_per_ray, "parallelism": f"ray-shard x{world} + RCCL gather"},
+                   "field_samples_per_ray": samples_per_ray,
+                   "parallelism": f"ray-shard x{world}" + (" + RCCL gather" if use_dist else " (no collective at N=1)")},
         "roofline": {
             "kernel": kname,
             "bound": "mfma",
@@ -670,6 +901,8 @@ def main():
             "reference_flops_per_sample": reference_flops_per_sample(),
             "avg_launch_ms": round(field_ms / max(field_launches, 1), 3),
             "field_share_of_step": round(field_ms / (elapsed * 1e3), 4),
+            "field_kernel_sha16": field_kernel_hash(),
+            "algorithmic_bytes_per_launch": int(alg_bytes),
         },
     }
     if args.precision == "x3":
@@ -679,28 +912,33 @@ def main():
         line["roofline"]["power_limited_peak"] = {
             "value": round(pl, 1), "unit": "TFLOP/s", "frac": round(achieved_tflops / pl, 4),
             "source": "profiles/r02_mfma_power_probe.txt (scripts/probe/mfma_probe.hip, random fp16 operands) / 3"}
+    if pmc is not None:
+        line["roofline"]["traffic"] = pmc["bytes_per_launch"]
+        line["roofline"]["traffic_source"] = (
+            f"this run: rocprofv3 --pmc passes over a child bench.py --pmc-child (same workload), mean of "
+            f"{pmc['dispatches']} field dispatches; 2 x FETCH_SIZE + WRITE_SIZE = L2->fabric bytes incl. "
+            "Infinity-Cache hits")
+        line["roofline"]["traffic_over_algorithmic"] = round(pmc["bytes_per_launch"] / alg_bytes, 1)
+        line["roofline"]["l2_hit_rate"] = None if pmc["l2_hit_rate"] is None else round(pmc["l2_hit_rate"], 4)
+    else:
+        line["roofline"]["traffic_source"] = f"not measured in this run ({pmc_note})"
     # the renderer's HBM-bound kernels (the metric's "achieved HBM GB/s vs roofline"), HIP events per launch,
-    # against the 8 TB/s peak and against what a device copy reaches on this box
+    # against the 8 TB/s peak and against what a streaming copy reaches on this box
     ach = achievable_hbm_gbs(device)
     line["hbm_achievable_GBs"] = round(ach, 1)
     line["hbm_kernels"] = hbm.report(achievable=ach)
-    pmc = os.path.join(REPO, "profiles", "field_pmc.json")
-    if os.path.exists(pmc):
-        # not measured in this run: the committed rocprofv3 --pmc pass over this bench (TCC_EA0 read/write
-        # bytes, FETCH_SIZE x2 on gfx950), i.e. L2->fabric bytes INCLUDING Infinity-Cache (MALL) hits
-        with open(pmc) as f:
-            j = json.load(f)
-        line["roofline"]["traffic"] = j.get("hbm_bytes_per_launch")
-        line["roofline"]["traffic_source"] = ("profiles/field_pmc.json constant (" + str(j.get("source", "")) +
-                                              "): L2->fabric bytes per field launch incl. MALL hits, not DRAM-only")
     if config == 4:
         line["config"]["fine_samples_evaluated_fraction"] = round(
-            fine_evaluated / (args.steps * R * (args.n_coarse + args.n_fine)), 4)
+            fine_evaluated[0] / (args.steps * R * (args.n_coarse + args.n_fine)), 4)
+    if world == 1 and config == 3 and not args.no_legs:
+        line["config5"] = config5_leg(args, net, fused, K, device)
+        if args.precision == "x3":
+            line["fp32"] = fp32_leg(args, net, fused, timer, K, c2w, x_pix, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

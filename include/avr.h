@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 6
+#define AVR_ABI_VERSION 7
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -313,6 +313,12 @@ int avr_raymarch(const avr_view_desc* view, const float* gate_table, const float
                  const float* b_hh, const float* w_out, const float* b_out, const float* ro, const float* rd,
                  const float* init_dist, int64_t n_rays, int steps, float* world, float* final_dist, float* trace,
                  void* stream);
+
+/* ------------------------------------------------------------ measurement
+ * Streaming device copy dst[0, n_bytes) = src[0, n_bytes) (16-B aligned,
+ * n_bytes a multiple of 16): the achievable-HBM yardstick bench.py reports
+ * every renderer kernel against. Not on the rendering path.      */
+int avr_stream_copy(const void* src, void* dst, int64_t n_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -48,5 +48,16 @@ def oracle_field(g):
                             n_blocks=int(g["n_blocks"]), combine_layer=int(g["combine_layer"]))
 
 
+def oracle_field_from_net(net):
+    """The oracle field with the parameters, latent and source view of a
+    product NewPixelNeRFNet (e.g. the bench's avr.scene.synthetic_scene)."""
+    sd = lambda m: {k: v.detach().float().cpu().numpy() for k, v in m.state_dict().items()}  # noqa: E731
+    mlp = net.mlp_coarse
+    return O.PixelNeRFField(sd(net.mlp_coarse), sd(net.mlp_fine), net.encoder.latent.detach().float().cpu().numpy(),
+                            to_np(net.poses), to_np(net.focal), to_np(net.c), to_np(net.image_shape),
+                            to_np(net.encoder.latent_scaling), n_blocks=mlp.n_blocks,
+                            combine_layer=mlp.combine_layer)
+
+
 def to_np(t):
     return t.detach().float().cpu().numpy()
