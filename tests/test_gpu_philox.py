@@ -14,7 +14,9 @@ oracle and compare:
     (128 + 64)) through the drop-in VolumeRenderer, checked on 4 096 rays with
     the renderers.py:133-277 protocol of tests/test_gpu_scale.py: coarse z
     bit-exact, fine bins / fine z / merge bit-exact given the HIP weights,
-    rgb / depth <= 1e-4 on >= 99.9 % of rays with every outlier a bin flip.
+    every ray's rgb / depth <= 1e-4 against the oracle's fine pass on the
+    same samples, and end to end every outlier a bin flip (fp32 noise in the
+    coarse weights moving a fine sample across a cdf step, quirk Q3).
 """
 import functools
 
@@ -141,8 +143,8 @@ def test_c3_philox_bench_path_vs_oracle():
     x_pix = T(x_pix_np)
     K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]], device=DEV)
     c2w = orbit_c2w(0.7).to(DEV).reshape(1, 1, 4, 4).expand(1, R3, 4, 4)
-    rend = VolumeRenderer(0.8, 1.8, NC, NF, 0, 0.01, True)       # bench.py:538
-    rend.seed = SEED                                             # bench.py:540
+    rend = VolumeRenderer(0.8, 1.8, NC, NF, 0, 0.01, True)       # bench.py main()
+    rend.seed = SEED                                             # bench.py main(): 1234 + rank
     with torch.no_grad():
         r_c, r_f, r_d, _ = rend(c2w, K, x_pix, net)
         # the same chain stage by stage (offset 0 = the renderer's first call)
@@ -175,10 +177,31 @@ def test_c3_philox_bench_path_vs_oracle():
     np.testing.assert_array_equal(to_np(zf[S]), zf_o[0])
     np.testing.assert_array_equal(to_np(zs[S]), np.sort(np.concatenate([to_np(zc[S]), zf_o[0]], -1), -1))
     same = (to_np(idx[S]) == aux["idx"][0]).all(-1)
-    print(f"philox C3: rays with the oracle's bins {same.mean():.5f}")
-    assert same.mean() >= 0.999, same.mean()
+    # the bench scene's random-init fog puts ~0.2 % of rays within fp32 noise of a cdf step (quirk Q3): those
+    # rays take other fine bins than the oracle's own weights give; the oracle's fine pass on the HIP-chosen
+    # samples (bins bit-exact above) must then match them like every other ray
+    flips = np.flatnonzero(~same)
+    print(f"philox C3: rays with the oracle's bins {same.mean():.5f} ({flips.size} bin flips)")
+    assert same.mean() >= 0.99, same.mean()
     np.testing.assert_allclose(to_np(ff[S])[same], aux["field_fine"][0][same], atol=5e-5, rtol=1e-4)
+    rgb_ref, depth_ref = o_f[0].copy(), o_d[0].copy()
+    if flips.size:
+        field = oracle_field_from_net(net)
+        c2w1 = orbit_c2w(0.7).numpy()
+        zs_h = to_np(zs[S])[flips][None]
+        ro_o, rd_o = aux["ro"][:, flips], aux["rd"][:, flips]
+        pts = ro_o[..., None, :] + rd_o[..., None, :] * zs_h[..., None]
+        vd = np.broadcast_to(rd_o[..., None, :], pts.shape)
+        ff_o = field(pts.reshape(1, -1, 3), vd.reshape(1, -1, 3), coarse=False).reshape(1, flips.size, -1, 4)
+        rgb_o, dist_o, _ = O.volume_integral(zs_h, ff_o[..., 3:4], ff_o[..., :3], True)
+        rgb_ref[flips] = rgb_o[0]
+        depth_ref[flips] = O.depth_from_world(ro_o + rd_o * dist_o, np.broadcast_to(c2w1, (1, flips.size, 4, 4)))[0]
+    # staged: every ray within 1e-4 of the oracle's fine pass on the same samples
+    staged = (np.abs(to_np(r_f[0, S]) - rgb_ref).max(-1) <= 1e-4) & (np.abs(to_np(r_d[0, S]) - depth_ref) <= 1e-4)
+    assert staged.all(), staged.mean()
+    # end to end against the pure oracle: an outlier only where the bins flipped
     ok = (np.abs(to_np(r_f[0, S]) - o_f[0]).max(-1) <= 1e-4) & (np.abs(to_np(r_d[0, S]) - o_d[0]) <= 1e-4)
-    assert ok.mean() >= 0.999, ok.mean()
+    print(f"philox C3: end-to-end within 1e-4 on {ok.mean():.5f} of rays")
+    assert ok.mean() >= 0.99, ok.mean()
     assert not (~ok & same).any(), "a ray with the oracle's bins must match it"
     assert np.abs(to_np(r_c[0, S]) - o_c[0]).max() <= 1e-4
