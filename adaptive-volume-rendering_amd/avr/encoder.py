@@ -194,10 +194,11 @@ class SpatialEncoder(nn.Module):
             if self.num_layers > k:
                 x = layer(x)
                 latents.append(x)
-        self.latents = latents
         align_corners = None if self.index_interp == "nearest " else True   # (sic, models.py:316)
         size = latents[0].shape[-2:]
         latents = [F.interpolate(t, size, mode=self.upsample_interp, align_corners=align_corners) for t in latents]
+        # the reference interpolates its list in place (models.py:315-324): encoder.latents holds the upsampled maps
+        self.latents = latents
         self.latent = torch.cat(latents, dim=1)
         self._set_scaling()
         return self.latent

@@ -322,9 +322,14 @@ class _DepthOfPoints(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        c2w = ctx.c2w_info[0]
+        c2w, sb_stride, ray_stride = ctx.c2w_info
         SB, R, _ = ctx.shape
-        row = -torch.linalg.inv(c2w.double())[..., 2, :3].to(F32)       # (SB, R or 1, 3)
+        if ray_stride == 0:
+            # one pose per batch (the stride-0 expand the callers pass): invert it once, not per ray
+            c2w = c2w[:, :1]
+        if sb_stride == 0:
+            c2w = c2w[:1]
+        row = -torch.linalg.inv(c2w.double())[..., 2, :3].to(F32)       # (SB or 1, R or 1, 3)
         return g.reshape(SB, R, 1) * row.expand(SB, R, 3), None
 
 

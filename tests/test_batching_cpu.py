@@ -32,3 +32,26 @@ def test_bbox_sample_inside_boxes():
     pix = bbox_sample(boxes, 4000, gen)
     b = boxes[pix[:, 0]]
     assert bool(((pix[:, 2] >= b[:, 0]) & (pix[:, 2] <= b[:, 2]) & (pix[:, 1] >= b[:, 1]) & (pix[:, 1] <= b[:, 3])).all())
+
+
+def test_train_py_encode_call_uses_image_centre(golden):
+    """train.py:68 calls net.encode(src_images, poses, focal, c): c lands in the
+    4th positional slot, z_bounds, which the reference ignores (models.py:682-733),
+    so the principal point is the image centre whatever source['c'] holds.
+    The same call on avr.models.NewPixelNeRFNet behaves the same way."""
+    from avr.batching import sample_ray_batch
+    from avr.models import NewPixelNeRFNet
+    from helpers import model_conf
+    g = golden("g8_batching.npz")
+    all_input = {k: torch.from_numpy(g[k]) for k in ("images", "cam2world", "intrinsics", "focal", "c", "x_pix",
+                                                     "bbox")}
+    torch.manual_seed(int(g["bbox0_seed"]))
+    src, _, _ = sample_ray_batch(all_input, 16)
+    conf = model_conf(64, 3, 1000, 64)
+    conf["encoder"] = {"backbone": "resnet34", "pretrained": False, "num_layers": 1}
+    net = NewPixelNeRFNet(conf).eval()
+    with torch.no_grad():
+        net.encode(src["images"], src["poses"], src["focal"], src["c"])     # train.py:68, positional
+    sl = src["images"].shape[-1]
+    np.testing.assert_array_equal(net.c.numpy(), [[sl * 0.5, sl * 0.5]])
+    assert not np.allclose(src["c"].numpy(), sl * 0.5)   # the dataset's c really is dropped, not equal by chance
