@@ -26,7 +26,8 @@ c_float = ctypes.c_float
 
 class FieldDims(ctypes.Structure):
     _fields_ = [("d_in", c_int), ("d_latent", c_int), ("d_hidden", c_int), ("n_blocks", c_int),
-                ("n_lin_z", c_int), ("num_freqs", c_int), ("freq_factor", c_float), ("precision", c_int)]
+                ("n_lin_z", c_int), ("num_freqs", c_int), ("freq_factor", c_float), ("precision", c_int),
+                ("bn", c_int)]
 
 
 FIELD_FP32 = 0
@@ -37,7 +38,8 @@ class ResnetFCWeights(ctypes.Structure):
     _fields_ = [("lin_in_w", c_void_p), ("lin_in_b", c_void_p), ("lin_out_w", c_void_p), ("lin_out_b", c_void_p),
                 ("fc0_w", c_void_p * AVR_MAX_BLOCKS), ("fc0_b", c_void_p * AVR_MAX_BLOCKS),
                 ("fc1_w", c_void_p * AVR_MAX_BLOCKS), ("fc1_b", c_void_p * AVR_MAX_BLOCKS),
-                ("lin_z_w", c_void_p * AVR_MAX_BLOCKS), ("lin_z_b", c_void_p * AVR_MAX_BLOCKS)]
+                ("lin_z_w", c_void_p * AVR_MAX_BLOCKS), ("lin_z_b", c_void_p * AVR_MAX_BLOCKS),
+                ("bn_scale", c_void_p * AVR_MAX_BLOCKS), ("bn_shift", c_void_p * AVR_MAX_BLOCKS)]
 
 
 class ViewDesc(ctypes.Structure):

@@ -18,19 +18,34 @@ from ._lib import FieldDims, ResnetFCWeights, ViewDesc, call, ptr, require_devic
 F32 = torch.float32
 
 
-def _resnetfc_ok(mlp, d_in, d_latent):
+def uses_bn(mlp):
+    """ResnetBlockFC(bn=True) blocks (train.py --bn, models.py:430-432, 456-461)."""
+    return any(getattr(blk, "bn", False) for blk in getattr(mlp, "blocks", ()))
+
+
+def _bn_ok(blk):
+    """Eval-mode BatchNorm with running statistics: a per-feature affine the
+    x3 kernel applies (training-mode BN needs cross-sample statistics: module
+    path)."""
+    bn = blk.bn_0
+    return (not blk.training and not bn.training and bn.track_running_stats and bn.running_mean is not None
+            and bn.affine)
+
+
+def _resnetfc_ok(mlp, d_in, d_latent, precision="x3"):
     return (mlp is not None and type(mlp).__name__ == "ResnetFC" and getattr(mlp, "d_in", -1) == d_in
             and mlp.d_latent == d_latent and mlp.d_out == 4 and mlp.d_hidden in (64, 128, 256, 512)
             and not getattr(mlp, "use_spade", False) and isinstance(mlp.activation, torch.nn.ReLU)
             and 1 <= mlp.n_blocks <= _lib.AVR_MAX_BLOCKS
-            and all(not blk.bn and blk.shortcut is None and isinstance(blk.activation, torch.nn.ReLU)
-                    for blk in mlp.blocks))
+            and all((not blk.bn or (precision == "x3" and _bn_ok(blk))) and blk.shortcut is None
+                    and isinstance(blk.activation, torch.nn.ReLU) for blk in mlp.blocks))
 
 
 def fused_eligible(net):
     """True when `net` is a NewPixelNeRFNet configured like conf/default*.conf:
     local encoder, xyz + PE(xyz) + raw viewdirs, normalize_z, bilinear/border
-    latent lookup, ResNet MLPs, one source view."""
+    latent lookup, ResNet MLPs (eval-mode BatchNorm allowed on the x3 path),
+    one source view."""
     try:
         code = getattr(net, "code", None)
         enc = net.encoder
@@ -44,7 +59,8 @@ def fused_eligible(net):
         if not ok:
             return False
         mlps = [net.mlp_coarse] + ([net.mlp_fine] if net.mlp_fine is not None else [])
-        return all(_resnetfc_ok(m, net.d_in, net.d_latent) for m in mlps)
+        precision = getattr(net, "field_precision", "x3")
+        return all(_resnetfc_ok(m, net.d_in, net.d_latent, precision) for m in mlps)
     except AttributeError:
         return False
 
@@ -92,11 +108,11 @@ class FusedField:
         code = self.net.code
         return FieldDims(self.net.d_in, self.net.d_latent, mlp.d_hidden, mlp.n_blocks,
                          min(mlp.combine_layer, mlp.n_blocks), code.num_freqs, _freq_factor(code),
-                         PRECISIONS[self.precision])
+                         PRECISIONS[self.precision], int(uses_bn(mlp)))
 
     def packed(self, coarse):
         mlp = self._mlp(coarse)
-        params = [p.detach() for p in mlp.parameters()]
+        params = [p.detach() for p in mlp.parameters()] + [b for b in mlp.buffers() if b.is_floating_point()]
         key = (id(mlp), _version_key(params))
         hit = self._packed.get(coarse)
         if hit is not None and hit[0] == key:
@@ -117,7 +133,18 @@ class FusedField:
         w.lin_in_w, w.lin_in_b = P(mlp.lin_in.weight), P(mlp.lin_in.bias)
         w.lin_out_w, w.lin_out_b = P(mlp.lin_out.weight), P(mlp.lin_out.bias)
         for b, blk in enumerate(mlp.blocks):
-            w.fc0_w[b], w.fc0_b[b] = P(blk.fc_0.weight), P(blk.fc_0.bias)
+            if dims.bn:
+                # eval BatchNorm1d as y = a x + c (torch's batch_norm: a = w / sqrt(var + eps), c = b - mean a);
+                # bn_0 sits in front of both relus of the block (models.py:456-461): the first is applied by
+                # the kernel, the second folds into fc_0's rows
+                bn = blk.bn_0
+                a = (bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps))
+                c = bn.bias.detach().float() - bn.running_mean.detach().float() * a
+                w.bn_scale[b], w.bn_shift[b] = P(a), P(c)
+                w.fc0_w[b] = P(blk.fc_0.weight.detach().float() * a[:, None])
+                w.fc0_b[b] = P(blk.fc_0.bias.detach().float() * a + c)
+            else:
+                w.fc0_w[b], w.fc0_b[b] = P(blk.fc_0.weight), P(blk.fc_0.bias)
             w.fc1_w[b], w.fc1_b[b] = P(blk.fc_1.weight), P(blk.fc_1.bias)
         for b in range(dims.n_lin_z):
             w.lin_z_w[b], w.lin_z_b[b] = P(mlp.lin_z[b].weight), P(mlp.lin_z[b].bias)

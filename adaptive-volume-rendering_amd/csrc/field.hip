@@ -62,6 +62,12 @@ static int make_layout(const avr_field_dims* d, Layout* L) {
     L->x3_fc1[b] = o; o += (int64_t)KC * NT * tile16;
   }
   L->x3_out = o; o += (int64_t)KC * tile16;
+  AVR_REQUIRE(d->bn == 0 || d->bn == 1, "field: bn must be 0 or 1");
+  L->bn = d->bn;
+  for (int b = 0; b < d->n_blocks; ++b) {
+    L->bn_a[b] = L->bn_c[b] = 0;
+    if (d->bn) { L->bn_a[b] = o; o += d->d_hidden; L->bn_c[b] = o; o += d->d_hidden; }
+  }
   L->total = o;
   return AVR_OK;
 }
@@ -477,6 +483,7 @@ static int field_common(const avr_field_dims* dims, const avr_view_desc* view, c
 static int dispatch_field(const avr_field_dims* dims, const FieldArgs& a, hipStream_t s) {
   const int d_hidden = dims->d_hidden;
   if (dims->precision == AVR_FIELD_X3) return dispatch_field_x3(d_hidden, a, s);
+  AVR_REQUIRE(!dims->bn, "field: BatchNorm nets run on the x3 path only");
   AVR_REQUIRE(dims->precision == AVR_FIELD_FP32, "field: unknown precision %d", dims->precision);
   switch (d_hidden) {
     case 64: return launch_field<4>(a, s);
@@ -529,6 +536,11 @@ extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_wei
   if ((rc = pack_bias(w->lin_in_b, dims->n_lin_z > 0 ? w->lin_z_b[0] : nullptr, H, H, packed + L.b_in, s)))
     return rc;
   if ((rc = pack_bias(w->lin_out_b, nullptr, 4, 16, packed + L.b_out, s))) return rc;
+  for (int b = 0; dims->bn && b < dims->n_blocks; ++b) {
+    AVR_REQUIRE(w->bn_scale[b] && w->bn_shift[b], "avr_field_pack: bn needs bn_scale / bn_shift of every block");
+    if ((rc = pack_bias(w->bn_scale[b], nullptr, H, H, packed + L.bn_a[b], s))) return rc;
+    if ((rc = pack_bias(w->bn_shift[b], nullptr, H, H, packed + L.bn_c[b], s))) return rc;
+  }
   // split-fp16 fragments (header word per layer: 0 lin_in, 1 lin_out, 2+2b fc0[b], 3+2b fc1[b])
   unsigned* hdr = reinterpret_cast<unsigned*>(packed + L.x3_hdr);
   if (hipMemsetAsync(hdr, 0, 64 * sizeof(float), s) != hipSuccess) return fail(AVR_E_HIP, "avr_field_pack: memset");
@@ -597,6 +609,7 @@ extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_
   int rc = field_common(dims, views, packed, tables, &a);
   if (rc) return rc;
   AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_fwd_points_train: the training path is x3 only");
+  AVR_REQUIRE(!dims->bn, "avr_field_fwd_points_train: BatchNorm nets train on the module path");
   AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points_train: bad size");
   AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && out && act && mask), "avr_field_fwd_points_train: null pointer");
   AVR_REQUIRE(act_rows >= n_scenes * n_points, "avr_field_fwd_points_train: act_rows < n_scenes * n_points");
@@ -626,6 +639,7 @@ extern "C" int avr_field_bwd(const avr_field_dims* dims, const float* packed, co
   int rc = make_layout(dims, &a.L);
   if (rc) return rc;
   AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_bwd: the training path is x3 only");
+  AVR_REQUIRE(!dims->bn, "avr_field_bwd: BatchNorm nets train on the module path");
   AVR_REQUIRE(n_points >= 0 && n_scenes >= 1, "avr_field_bwd: bad size");
   if (n_points == 0) return AVR_OK;
   AVR_REQUIRE(packed && packed_bwd && out && grad_out && mask && grads, "avr_field_bwd: null pointer");

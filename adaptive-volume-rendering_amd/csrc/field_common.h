@@ -28,6 +28,8 @@ struct Layout {
   int64_t w_in, w_out, fc0[AVR_MAX_BLOCKS], fc1[AVR_MAX_BLOCKS], lin_z[AVR_MAX_BLOCKS];
   int64_t b_in, b_out, b_fc0[AVR_MAX_BLOCKS], b_fc1[AVR_MAX_BLOCKS];
   int64_t x3_hdr, x3_in, x3_out, x3_fc0[AVR_MAX_BLOCKS], x3_fc1[AVR_MAX_BLOCKS];
+  int64_t bn_a[AVR_MAX_BLOCKS], bn_c[AVR_MAX_BLOCKS];   // eval BatchNorm affine of block b (bn != 0)
+  int bn;
   int64_t total;          // floats
 };
 

@@ -227,7 +227,8 @@ __device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const 
 // VALU issue rate of the epilogues and hides one wave's stalls behind the
 // other); wave w owns the FT 16-row feature tiles FT*w .. FT*w + FT-1.
 // SAVE (training forward): also write every GEMM input and its relu mask.
-template <int FT, int NW, bool SAVE>
+// BN: eval-mode BatchNorm nets (x3_gemm.h max_relu_bn): the block input is relu(a * h + c).
+template <int FT, int NW, bool SAVE, bool BN = false>
 __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   constexpr int HID = 16 * FT * NW;
   using P = LdsPlan<HID>;
@@ -238,6 +239,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   constexpr bool TWO = NW > 4;
   constexpr int NPF = TWO ? FT : kPrefetch;   // chunk-0 weight tiles loaded ahead of each layer's publish
   static_assert(!(SAVE && TWO), "the training forward keeps the 4-wave layout");
+  static_assert(!(SAVE && BN), "BatchNorm nets train on the module path");
   const floatx4 bz[FT] = {};
   // 8 waves: waves 0-3 at priority 1 leave each GEMM first, so their epilogue VALU overlaps the last MFMAs of
   // waves 4-7 on the same SIMDs (measured against no priority, priority for waves 4-7, and a barrier every one
@@ -413,6 +415,12 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       }
       mx = TWO ? max_relu_affine<FT, false>(h, 1.0f / S_h, bz) : prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
     }
+    const float* bn_a = a.packed + L.bn_a[b];
+    const float* bn_c = a.packed + L.bn_c[b];
+    if constexpr (BN) {   // the block input is relu(bn_0(h)) (models.py:456-458), not relu(h)
+      if constexpr (TWO) mx = max_relu_bn<FT>(h, 1.0f / S_h, bn_a, bn_c, wid, g);
+      else mx = prep_bn<FT>(v, h, 1.0f / S_h, bn_a, bn_c, wid, g);
+    }
     AVR_STAMP(5 + 5 * (b & 3));
     if (SAVE) save_layer<FT, NW>(a, 2 * b, v, mx, base, roff, wid, g, j, lane);
     const uint4* W0 = P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
@@ -420,7 +428,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     prefetch_a<FT, NPF>(A0, W0, lane);
     if constexpr (TWO) {
       // the fc_1 bias loads are issued before the t publish, whose barriers cover their latency
-      s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
+      if constexpr (BN) s_x = publish_bn<FT, NW>(X16, h, 1.0f / S_h, bn_a, bn_c, mx, red, wid, lane, g, j);
+      else s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
       AVR_STAMP(6 + 5 * (b & 3));
       const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
       gemm<FT, true, TWO>(t, A0, W0, KC, 64 * NTT, X16, lane);
@@ -572,12 +581,12 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     a.out[roff + m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
 }
 
-template <int FT, int NW, bool SAVE>
+template <int FT, int NW, bool SAVE, bool BN = false>
 static int launch_x3(const FieldArgs& a, hipStream_t s) {
   const size_t shm = LdsPlan<16 * FT * NW>::BYTES;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT, NW, SAVE>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT, NW, SAVE, BN>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
       return fail(AVR_E_HIP, "field_x3_kernel: cannot set dynamic LDS to %zu", shm);
     attr = true;
@@ -585,22 +594,29 @@ static int launch_x3(const FieldArgs& a, hipStream_t s) {
   const int64_t blocks = (SAVE || a.n_scenes > 1) ? a.blocks_per_scene * a.n_scenes
                                                   : (a.M + kX3Samples - 1) / kX3Samples;
   AVR_REQUIRE(blocks < (1ll << 31), "field: too many points");
-  field_x3_kernel<FT, NW, SAVE><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
+  field_x3_kernel<FT, NW, SAVE, BN><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("field_x3_kernel");
 }
 
+// AVR_X3_WAVES (diagnostics), read per launch so a test can switch layouts in one process
 static int x3_waves() {
-  static int w = -1;
-  if (w < 0) {
-    const char* e = getenv("AVR_X3_WAVES");
-    w = (e && atoi(e) == 4) ? 4 : 8;
-  }
-  return w;
+  const char* e = getenv("AVR_X3_WAVES");
+  return (e && atoi(e) == 4) ? 4 : 8;
 }
 
 int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s) {
   // inference at d_hidden 512: 8 waves x 4 tiles (+2.7-4.7 % over the 4-wave layout on the same box);
   // AVR_X3_WAVES=4 selects the 4-wave layout (diagnostics)
+  if (a.L.bn) {   // eval-mode BatchNorm (inference only)
+    AVR_REQUIRE(!a.act, "field x3: BatchNorm nets train on the module path");
+    switch (d_hidden) {
+      case 64: return launch_x3<1, 4, false, true>(a, s);
+      case 128: return launch_x3<2, 4, false, true>(a, s);
+      case 256: return launch_x3<4, 4, false, true>(a, s);
+      case 512: return x3_waves() == 8 ? launch_x3<4, 8, false, true>(a, s) : launch_x3<8, 4, false, true>(a, s);
+    }
+    return fail(AVR_E_UNSUPPORTED, "field x3: d_hidden %d", d_hidden);
+  }
   if (d_hidden == 512 && !a.act && x3_waves() == 8) return launch_x3<4, 8, false>(a, s);
   switch (d_hidden) {
     case 64: return a.act ? launch_x3<1, 4, true>(a, s) : launch_x3<1, 4, false>(a, s);

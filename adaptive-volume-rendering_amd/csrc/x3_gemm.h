@@ -303,6 +303,57 @@ __device__ __forceinline__ void store_split_affine(uint4* X16, const floatx4 (&a
   }
 }
 
+// ---- Eval-mode BatchNorm in front of fc_0's relu (train.py --bn; ResnetBlockFC.bn_0,
+// models.py:456-458): relu(a * x + c) per feature of the residual stream x = acc * f,
+// with this lane's (a, c) loaded per feature tile (bn_a / bn_c: d_hidden floats in the
+// packed blob). The second bn_0 (in front of fc_1's relu) is folded into fc_0 at pack time.
+template <int FT>
+__device__ __forceinline__ void bn_tile(floatx4& a4, floatx4& c4, const float* __restrict__ bn_a,
+                                        const float* __restrict__ bn_c, float f, int wid, int ft, int g) {
+  const int o = 16 * (FT * wid + ft) + 4 * g;
+  a4 = *reinterpret_cast<const floatx4*>(bn_a + o) * f;
+  c4 = *reinterpret_cast<const floatx4*>(bn_c + o);
+}
+
+template <int FT>
+__device__ __forceinline__ float max_relu_bn(const floatx4 (&acc)[FT][4], float f, const float* __restrict__ bn_a,
+                                             const float* __restrict__ bn_c, int wid, int g) {
+  float mx = 0.f;
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    floatx4 a4, c4;
+    bn_tile<FT>(a4, c4, bn_a, bn_c, f, wid, ft, g);
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      const floatx4 x = acc[ft][sg] * a4 + c4;
+      mx = fmaxf(mx, fmaxf(x.x, x.y));
+      mx = fmaxf(mx, fmaxf(x.z, x.w));
+    }
+  }
+  return wave_max(mx);
+}
+
+// v = relu(acc * f * a + c) (4-wave layouts, materialised layer input); returns the wave max
+template <int FT>
+__device__ __forceinline__ float prep_bn(floatx4 (&v)[FT][4], const floatx4 (&acc)[FT][4], float f,
+                                         const float* __restrict__ bn_a, const float* __restrict__ bn_c, int wid,
+                                         int g) {
+  float mx = 0.f;
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    floatx4 a4, c4;
+    bn_tile<FT>(a4, c4, bn_a, bn_c, f, wid, ft, g);
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      floatx4 x = acc[ft][sg] * a4 + c4;
+      x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
+      v[ft][sg] = x;
+      mx = fmaxf(fmaxf(mx, x.x), fmaxf(fmaxf(x.y, x.z), x.w));
+    }
+  }
+  return wave_max(mx);
+}
+
 __device__ __forceinline__ float layer_scale(const float* packed, const Layout& L, int layer) {
   return pow2_scale_for(__uint_as_float(reinterpret_cast<const unsigned*>(packed + L.x3_hdr)[layer]));
 }
@@ -324,6 +375,35 @@ __device__ __forceinline__ float publish(uint4* X16, const floatx4 (&v)[FT][4], 
   lds_barrier();
   const float s_x = pow2_scale_for(red_max<NW>(red));
   store_split<FT>(X16, v, s_x, wid, g, j);
+  lds_barrier();
+  return s_x;
+}
+
+// Two-pass publish of relu(acc * f * a + c) per feature (mx from max_relu_bn); returns s_x
+template <int FT, int NW>
+__device__ __forceinline__ float publish_bn(uint4* X16, const floatx4 (&acc)[FT][4], float f,
+                                            const float* __restrict__ bn_a, const float* __restrict__ bn_c, float mx,
+                                            float* red, int wid, int lane, int g, int j) {
+  if (lane == 0) red[wid] = mx;
+  lds_barrier();
+  const float s_x = pow2_scale_for(red_max<NW>(red));
+  char* base = reinterpret_cast<char*>(X16);
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    floatx4 a4, c4;
+    bn_tile<FT>(a4, c4, bn_a, bn_c, f, wid, ft, g);
+    const int ftg = FT * wid + ft;
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      floatx4 x = acc[ft][sg] * a4 + c4;
+      x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
+      uint2 hi, lo;
+      split4(x, s_x, hi, lo);
+      const int s = 16 * sg + j;
+      *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 0, g, s) * 16 + (ftg & 1) * 8) = hi;
+      *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 1, g, s) * 16 + (ftg & 1) * 8) = lo;
+    }
+  }
   lds_barrier();
   return s_x;
 }

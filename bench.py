@@ -50,10 +50,13 @@ def reference_flops_per_sample(d_in=42, d_latent=512, d_hidden=512, n_blocks=3, 
                 + d_hidden * d_out)
 
 
-def build_scene(device, seed=0, sigma_bias=0.0):
-    """avr.scene.synthetic_scene: default.conf field (fc_1 ~ N(0, 0.02)), random 512x64x64 latent."""
+def build_scene(device, seed=0, sigma_bias=0.0, conf="default"):
+    """avr.scene.synthetic_scene: the default.conf field (or default_mv.conf's: 5 blocks, combine_layer 3)
+    with fc_1 ~ N(0, 0.02), random 512x64x64 latent."""
+    from avr.conf import default_conf
     from avr.scene import synthetic_scene
-    return synthetic_scene(device, seed, sigma_bias=sigma_bias)
+    model = default_conf(multiview=conf == "default_mv")["model"]
+    return synthetic_scene(device, seed, model, sigma_bias=sigma_bias)
 
 
 def orbit_c2w(angle, radius=1.3, z_height=0.4):
@@ -380,13 +383,15 @@ def run_train(args, device):
     the conf/default.conf renderer (64 coarse + 32 fine of which 16 depth
     samples) and field, MSE on rgb coarse + fine, backward, Adam (lr 1e-4).
     The latent maps are fixed inputs (the ResNet34 encoder is out of scope).
+    --conf default_mv: the field train.py itself builds (train.py:262 parses
+    conf/default_mv.conf: ResnetFC 5 x 512, combine_layer 3), same renderer.
     Timed twice: autograd through the HIP field (x3 training forward + HIP
     backward chain + the x3 weight-gradient kernel) and PyTorch autograd of
     the same module (forward_torch; the rest of the step is identical)."""
     from avr.conf import default_conf
     from avr.renderers import VolumeRenderer
     SB, R = 4, 512
-    net = build_scene(device)
+    net = build_scene(device, conf=args.conf)
     g = torch.Generator(device="cpu").manual_seed(7)
     net.encoder.set_latent(torch.randn(SB, net.d_latent, 64, 64, generator=g).to(device))
     net.num_objs = SB
@@ -431,9 +436,11 @@ def run_train(args, device):
         "value": round(SB * R / res["hip"], 1), "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(res["hip"] * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (field products as 3 fp16 MFMA terms)",
-        "data": "synthetic: random-init default.conf field, 4 random 512x64x64 latents, random pixels/targets",
+        "data": f"synthetic: random-init {args.conf}.conf field, 4 random 512x64x64 latents, random pixels/targets",
         "config": {"workload": f"train.py defaults: {SB} scenes x {R} rays, {rend.n_coarse} coarse + "
-                               f"{rend.n_fine} fine ({rend.n_fine_depth} depth) samples, Adam lr 1e-4",
+                               f"{rend.n_fine} fine ({rend.n_fine_depth} depth) samples, Adam lr 1e-4, field of "
+                               f"conf/{args.conf}.conf ({net.mlp_coarse.n_blocks} x {net.mlp_coarse.d_hidden} "
+                               f"ResnetFC, combine_layer {net.mlp_coarse.combine_layer})",
                    "field_samples_per_step": SB * R * spr},
     }
     if "torch" in res:

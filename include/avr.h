@@ -156,7 +156,7 @@ int avr_march_finish(const void* state, int64_t n_rays, int white_back, float* r
  * SpatialEncoder.index :245-274 (bilinear, border, align_corners=True),
  * ResnetFC :541-592, ResnetBlockFC :454-470 — for the default.conf family:
  * use_encoder, use_xyz, normalize_z, PE on xyz only (include_input), raw
- * viewdirs, ReLU, no BN, NS = 1.
+ * viewdirs, ReLU, NS = 1, and (x3 inference) eval-mode BatchNorm (dims->bn).
  *
  * The lin_z projections are applied to the latent map once per texel
  * (avr_field_latent_table) and bilinearly interpolated per sample: the
@@ -172,6 +172,11 @@ typedef struct {
   float freq_factor;
   int precision;   /* AVR_FIELD_FP32: v_mfma_f32_16x16x4_f32;
                       AVR_FIELD_X3: split-fp16 v_mfma_f32_16x16x32_f16 (3 products, fp32 accumulate) */
+  int bn;          /* 1: eval-mode BatchNorm in every block (train.py --bn, models.py:430-432, 456-461):
+                      ResnetBlockFC applies bn_0 in front of BOTH relus (the reference's bn_0-twice quirk).
+                      The caller folds the second one into fc_0 (fc0_w := diag(a) W0, fc0_b := a*b0 + c) and
+                      passes the per-feature affine y = a*x + c of bn_0 as bn_scale / bn_shift; the kernel
+                      applies it to the residual stream in front of fc_0's relu. x3 inference only.       */
 } avr_field_dims;
 
 #define AVR_FIELD_FP32 0
@@ -184,6 +189,9 @@ typedef struct {
   const float* fc0_w[AVR_MAX_BLOCKS]; const float* fc0_b[AVR_MAX_BLOCKS];
   const float* fc1_w[AVR_MAX_BLOCKS]; const float* fc1_b[AVR_MAX_BLOCKS];
   const float* lin_z_w[AVR_MAX_BLOCKS]; const float* lin_z_b[AVR_MAX_BLOCKS];
+  /* dims->bn only: eval BatchNorm1d bn_0 of block b as a per-feature affine (d_hidden floats each):
+     a = weight / sqrt(running_var + eps), c = bias - running_mean * a                                 */
+  const float* bn_scale[AVR_MAX_BLOCKS]; const float* bn_shift[AVR_MAX_BLOCKS];
 } avr_resnetfc_weights;
 
 /* Source-view buffers set by NewPixelNeRFNet.encode (models.py:705-734) and

@@ -207,17 +207,34 @@ def _linear(x, W, b):
     return np.add(y, np.asarray(b, F32), out=y)
 
 
+def batch_norm_eval(x, p, prefix, eps=1e-5):
+    """nn.BatchNorm1d in eval mode on (B, C) as ATen's CPU kernel evaluates it:
+    alpha = weight / sqrt(running_var + eps), beta = bias - running_mean * alpha,
+    y = x * alpha + beta (fp32)."""
+    invstd = (F32(1) / np.sqrt(np.asarray(p[prefix + ".running_var"], F32) + F32(eps))).astype(F32)
+    alpha = (invstd * np.asarray(p[prefix + ".weight"], F32)).astype(F32)
+    beta = (np.asarray(p[prefix + ".bias"], F32) - np.asarray(p[prefix + ".running_mean"], F32) * alpha).astype(F32)
+    return (np.asarray(x, F32) * alpha + beta).astype(F32)
+
+
 def resnetfc_forward(zx, p, d_latent, n_blocks, combine_layer):
     """ResnetFC.forward (models.py:541-592) with ResnetBlockFC (:454-470), ReLU,
-    bn=False, use_spade=False, NS=1 (combine_interleaved is the identity)."""
+    use_spade=False, NS=1 (combine_interleaved is the identity). With bn
+    parameters in `p` (train.py --bn, eval mode) every block applies bn_0 in
+    front of BOTH relus, as the reference does (models.py:456-461: bn_1 unused)."""
     z = zx[:, :d_latent]
     x = _linear(zx[:, d_latent:], p["lin_in.weight"], p["lin_in.bias"])
     relu = lambda v: np.maximum(v, F32(0))  # noqa: E731
     for b in range(n_blocks):
         if d_latent > 0 and b < combine_layer:
             x = x + _linear(z, p[f"lin_z.{b}.weight"], p[f"lin_z.{b}.bias"])
-        net = _linear(relu(x), p[f"blocks.{b}.fc_0.weight"], p[f"blocks.{b}.fc_0.bias"])
-        dx = _linear(relu(net), p[f"blocks.{b}.fc_1.weight"], p[f"blocks.{b}.fc_1.bias"])
+        bn = f"blocks.{b}.bn_0"
+        if bn + ".running_mean" in p:
+            net = _linear(relu(batch_norm_eval(x, p, bn)), p[f"blocks.{b}.fc_0.weight"], p[f"blocks.{b}.fc_0.bias"])
+            dx = _linear(relu(batch_norm_eval(net, p, bn)), p[f"blocks.{b}.fc_1.weight"], p[f"blocks.{b}.fc_1.bias"])
+        else:
+            net = _linear(relu(x), p[f"blocks.{b}.fc_0.weight"], p[f"blocks.{b}.fc_0.bias"])
+            dx = _linear(relu(net), p[f"blocks.{b}.fc_1.weight"], p[f"blocks.{b}.fc_1.bias"])
         x = x + dx
     return _linear(relu(x), p["lin_out.weight"], p["lin_out.bias"])
 

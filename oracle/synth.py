@@ -139,4 +139,25 @@ def field_from_meta(g):
         pc = resnetfc_params(d_in, L, d_hidden, n_blocks, combine, int(g["weight_seed_coarse"]))
         pf = resnetfc_params(d_in, L, d_hidden, n_blocks, combine, int(g["weight_seed_fine"]))
         latent = hashed_normalish((1, L) + hw, int(g["latent_seed"]), 1.0)
+    # eval-mode BatchNorm statistics / affine of bn=True nets (stored explicitly in the fixture)
+    for tag, p in (("coarse", pc), ("fine", pf)):
+        pre = f"bn_{tag}."
+        p.update({k[len(pre):]: g[k] for k in g if k.startswith(pre)})
     return pc, pf, latent
+
+
+def bn_params(d_hidden, n_blocks, seed):
+    """Non-trivial eval BatchNorm1d state for every block's bn_0 / bn_1 (the
+    reference creates both; only bn_0 is applied, models.py:456-461): weights
+    of both signs, shifts, running means and variances."""
+    p = {}
+    for b in range(n_blocks):
+        for m in ("bn_0", "bn_1"):
+            s = seed * 100 + 10 * b + (0 if m == "bn_0" else 5)
+            w = hashed_uniform((d_hidden,), s + 1, 0.5, 1.5)
+            sign = np.where(hashed_uniform((d_hidden,), s + 2) < 0.1, -1.0, 1.0).astype(np.float32)
+            p[f"blocks.{b}.{m}.weight"] = (w * sign).astype(np.float32)
+            p[f"blocks.{b}.{m}.bias"] = hashed_uniform((d_hidden,), s + 3, -0.2, 0.2)
+            p[f"blocks.{b}.{m}.running_mean"] = hashed_uniform((d_hidden,), s + 4, -0.3, 0.3)
+            p[f"blocks.{b}.{m}.running_var"] = hashed_uniform((d_hidden,), s + 5, 0.3, 2.0)
+    return p

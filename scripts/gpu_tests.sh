@@ -1,8 +1,8 @@
 #!/bin/bash
-# Selected GPU tests: TESTS="tests/x.py tests/y.py" K="expr" bash scripts/gpu_tests.sh
+# The whole -m gpu suite in one process (per-test timeout), log under gpurun_out/$TAG.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out; mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu ${K:+-k "$K"} -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_sel.log 2>&1
-rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed|max rel" $OUT/pytest_sel.log | tail -40; exit $rc
+OUT=gpurun_out/${TAG:-tests}; mkdir -p $OUT
+timeout -k 10 1000 python -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests/ ${EXTRA:-} > $OUT/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 $OUT/pytest_gpu.log; exit $rc

@@ -142,22 +142,25 @@ def import_reference():
     return ref_utils, ref_renderers, ref_models
 
 
-def build_field(ref_models, d_hidden, n_blocks, combine_layer, num_layers, latent_hw, seed, store_weights):
-    net = ref_models.NewPixelNeRFNet(model_conf(d_hidden, n_blocks, combine_layer, num_layers))
+def build_field(ref_models, d_hidden, n_blocks, combine_layer, num_layers, latent_hw, seed, store_weights, bn=False):
+    net = ref_models.NewPixelNeRFNet(model_conf(d_hidden, n_blocks, combine_layer, num_layers), bn=bn)
     L = net.latent_size
     d_in = net.d_in
     params = {}
     for tag, mlp, s in (("coarse", net.mlp_coarse, seed), ("fine", net.mlp_fine, seed + 17)):
         p = synth.resnetfc_params(d_in, L, d_hidden, n_blocks, combine_layer, s)
+        bnp = synth.bn_params(d_hidden, n_blocks, s) if bn else {}
         sd = mlp.state_dict()
-        for k in p:
+        for k, v in list(p.items()) + list(bnp.items()):
             assert k in sd, k
-            sd[k] = torch.from_numpy(p[k])
+            sd[k] = torch.from_numpy(v)
         assert all(k in p or ".bn_" in k for k in sd), [k for k in sd if k not in p]
         mlp.load_state_dict(sd)
         if store_weights:
             for k, v in p.items():
                 params[f"{tag}.{k}"] = v
+        for k, v in bnp.items():    # eval BatchNorm state: always stored (not hash-regenerated by the tests)
+            params[f"bn_{tag}.{k}"] = v
     poses, focal, c, image_shape, latent_scaling = synth.source_view(latent_hw)
     latent = synth.hashed_normalish((1, L) + tuple(latent_hw), seed + 5, 1.0)
     net.encoder.latent = torch.from_numpy(latent)
@@ -167,7 +170,7 @@ def build_field(ref_models, d_hidden, n_blocks, combine_layer, num_layers, laten
     net.c = torch.from_numpy(c)
     net.image_shape = torch.from_numpy(image_shape)
     net.num_views_per_obj = 1
-    meta = dict(d_hidden=d_hidden, n_blocks=n_blocks, combine_layer=combine_layer, d_latent=L, d_in=d_in,
+    meta = dict(d_hidden=d_hidden, n_blocks=n_blocks, combine_layer=combine_layer, d_latent=L, d_in=d_in, bn=int(bn),
                 latent_hw=np.array(latent_hw), weight_seed_coarse=seed, weight_seed_fine=seed + 17,
                 latent_seed=seed + 5, poses=poses, focal=focal, c=c, image_shape=image_shape,
                 latent_scaling=latent_scaling)
@@ -314,8 +317,13 @@ def g4_field():
         # conf/default_mv.conf:4-21 (5 x 512, combine_layer 3): train.py:262's config
         "mv512": (512, 5, 3, 4, (64, 64), False),
         "d256": (256, 3, 1000, 4, (64, 64), False),
+        # train.py --bn (train.py:210, :265): eval-mode BatchNorm blocks, default.conf and default_mv.conf nets
+        "bn_small": (64, 3, 1000, 1, (8, 8), True),
+        "bn512": (512, 3, 1000, 4, (64, 64), False),
+        "bn_mv512": (512, 5, 3, 4, (64, 64), False),
     }.items():
-        net, meta, params = build_field(REF_M, d_hidden, n_blocks, combine, num_layers, lhw, 40, store)
+        net, meta, params = build_field(REF_M, d_hidden, n_blocks, combine, num_layers, lhw, 40, store,
+                                        bn=tag.startswith("bn"))
         xyz = synth.hashed_uniform((1, B, 3), 41, -0.5, 0.5)
         vd = synth.hashed_uniform((1, B, 3), 42, -1.0, 1.0)
         vd /= np.linalg.norm(vd, axis=-1, keepdims=True).astype(np.float32)

@@ -22,7 +22,7 @@ def build_net(g, device, precision="x3"):
     from avr.models import NewPixelNeRFNet
     pc, pf, latent = synth.field_from_meta(g)
     net = NewPixelNeRFNet(model_conf(int(g["d_hidden"]), int(g["n_blocks"]), int(g["combine_layer"]),
-                                     int(g["d_latent"])))
+                                     int(g["d_latent"])), bn=bool(int(g["bn"])) if "bn" in g else False)
     for mlp, p in ((net.mlp_coarse, pc), (net.mlp_fine, pf)):
         sd = mlp.state_dict()
         for k, v in p.items():

@@ -268,6 +268,42 @@ PRECISIONS = ["fp32", "x3"]
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("tag", ["small", "small_mv", "full", "mv512", "d256"])
 def test_field_points_golden(golden, tag, precision):
+    _field_points_golden(golden, tag, precision)
+
+
+@pytest.mark.parametrize("waves", ["8", "4"])
+@pytest.mark.parametrize("tag", ["bn_small", "bn512", "bn_mv512"])
+def test_field_points_golden_batchnorm(golden, tag, waves, monkeypatch):
+    """train.py --bn nets (eval-mode BatchNorm: bn_0 in front of both relus of
+    every block, models.py:456-461) on the fused x3 kernel, against the
+    reference's own forward (g4 bn fixtures), both 512-wide layouts."""
+    monkeypatch.setenv("AVR_X3_WAVES", waves)
+    if waves == "4" and not tag.endswith("512"):
+        pytest.skip("one layout below 512 wide")
+    _field_points_golden(golden, tag, "x3")
+
+
+def test_field_batchnorm_routes(golden):
+    """BatchNorm nets: fused only on the x3 path in eval mode. precision fp32,
+    train-mode BN (batch statistics) and autograd run the module's PyTorch
+    graph, which matches the reference's eval forward too."""
+    g = golden("g4_field_bn512.npz")
+    net = build_net(g, DEV, "fp32")
+    xyz, vd = T(g["xyz"]), T(g["viewdirs"])
+    with torch.no_grad():
+        assert not net.can_fuse(xyz)
+        np.testing.assert_allclose(to_np(net(xyz, coarse=True, viewdirs=vd)), g["out_coarse"], atol=5e-5, rtol=1e-4)
+        net.field_precision = "x3"
+        assert net.can_fuse(xyz)
+        net.mlp_coarse.train()
+        assert not net.can_fuse(xyz)
+        net.mlp_coarse.eval()
+    for p in net.parameters():
+        p.requires_grad_(True)
+    assert not net.can_train_fused(xyz, vd)
+
+
+def _field_points_golden(golden, tag, precision):
     g = golden(f"g4_field_{tag}.npz")
     net = build_net(g, DEV, precision)
     with torch.no_grad():

@@ -99,7 +99,8 @@ def _compare64(g_hip, g_t32, g_64, floor=3e-5):
     return worst
 
 
-@pytest.mark.parametrize("d_hidden,n_blocks,combine_layer", [(64, 3, 1000), (128, 5, 3), (512, 3, 1000)])
+@pytest.mark.parametrize("d_hidden,n_blocks,combine_layer", [(64, 3, 1000), (128, 5, 3), (512, 3, 1000),
+                                                          (512, 5, 3)])   # (512, 5, 3): conf/default_mv.conf
 def test_field_train_grads_match_torch_autograd(d_hidden, n_blocks, combine_layer):
     from avr.field import _FieldTrain  # noqa: F401  (the path under test)
     d_latent = 512 if d_hidden == 512 else 64

@@ -62,7 +62,7 @@ def test_geometry(golden):
     np.testing.assert_allclose(O.opencv_pixel_coordinates(8, 8), g["opencv_pix_8"], atol=0)
 
 
-@pytest.mark.parametrize("tag", ["small", "small_mv", "full", "mv512", "d256"])
+@pytest.mark.parametrize("tag", ["small", "small_mv", "full", "mv512", "d256", "bn_small", "bn512", "bn_mv512"])
 def test_field(golden, tag):
     g = golden(f"g4_field_{tag}.npz")
     pc, pf, latent = synth.field_from_meta(g)
