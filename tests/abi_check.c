@@ -1,0 +1,132 @@
+/* Host-side argument checks of the C ABI (include/avr.h) under AddressSanitizer
+ * (SURVEY §5 "Race detection / sanitizers": a host -fsanitize=address build of
+ * the library, `make -C adaptive-volume-rendering_amd asan`). Every call below
+ * must be rejected (AVR_E_INVALID / AVR_E_UNSUPPORTED) or be a no-op (zero
+ * work) BEFORE any HIP call, so the harness runs without a GPU; ASan checks
+ * the validation code itself (struct reads, error-string formatting).
+ * Exit status: number of failed checks. Run by tests/test_asan_cpu.py.      */
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "avr.h"
+
+static int failures = 0;
+
+static void expect(const char* what, int got, int want) {
+  if (got != want) {
+    fprintf(stderr, "FAIL %s: got %d want %d (%s)\n", what, got, want, avr_last_error_string());
+    ++failures;
+  } else if (want != AVR_OK && strlen(avr_last_error_string()) == 0) {
+    fprintf(stderr, "FAIL %s: no error string\n", what);
+    ++failures;
+  }
+}
+
+static void check(const char* what, int cond) {
+  if (!cond) {
+    fprintf(stderr, "FAIL %s\n", what);
+    ++failures;
+  }
+}
+
+int main(void) {
+  float buf[64] = {0};
+  int64_t n = 0;
+  check("version", avr_version() == AVR_ABI_VERSION);
+  check("device_count>=0", avr_device_count() >= 0);
+
+  /* geometry / sampling */
+  expect("world_rays null", avr_world_rays(NULL, NULL, NULL, 0, 0, 1, 4, NULL, NULL, NULL), AVR_E_INVALID);
+  expect("world_rays empty", avr_world_rays(NULL, NULL, NULL, 0, 0, 1, 0, NULL, NULL, NULL), AVR_OK);
+  expect("depth null", avr_depth_from_world(NULL, NULL, NULL, NULL, 0, 0, 1, 3, NULL, NULL, NULL), AVR_E_INVALID);
+  expect("coarse bad n", avr_sample_coarse(0.8f, 1.8f, 4, 0, NULL, 0, 0, NULL, buf, NULL), AVR_E_INVALID);
+  expect("coarse neg rays", avr_sample_coarse(0.8f, 1.8f, -1, 8, NULL, 0, 0, NULL, buf, NULL), AVR_E_INVALID);
+  expect("coarse null z", avr_sample_coarse(0.8f, 1.8f, 4, 8, NULL, 0, 0, NULL, NULL, NULL), AVR_E_INVALID);
+  expect("coarse empty", avr_sample_coarse(0.8f, 1.8f, 0, 8, NULL, 0, 0, NULL, NULL, NULL), AVR_OK);
+  expect("rays_coarse null", avr_rays_sample_coarse(NULL, NULL, NULL, 0, 0, 1, 8, 0.8f, 1.8f, 16, NULL, 0, 0, NULL,
+                                                    NULL, NULL, NULL, NULL, NULL), AVR_E_INVALID);
+  expect("coarse_rays null", avr_sample_coarse_rays(NULL, NULL, 4, 8, NULL, 0, 0, NULL, NULL), AVR_E_INVALID);
+  expect("fine null", avr_sample_fine(NULL, NULL, 0.8f, 1.8f, 4, 64, 32, 0, 0.01f, NULL, NULL, NULL, 0, 0, NULL,
+                                      NULL, NULL, NULL, NULL), AVR_E_INVALID);
+  expect("fine nc too big", avr_sample_fine(buf, buf, 0.8f, 1.8f, 4, 257, 32, 0, 0.01f, NULL, NULL, NULL, 0, 0,
+                                            NULL, buf, NULL, NULL, NULL), AVR_E_INVALID);
+  expect("fine total too big", avr_sample_fine(buf, buf, 0.8f, 1.8f, 4, 256, 200, 100, 0.01f, NULL, NULL, NULL, 0,
+                                               0, NULL, buf, NULL, NULL, NULL), AVR_E_INVALID);
+  expect("fine half noise", avr_sample_fine(buf, buf, 0.8f, 1.8f, 4, 64, 32, 0, 0.01f, buf, NULL, NULL, 0, 0, NULL,
+                                            buf, NULL, NULL, NULL), AVR_E_INVALID);
+  expect("fine empty", avr_sample_fine(NULL, NULL, 0.8f, 1.8f, 0, 64, 32, 0, 0.01f, NULL, NULL, NULL, 0, 0, NULL,
+                                       NULL, NULL, NULL, NULL), AVR_OK);
+
+  /* compositing */
+  expect("composite null", avr_composite_fwd(NULL, NULL, 4, 8, 1, 1.8f, NULL, NULL, NULL, NULL), AVR_E_INVALID);
+  expect("composite_depth null", avr_composite_fwd_depth(NULL, NULL, 4, 8, 1, 1.8f, NULL, NULL, NULL, NULL, NULL,
+                                                         NULL, NULL, NULL), AVR_E_INVALID);
+  expect("composite_bwd null", avr_composite_bwd(NULL, NULL, 4, 8, 1, 1.8f, NULL, NULL, NULL, NULL, NULL, NULL),
+         AVR_E_INVALID);
+  expect("march bytes null", avr_march_state_bytes(16, NULL), AVR_E_INVALID);
+  expect("march bytes", avr_march_state_bytes(16, &n), AVR_OK);
+  check("march bytes >0", n > 0);
+
+  /* field */
+  avr_field_dims d;
+  memset(&d, 0, sizeof d);
+  d.d_in = 42; d.d_latent = 512; d.d_hidden = 384; d.n_blocks = 3; d.n_lin_z = 3; d.num_freqs = 6;
+  d.freq_factor = 1.5f; d.precision = AVR_FIELD_X3;
+  expect("packed_floats bad hidden", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
+  d.d_hidden = 512;
+  expect("packed_floats", avr_field_packed_floats(&d, &n), AVR_OK);
+  int64_t plain = n;
+  d.bn = 1;
+  expect("packed_floats bn", avr_field_packed_floats(&d, &n), AVR_OK);
+  check("bn adds 2 x d_hidden per block", n - plain == 2 * 512 * 3);
+  d.bn = 2;
+  expect("packed_floats bad bn", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
+  d.bn = 0;
+  d.n_blocks = AVR_MAX_BLOCKS + 1;
+  expect("packed_floats too many blocks", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
+  d.n_blocks = 3;
+  d.d_in = 40;
+  expect("packed_floats bad d_in", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
+  d.d_in = 42;
+  expect("packed_floats null out", avr_field_packed_floats(&d, NULL), AVR_E_INVALID);
+  avr_resnetfc_weights w;
+  memset(&w, 0, sizeof w);
+  expect("pack null blob", avr_field_pack(&d, &w, NULL, NULL), AVR_E_INVALID);
+  expect("pack null dims", avr_field_pack(NULL, &w, buf, NULL), AVR_E_INVALID);
+  avr_view_desc v;
+  memset(&v, 0, sizeof v);
+  expect("fwd_rays bad latent", avr_field_fwd_rays(&d, &v, buf, buf, NULL, NULL, NULL, 4, 8, NULL, NULL),
+         AVR_E_INVALID);
+  v.latent_h = v.latent_w = 8;
+  expect("fwd_rays null ro", avr_field_fwd_rays(&d, &v, buf, buf, NULL, NULL, NULL, 4, 8, NULL, NULL),
+         AVR_E_INVALID);
+  expect("fwd_rays empty", avr_field_fwd_rays(&d, &v, buf, buf, NULL, NULL, NULL, 0, 8, NULL, NULL), AVR_OK);
+  expect("fwd_points empty", avr_field_fwd_points(&d, &v, buf, buf, NULL, NULL, 0, NULL, NULL), AVR_OK);
+  expect("batch too many scenes", avr_field_fwd_rays_batch(&d, &v, AVR_MAX_SCENES + 1, buf, buf, NULL, NULL, NULL,
+                                                           4, 8, NULL, NULL), AVR_E_INVALID);
+  d.precision = AVR_FIELD_FP32;
+  d.bn = 1;
+  expect("bn on fp32 rejected", avr_field_fwd_points(&d, &v, buf, buf, buf, buf, 4, buf, NULL), AVR_E_INVALID);
+  d.precision = AVR_FIELD_X3;
+  expect("bn training rejected", avr_field_fwd_points_train(&d, &v, 1, buf, buf, buf, buf, 4, buf, buf, 4,
+                                                            (uint32_t*)buf, NULL, NULL), AVR_E_INVALID);
+  d.bn = 0;
+  int64_t act = 0, mw = 0;
+  expect("train sizes", avr_field_train_sizes(&d, 2, 100, &act, &mw), AVR_OK);
+  check("train sizes act", act == (int64_t)7 * 2 * 100 * 512);
+  expect("train sizes bad", avr_field_train_sizes(&d, 0, 100, &act, &mw), AVR_E_INVALID);
+  expect("latent_table null", avr_field_latent_table(&d, NULL, NULL, 8, 8, NULL, NULL), AVR_E_INVALID);
+  expect("wgrad no layers", avr_weight_grads(NULL, 0, 0, 1, NULL), AVR_E_INVALID);
+  expect("latent_features null view", avr_latent_features(NULL, NULL, 4, NULL, 3, NULL, NULL), AVR_E_INVALID);
+  expect("raymarch null", avr_raymarch(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 4, 10, NULL, NULL,
+                                       NULL, NULL), AVR_E_INVALID);
+
+  /* measurement */
+  expect("copy odd size", avr_stream_copy(buf, buf + 8, 15, NULL), AVR_E_INVALID);
+  expect("copy null", avr_stream_copy(NULL, buf, 16, NULL), AVR_E_INVALID);
+  expect("copy empty", avr_stream_copy(NULL, NULL, 0, NULL), AVR_OK);
+
+  printf("abi_check: %d failure(s)\n", failures);
+  return failures;
+}
