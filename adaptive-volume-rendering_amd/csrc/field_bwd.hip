@@ -51,16 +51,18 @@ __device__ __forceinline__ void store_rows(float* G, const floatx4 (&v)[FT][4], 
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) {
       const int64_t m = base + 16 * sg + j;
-      if (m < M) *reinterpret_cast<floatx4*>(G + m * HID + 16 * (FT * wid + ft) + 4 * g) = v[ft][sg];
+      if (m < M) __builtin_nontemporal_store(v[ft][sg], reinterpret_cast<floatx4*>(G + m * HID + 16 * (FT * wid + ft) + 4 * g));
     }
 }
 
-// layer l's rows + its running max |G| (mx: the wave's max |v|)
-template <int FT, int NW>
-__device__ __forceinline__ void store_layer(const BwdArgs& a, int layer, const floatx4 (&v)[FT][4], float mx,
-                                            int64_t base, int64_t roff, int wid, int g, int j, int lane) {
-  store_rows<FT, NW>(a.G + layer * a.g_stride + roff * (16 * FT * NW), v, base, a.M, wid, g, j);
-  if (a.g_max && lane == 0) atomicMax(a.g_max + layer, __float_as_uint(mx));
+// G rows of `layer` copied out of the LDS operand by a GEMM side task (x3_gemm.h RowSideH): lane (g, j)
+// of wave w copies sample 16 w + j
+template <int HID>
+__device__ __forceinline__ RowSideH<HID> grad_side(const BwdArgs& a, int layer, float s_x, int64_t base, int64_t roff,
+                                                   int wid) {
+  RowSideH<HID> rs;
+  rs.template init<HID>(a.G + (int64_t)layer * a.g_stride + (roff + base) * HID, s_x, a.M - base, wid);
+  return rs;
 }
 
 template <int FT>
@@ -89,7 +91,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   extern __shared__ float lds[];
   uint4* X16 = reinterpret_cast<uint4*>(lds);   // KC chunks x 8 KiB, the forward's operand layout
   float* red = lds + KC * 2048;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* lmax = red + 16;                       // per-layer workgroup max |G| (kX3MaxLayers)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, j = lane & 15;
   const int scene = (int)(blockIdx.x / a.blocks_per_scene);   // the forward's workgroup -> scene map
   const int64_t base = (int64_t)(blockIdx.x - (int64_t)scene * a.blocks_per_scene) * kX3Samples;
@@ -130,39 +133,46 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   FragX3 A0[FT];
   for (int b = nb - 1; b >= 0; --b) {
     // ---- fc_1^T
+    // G[2b + 1] = dx and G[2b] are the operands of the two GEMMs: their rows are copied out of
+    // LDS during those GEMMs (RowSide), not stored as a burst ahead of the weight loads
     float mx = absmax<FT>(dx);
-    store_layer<FT, NW>(a, 2 * b + 1, dx, mx, base, roff, wid, g, j, lane);
     const uint4* W1 = PB + a.LB.fc1t[b] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W1, lane);
-    float s_x = publish<FT, NW>(X16, dx, mx, red, wid, lane, g, j);
+    float s_x = publish<FT, NW>(X16, dx, mx, red, wid, lane, g, j, &lmax[2 * b + 1]);
     load_mask<FT, NW>(mb, a.mask, 2 * b + 1, lane, wid);
-    gemm_x3<FT, true, false>(t, A0, W1, KC, 64 * NTT, X16, lane);
+    gemm_x3<FT, true, false>(t, A0, W1, KC, 64 * NTT, X16, lane, grad_side<HID>(a, 2 * b + 1, s_x, base, roff, wid));
     float inv = 1.0f / (bwd_scale(a.packed_bwd, 3 + 2 * b) * s_x);
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
       for (int sg = 0; sg < 4; ++sg) t[ft][sg] = masked<FT>(t[ft][sg] * inv, mb, ft, sg);
     mx = absmax<FT>(t);
-    store_layer<FT, NW>(a, 2 * b, t, mx, base, roff, wid, g, j, lane);
     // ---- fc_0^T
     const uint4* W0 = PB + a.LB.fc0t[b] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT>(A0, W0, lane);
-    s_x = publish<FT, NW>(X16, t, mx, red, wid, lane, g, j);
+    s_x = publish<FT, NW>(X16, t, mx, red, wid, lane, g, j, &lmax[2 * b]);
     load_mask<FT, NW>(mb, a.mask, 2 * b, lane, wid);
-    gemm_x3<FT, true, false>(t, A0, W0, KC, 64 * NTT, X16, lane);
+    gemm_x3<FT, true, false>(t, A0, W0, KC, 64 * NTT, X16, lane, grad_side<HID>(a, 2 * b, s_x, base, roff, wid));
     inv = 1.0f / (bwd_scale(a.packed_bwd, 2 + 2 * b) * s_x);
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
       for (int sg = 0; sg < 4; ++sg) dx[ft][sg] += masked<FT>(t[ft][sg] * inv, mb, ft, sg);
   }
-  store_layer<FT, NW>(a, 2 * nb, dx, absmax<FT>(dx), base, roff, wid, g, j, lane);
+  // G_in (nothing waits on these stores any more), then the layer maxima: one atomic per workgroup and
+  // layer for the GEMM operands (the workgroup max publish recorded), one per wave for G_in
+  store_rows<FT, NW>(a.G + 2 * nb * a.g_stride + roff * HID, dx, base, a.M, wid, g, j);
+  if (a.g_max) {
+    const float mx_in = absmax<FT>(dx);
+    if (lane == 0) atomicMax(a.g_max + 2 * nb, __float_as_uint(mx_in));
+    if (wid == 0 && lane < 2 * nb) atomicMax(a.g_max + lane, __float_as_uint(lmax[lane]));
+  }
 }
 
 template <int FT, int NW>
 static int launch_bwd(const BwdArgs& a, hipStream_t s) {
   constexpr int HID = 16 * FT * NW;
-  const size_t shm = (size_t)(HID / 32) * 8192 + 64;
+  const size_t shm = (size_t)(HID / 32) * 8192 + 64 + 4 * kX3MaxLayers;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bwd_x3_kernel<FT, NW>),

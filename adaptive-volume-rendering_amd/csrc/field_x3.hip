@@ -48,6 +48,7 @@ struct ZTail {
   int uniq[256];         // [slot] texel
   float red[16];
   int wtot[4];
+  float lmax[kX3MaxLayers];   // training forward: max of each saved layer over the workgroup
 };
 constexpr unsigned kEmpty = 0xffffffffu;
 
@@ -188,22 +189,27 @@ struct LdsPlan {
   static_assert(CAP * (4 * HID >= 1024 ? HID / 256 : 1) <= 4 * 64, "stage_rows: one lane per piece");
 };
 
-#ifdef AVR_STAMPS
+#if defined(AVR_DIAG_ONE_LAYER)   // timing-only diagnostic: every block reads block 0's weights (L2-resident)
+#define DBG_B(b) 0
+#elif defined(AVR_STAMPS)
 #define DBG_B(b) ((a.debug & 1) ? 0 : (b))
 #else
 #define DBG_B(b) (b)
 #endif
 
 // Training forward: GEMM input `layer` (relu'd, true scale) -> act rows and
-// its relu mask bits -> mask (both consumed by the backward pass).
-// mx: the wave's max of v (v >= 0), folded into the layer's max for the
-// weight-gradient split scales.
+// its relu mask bits -> mask (both consumed by the backward pass); the
+// workgroup's max of the layer goes to tail->lmax (publish). Called after the
+// next GEMM's weight prefetch (vmcnt retires in order: the first weight waits
+// then do not wait for these stores). The rows are stored non-temporally: 4 B
+// per value of every layer stream through once (4.4 GB per default_mv fine
+// pass), and allocating them in L2 evicts the weights (same-box A/B,
+// scripts/gpu_train_prof.sh: 5.16 -> 3.88 ms per fine-pass launch).
 template <int FT, int NW>
-__device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const floatx4 (&v)[FT][4], float mx,
-                                           int64_t base, int64_t roff, int wid, int g, int j, int lane) {
+__device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const floatx4 (&v)[FT][4], int64_t base,
+                                           int64_t roff, int wid, int g, int j, int lane) {
   constexpr int HID = 16 * FT * NW, MW = mask_words(FT);
   float* act = a.act + (int64_t)layer * a.act_stride + roff * HID;
-  if (a.act_max && lane == 0) atomicMax(a.act_max + layer, __float_as_uint(mx));
   unsigned bits[MW];
 #pragma unroll
   for (int q = 0; q < MW; ++q) bits[q] = 0u;
@@ -213,7 +219,9 @@ __device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const 
     for (int sg = 0; sg < 4; ++sg) {
       const floatx4 x = v[ft][sg];
       const int64_t m = base + 16 * sg + j;
-      if (m < a.M) *reinterpret_cast<floatx4*>(act + m * HID + 16 * (FT * wid + ft) + 4 * g) = x;
+#ifndef AVR_DIAG_NO_ACT_STORE   // timing-only diagnostic: the act rows are not written
+      if (m < a.M) __builtin_nontemporal_store(x, reinterpret_cast<floatx4*>(act + m * HID + 16 * (FT * wid + ft) + 4 * g));
+#endif
       const int idx = (ft * 4 + sg) * 4;
       const unsigned nib = (x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) | (x.w > 0.f ? 8u : 0u);
       bits[idx >> 5] |= nib << (idx & 31);
@@ -422,7 +430,6 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       else mx = prep_bn<FT>(v, h, 1.0f / S_h, bn_a, bn_c, wid, g);
     }
     AVR_STAMP(5 + 5 * (b & 3));
-    if (SAVE) save_layer<FT, NW>(a, 2 * b, v, mx, base, roff, wid, g, j, lane);
     const uint4* W0 = P16 + L.x3_fc0[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
     const uint4* W1 = P16 + L.x3_fc1[DBG_B(b)] / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT, NPF>(A0, W0, lane);
@@ -454,7 +461,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       S_h = S1;
       gemm<FT, false, TWO>(h, A0, W1, KC, 64 * NTT, X16, lane);
     } else {
-      s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+      if (SAVE) save_layer<FT, NW>(a, 2 * b, v, base, roff, wid, g, j, lane);
+      s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j, SAVE ? &tail->lmax[2 * b] : nullptr);
       AVR_STAMP(6 + 5 * (b & 3));
       // fc_0 (from zero)
       const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
@@ -462,9 +470,9 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       AVR_STAMP(7 + 5 * (b & 3));
       // fc_1 input relu(t + b0)
       mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
-      if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, mx, base, roff, wid, g, j, lane);
       prefetch_a<FT, NPF>(A0, W1, lane);
-      s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+      if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, base, roff, wid, g, j, lane);
+      s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j, SAVE ? &tail->lmax[2 * b + 1] : nullptr);
       AVR_STAMP(8 + 5 * (b & 3));
       // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
       const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
@@ -552,8 +560,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
   } else {
     mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
-    if (SAVE) save_layer<FT, NW>(a, 2 * a.n_blocks, v, mx, base, roff, wid, g, j, lane);
-    s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j);
+    if (SAVE) save_layer<FT, NW>(a, 2 * a.n_blocks, v, base, roff, wid, g, j, lane);
+    s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j, SAVE ? &tail->lmax[2 * a.n_blocks] : nullptr);
   }
   if (wid < 4) {
 #pragma unroll
@@ -579,6 +587,12 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   const int64_t m = base + 16 * wid + j;
   if (g == 0 && m < a.M)
     a.out[roff + m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
+  if constexpr (SAVE) {
+    // the layer maxima: one atomic per workgroup and layer, issued last (nothing waits on them here;
+    // one per wave and layer in front of the weight loads cost ~1 ms per default_mv fine pass)
+    const int nl = 2 * a.n_blocks + 1;
+    if (a.act_max && wid == 0 && lane < nl) atomicMax(a.act_max + lane, __float_as_uint(tail->lmax[lane]));
+  }
 }
 
 template <int FT, int NW, bool SAVE, bool BN = false>

@@ -57,6 +57,64 @@ __device__ __forceinline__ void split4(const floatx4& x, float s, uint2& hi, uin
   lo = make_uint2(l0, l1);
 }
 
+// Side task of a GEMM (the backward kernel, RowSideH): copy the GEMM's own operand X out of
+// LDS as fp32 rows while the MFMAs run, so the row stores spread over the K
+// loop instead of bursting ahead of it (a burst queues in front of the next
+// weight loads: vmcnt retires in order). NoSide: inference.
+struct NoSide {
+  __device__ __forceinline__ void load(const uint4*, int) {}
+  __device__ __forceinline__ void store(int) {}
+};
+
+// Lane (g, j) of wave w copies slot pair (chunk c, g, sample 16 w + j) of X:
+// features 32c + 4g .. +3 and 32c + 16 + 4g .. +3 of that sample, each value
+// (hi + lo) / s_x -- the operand the GEMM multiplies (exact in fp32: hi and lo
+// hold <= 22 significant bits together; 1 / s_x is a power of two). Only
+// wave-uniform fields (SGPRs): the lane's sample and group are re-derived
+// from its id at each use, so the task holds just the 8 VGPRs in flight.
+struct RowSide {
+  __amdgpu_buffer_rsrc_t rows;   // rows of the workgroup's samples 0 .. nvalid-1 (raw buffer: stores
+                                 // past the last existing row are dropped by the hardware, no branch)
+  float inv;                     // 1 / s_x
+  int wid;
+  uint4 h, l;
+  template <int HID>
+  __device__ __forceinline__ void init(float* rows0, float s_x, int64_t nrows, int w) {
+    const int nvalid = nrows < 64 ? (int)nrows : 64;
+    rows = __builtin_amdgcn_make_buffer_rsrc(rows0, 0, nvalid * HID * 4, 0x00020000);
+    inv = 1.0f / s_x;
+    wid = w;
+  }
+  __device__ __forceinline__ void load(const uint4* X16, int c) {
+    const int lane = __lane_id(), s = 16 * wid + (lane & 15), g = lane >> 4;
+    h = X16[xidx(c, 0, g, s)];
+    l = X16[xidx(c, 1, g, s)];
+  }
+  template <int HID>
+  __device__ __forceinline__ void store_hid(int c) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = __lane_id(), s = 16 * wid + (lane & 15), g = lane >> 4;
+    const half8 hh = __builtin_bit_cast(half8, h), ll = __builtin_bit_cast(half8, l);
+    floatx4 a, b;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] = ((float)hh[e] + (float)ll[e]) * inv;
+      b[e] = ((float)hh[e + 4] + (float)ll[e + 4]) * inv;
+    }
+    const int off = 4 * (s * HID + 32 * c + 4 * g);
+    // non-temporal (aux bit 1 = nt): the rows stream through once; allocated in L2 they evict the weights
+    // (scripts/gpu_train_prof.sh sweep of sc0 / sc1 / nt: nt alone is fastest, 3.69 -> 2.94 ms per
+    // default_mv fine-pass backward)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), rows, off, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), rows, off + 64, 0, 2);
+  }
+};
+
+template <int HID>
+struct RowSideH : RowSide {
+  __device__ __forceinline__ void store(int c) { store_hid<HID>(c); }
+};
+
 // One K-chunk on resident fragments A (this wave's FT tiles) and B (the 4
 // sample groups), in feature-tile pairs: pair p issues its 3 x 2 x 4 chained
 // v_mfma_f32_16x16x32_f16 (each accumulation chain issues back to back at full
@@ -64,10 +122,12 @@ __device__ __forceinline__ void split4(const floatx4& x, float s, uint2& hi, uin
 // into An, one load per few MFMAs (sched_group_barrier), so every A load has a
 // whole chunk of MFMAs to land in and its issue hides in the MFMA gaps. In the
 // last pair each B[sg] is refilled with the next chunk's fragment as soon as
-// its MFMAs have issued.
-template <int FT, bool ZERO>
+// its MFMAs have issued. The side task reads its slots of chunk cc in pair 0
+// and converts / stores them in pair 1 (in pair 0's tail for a single pair).
+template <int FT, bool ZERO, typename Side = NoSide>
 __device__ __forceinline__ void chunk_step(floatx4 (&acc)[FT][4], const FragX3 (&A)[FT], FragX3 (&An)[FT],
-                                           const uint4* wn, BPair (&B)[4], const uint4* X16, int cn, int g, int j) {
+                                           const uint4* wn, BPair (&B)[4], const uint4* X16, int cn, int g, int j,
+                                           Side& side, int cc) {
   constexpr int GS = FT >= 2 ? 2 : 1;       // tiles per group
   constexpr int NG = FT / GS;
   constexpr int NMF = 3 * GS * 4;           // MFMAs per group
@@ -75,6 +135,7 @@ __device__ __forceinline__ void chunk_step(floatx4 (&acc)[FT][4], const FragX3 (
   constexpr int PER = NMF / (NLD + 1);
 #pragma unroll
   for (int p = 0; p < NG; ++p) {
+    if (p == 0) side.load(X16, cc);
 #pragma unroll
     for (int q = 0; q < GS; ++q) An[GS * p + q] = load_frag(wn + 2 * 64 * (GS * p + q));
 #pragma unroll
@@ -96,6 +157,7 @@ __device__ __forceinline__ void chunk_step(floatx4 (&acc)[FT][4], const FragX3 (
     __builtin_amdgcn_sched_group_barrier(0x008, NMF - NLD * PER, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
+  side.store(cc);
 }
 
 // acc (+)= W . X over KC chunks (KC even, runtime; ZERO: acc starts from 0).
@@ -116,10 +178,10 @@ __device__ __forceinline__ void prefetch_a(FragX3 (&A0)[FT], const uint4* __rest
   for (int ft = 0; ft < (FT < NPF ? FT : NPF); ++ft) A0[ft] = load_frag(W + (unsigned)(lane + 2 * 64 * ft));
 }
 
-// A0 holds chunk 0 (prefetch_a).
-template <int FT, bool ZERO, bool SYNC>
+// A0 holds chunk 0 (prefetch_a). side: an optional side task per K-chunk (RowSide).
+template <int FT, bool ZERO, bool SYNC, typename Side = NoSide>
 __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W, int KC,
-                                        int cstride, const uint4* X16, int lane) {
+                                        int cstride, const uint4* X16, int lane, Side side = Side{}) {
   const int g = lane >> 4, j = lane & 15;
   const uint4* wl = W + lane;
   FragX3 A1[FT];
@@ -134,10 +196,10 @@ __device__ __forceinline__ void gemm_x3(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT],
     const uint4* w1 = wl + (int64_t)2 * (c + 1) * cstride;
     const uint4* w2 = wl + (int64_t)2 * c2 * cstride;
     if (ZERO && c == 0)
-      chunk_step<FT, true>(acc, A0, A1, w1, B, X16, c + 1, g, j);
+      chunk_step<FT, true>(acc, A0, A1, w1, B, X16, c + 1, g, j, side, c);
     else
-      chunk_step<FT, false>(acc, A0, A1, w1, B, X16, c + 1, g, j);
-    chunk_step<FT, false>(acc, A1, A0, w2, B, X16, c2, g, j);
+      chunk_step<FT, false>(acc, A0, A1, w1, B, X16, c + 1, g, j, side, c);
+    chunk_step<FT, false>(acc, A1, A0, w2, B, X16, c2, g, j, side, c + 1);
     // two waves per SIMD: the older one would otherwise win the MFMA pipe and
     // run a whole layer ahead, leaving its partner's epilogue unoverlapped;
     // a plain barrier every two chunks keeps them in step (the MFMA pipe stays
@@ -368,12 +430,15 @@ __device__ __forceinline__ float red_max(const float* red) {
 
 // relu'd layer input -> LDS (two barriers: all reads of the previous X done /
 // all writes of the new X visible); returns the operand scale s_x
+// wgmax (training kernels): wave 0 records the workgroup's max there (LDS)
 template <int FT, int NW>
 __device__ __forceinline__ float publish(uint4* X16, const floatx4 (&v)[FT][4], float mx, float* red, int wid,
-                                         int lane, int g, int j) {
+                                         int lane, int g, int j, float* wgmax = nullptr) {
   if (lane == 0) red[wid] = mx;
   lds_barrier();
-  const float s_x = pow2_scale_for(red_max<NW>(red));
+  const float m = red_max<NW>(red);
+  if (wgmax && wid == 0 && lane == 0) *wgmax = m;
+  const float s_x = pow2_scale_for(m);
   store_split<FT>(X16, v, s_x, wid, g, j);
   lds_barrier();
   return s_x;
