@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -27,7 +27,7 @@ c_float = ctypes.c_float
 class FieldDims(ctypes.Structure):
     _fields_ = [("d_in", c_int), ("d_latent", c_int), ("d_hidden", c_int), ("n_blocks", c_int),
                 ("n_lin_z", c_int), ("num_freqs", c_int), ("freq_factor", c_float), ("precision", c_int),
-                ("bn", c_int)]
+                ("bn", c_int), ("spade", c_int), ("beta", c_float)]
 
 
 FIELD_FP32 = 0
@@ -39,7 +39,8 @@ class ResnetFCWeights(ctypes.Structure):
                 ("fc0_w", c_void_p * AVR_MAX_BLOCKS), ("fc0_b", c_void_p * AVR_MAX_BLOCKS),
                 ("fc1_w", c_void_p * AVR_MAX_BLOCKS), ("fc1_b", c_void_p * AVR_MAX_BLOCKS),
                 ("lin_z_w", c_void_p * AVR_MAX_BLOCKS), ("lin_z_b", c_void_p * AVR_MAX_BLOCKS),
-                ("bn_scale", c_void_p * AVR_MAX_BLOCKS), ("bn_shift", c_void_p * AVR_MAX_BLOCKS)]
+                ("bn_scale", c_void_p * AVR_MAX_BLOCKS), ("bn_shift", c_void_p * AVR_MAX_BLOCKS),
+                ("scale_z_w", c_void_p * AVR_MAX_BLOCKS), ("scale_z_b", c_void_p * AVR_MAX_BLOCKS)]
 
 
 class ViewDesc(ctypes.Structure):

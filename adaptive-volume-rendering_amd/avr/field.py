@@ -23,6 +23,25 @@ def uses_bn(mlp):
     return any(getattr(blk, "bn", False) for blk in getattr(mlp, "blocks", ()))
 
 
+def softplus_beta(mlp):
+    """beta of a ResnetFC(beta > 0) (models.py:442-445, 536-537: Softplus(beta) everywhere the
+    ReLU would be), 0.0 for ReLU nets, None for anything else (torch's default threshold 20 only)."""
+    acts = [mlp.activation] + [blk.activation for blk in mlp.blocks]
+    if all(isinstance(a, torch.nn.ReLU) for a in acts):
+        return 0.0
+    if all(isinstance(a, torch.nn.Softplus) and a.threshold == 20 and a.beta > 0 for a in acts):
+        betas = {float(a.beta) for a in acts}
+        if len(betas) == 1:
+            return betas.pop()
+    return None
+
+
+def inference_only(mlp):
+    """ResnetFC options the x3 kernel runs for inference only (training: the module path):
+    eval BatchNorm, use_spade, Softplus."""
+    return uses_bn(mlp) or getattr(mlp, "use_spade", False) or bool(softplus_beta(mlp))
+
+
 def _bn_ok(blk):
     """Eval-mode BatchNorm with running statistics: a per-feature affine the
     x3 kernel applies (training-mode BN needs cross-sample statistics: module
@@ -33,12 +52,18 @@ def _bn_ok(blk):
 
 
 def _resnetfc_ok(mlp, d_in, d_latent, precision="x3"):
-    return (mlp is not None and type(mlp).__name__ == "ResnetFC" and getattr(mlp, "d_in", -1) == d_in
+    if not (mlp is not None and type(mlp).__name__ == "ResnetFC" and getattr(mlp, "d_in", -1) == d_in
             and mlp.d_latent == d_latent and mlp.d_out == 4 and mlp.d_hidden in (64, 128, 256, 512)
-            and not getattr(mlp, "use_spade", False) and isinstance(mlp.activation, torch.nn.ReLU)
-            and 1 <= mlp.n_blocks <= _lib.AVR_MAX_BLOCKS
-            and all((not blk.bn or (precision == "x3" and _bn_ok(blk))) and blk.shortcut is None
-                    and isinstance(blk.activation, torch.nn.ReLU) for blk in mlp.blocks))
+            and 1 <= mlp.n_blocks <= _lib.AVR_MAX_BLOCKS and all(blk.shortcut is None for blk in mlp.blocks)):
+        return False
+    beta = softplus_beta(mlp)
+    spade = getattr(mlp, "use_spade", False)
+    bn = uses_bn(mlp)
+    if beta is None or ((spade or beta > 0 or bn) and precision != "x3"):
+        return False          # the fp32 kernel runs the default ReLU net only
+    if bn and (spade or beta > 0):
+        return False          # BatchNorm with use_spade / Softplus: module path
+    return all(not blk.bn or _bn_ok(blk) for blk in mlp.blocks)
 
 
 def fused_eligible(net):
@@ -87,6 +112,11 @@ class _Packed:
 PRECISIONS = {"fp32": _lib.FIELD_FP32, "x3": _lib.FIELD_X3}
 
 
+def n_tables(dims):
+    """Per-texel tables of a packed net: lin_z[b], then scale_z[b] with use_spade."""
+    return dims.n_lin_z * (2 if dims.spade else 1)
+
+
 class FusedField:
     """precision: "x3" (default) = split-fp16 MFMA (3 products per fp32 product,
     fp32 accumulation, within fp32 noise of the fp32 path); "fp32" = fp32 MFMA."""
@@ -108,7 +138,8 @@ class FusedField:
         code = self.net.code
         return FieldDims(self.net.d_in, self.net.d_latent, mlp.d_hidden, mlp.n_blocks,
                          min(mlp.combine_layer, mlp.n_blocks), code.num_freqs, _freq_factor(code),
-                         PRECISIONS[self.precision], int(uses_bn(mlp)))
+                         PRECISIONS[self.precision], int(uses_bn(mlp)), int(getattr(mlp, "use_spade", False)),
+                         float(softplus_beta(mlp) or 0.0))
 
     def packed(self, coarse):
         mlp = self._mlp(coarse)
@@ -148,6 +179,8 @@ class FusedField:
             w.fc1_w[b], w.fc1_b[b] = P(blk.fc_1.weight), P(blk.fc_1.bias)
         for b in range(dims.n_lin_z):
             w.lin_z_w[b], w.lin_z_b[b] = P(mlp.lin_z[b].weight), P(mlp.lin_z[b].bias)
+            if dims.spade:   # scale_z[b](z) * x + lin_z[b](z) (models.py:585-587): both as per-texel tables
+                w.scale_z_w[b], w.scale_z_b[b] = P(mlp.scale_z[b].weight), P(mlp.scale_z[b].bias)
         require_device(*keep)
         call("avr_field_pack", ctypes.byref(dims), ctypes.byref(w), ptr(packed), stream_of(packed))
         entry = _Packed(dims, packed, None)
@@ -181,7 +214,7 @@ class FusedField:
         L, H, W = lat.shape[1:]
         latent = lat[sb].detach().to(F32).contiguous()
         require_device(latent)
-        table = torch.empty(max(dims.n_lin_z, 1), H * W, dims.d_hidden, device=latent.device, dtype=F32)
+        table = torch.empty(max(n_tables(dims), 1), H * W, dims.d_hidden, device=latent.device, dtype=F32)
         call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W, ptr(table),
              stream_of(table))
         entry.tables[sb] = (key, table, lat)  # holding `lat` keeps its address from being reused
@@ -189,7 +222,7 @@ class FusedField:
 
     def tables_batch(self, coarse, n_scenes):
         """The lin_z tables of scenes 0 .. n_scenes-1 back to back, (n_scenes,
-        max(n_lin_z, 1), H*W, d_hidden): one buffer for the training launches."""
+        max(n_tables, 1), H*W, d_hidden): one buffer for the training launches."""
         entry = self.packed(coarse)
         lat = self.net.encoder.latent
         key = (n_scenes, lat.data_ptr(), lat._version, tuple(lat.shape))
@@ -198,7 +231,7 @@ class FusedField:
             return hit[1]
         dims = entry.dims
         L, H, W = lat.shape[1:]
-        out = torch.empty(n_scenes, max(dims.n_lin_z, 1), H * W, dims.d_hidden, device=lat.device, dtype=F32)
+        out = torch.empty(n_scenes, max(n_tables(dims), 1), H * W, dims.d_hidden, device=lat.device, dtype=F32)
         for sb in range(n_scenes):
             latent = lat[min(sb, lat.shape[0] - 1)].detach().to(F32).contiguous()
             call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W, ptr(out[sb]),

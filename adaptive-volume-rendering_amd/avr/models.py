@@ -272,10 +272,10 @@ class NewPixelNeRFNet(nn.Module):
         """Autograd on the HIP path (avr.field._FieldTrain): parameters, the
         latent or the points need gradients (VolumeRenderer training; the
         adaptive renderer's band points); view directions must not."""
-        from .field import fused_eligible, uses_bn
+        from .field import fused_eligible, inference_only
         return (self.use_fused and self.hip_backward and xyz.is_cuda and torch.is_grad_enabled()
                 and viewdirs is not None and not viewdirs.requires_grad and fused_eligible(self)
-                and not any(uses_bn(m) for m in (self.mlp_coarse, self.mlp_fine) if m is not None))
+                and not any(inference_only(m) for m in (self.mlp_coarse, self.mlp_fine) if m is not None))
 
     def forward(self, xyz, coarse=True, viewdirs=None, far=False, return_features=False):
         if not return_features and self.can_fuse(xyz):

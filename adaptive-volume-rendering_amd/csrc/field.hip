@@ -68,6 +68,19 @@ static int make_layout(const avr_field_dims* d, Layout* L) {
     L->bn_a[b] = L->bn_c[b] = 0;
     if (d->bn) { L->bn_a[b] = o; o += d->d_hidden; L->bn_c[b] = o; o += d->d_hidden; }
   }
+  AVR_REQUIRE(d->spade == 0 || d->spade == 1, "field: spade must be 0 or 1");
+  AVR_REQUIRE(d->beta >= 0.f && d->beta < 1e30f, "field: beta must be >= 0 (0: ReLU)");
+  AVR_REQUIRE(!(d->beta > 0.f && d->bn), "field: Softplus with BatchNorm runs on the module path");
+  AVR_REQUIRE(!(d->spade && d->bn), "field: use_spade with BatchNorm runs on the module path");
+  L->spade = d->spade;
+  L->n_lin_z = d->n_lin_z;
+  L->n_tables = d->n_lin_z * (d->spade ? 2 : 1);
+  for (int b = 0; b < AVR_MAX_BLOCKS; ++b) L->scale_z[b] = 0;
+  for (int t = 0; t < 2 * AVR_MAX_BLOCKS; ++t) L->b_tab[t] = 0;
+  if (d->spade) {
+    for (int b = 0; b < d->n_lin_z; ++b) { L->scale_z[b] = o; o += (int64_t)L->KTl * NT * tile; }
+    for (int t = 0; t < L->n_tables; ++t) { L->b_tab[t] = o; o += d->d_hidden; }
+  }
   L->total = o;
   return AVR_OK;
 }
@@ -305,7 +318,13 @@ __global__ void __launch_bounds__(256, 1) field_fwd_kernel(FieldArgs a) {
   if (g == 0 && valid) a.out[m] = make_float4(sigmoidf_(o.x), sigmoidf_(o.y), sigmoidf_(o.z), fmaxf(o.w, 0.f));
 }
 
+// Table t's weights: lin_z[t], then (use_spade) scale_z[t - n_lin_z].
+__device__ __forceinline__ int64_t table_weights(const Layout& L, int t) {
+  return t < L.n_lin_z ? L.lin_z[t] : L.scale_z[t - L.n_lin_z];
+}
+
 // table[b][texel][f] = sum_c Wz_b[f][c] latent[c][texel]  (16 texels per wave)
+// (+ the table's bias with use_spade)
 template <int NT>
 __global__ void __launch_bounds__(256, 1) latent_table_kernel(const float* __restrict__ packed, Layout L,
                                                               const float* __restrict__ latent, int HW,
@@ -327,7 +346,11 @@ __global__ void __launch_bounds__(256, 1) latent_table_kernel(const float* __res
 #pragma unroll
   for (int ot = 0; ot < NT; ++ot) acc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
   constexpr int P = NT >= 16 ? 16 : NT;
-  gemm_tiles<NT, P>(acc, reinterpret_cast<const floatx4*>(packed + L.lin_z[b]), L.KTl, slab, lane);
+  gemm_tiles<NT, P>(acc, reinterpret_cast<const floatx4*>(packed + table_weights(L, b)), L.KTl, slab, lane);
+  if (L.spade) {
+#pragma unroll
+    for (int ot = 0; ot < NT; ++ot) acc[ot] += *reinterpret_cast<const floatx4*>(packed + L.b_tab[b] + 16 * ot + 4 * g);
+  }
   if (valid) {
     float* dst = table + ((int64_t)b * HW + texel) * (NT * 16) + 4 * g;
 #pragma unroll
@@ -362,8 +385,13 @@ __global__ void __launch_bounds__(256) latent_table_split_kernel(const float* __
   floatx4 acc[NWT];
 #pragma unroll
   for (int ot = 0; ot < NWT; ++ot) acc[ot] = floatx4{0.f, 0.f, 0.f, 0.f};
-  gemm_tiles<NWT, P, NT>(acc, reinterpret_cast<const floatx4*>(packed + L.lin_z[b]) + NWT * wid * 64, L.KTl, lds,
-                         lane);
+  gemm_tiles<NWT, P, NT>(acc, reinterpret_cast<const floatx4*>(packed + table_weights(L, b)) + NWT * wid * 64, L.KTl,
+                         lds, lane);
+  if (L.spade) {
+#pragma unroll
+    for (int ot = 0; ot < NWT; ++ot)
+      acc[ot] += *reinterpret_cast<const floatx4*>(packed + L.b_tab[b] + 16 * (NWT * wid + ot) + 4 * g);
+  }
   if (valid) {
     float* dst = table + ((int64_t)b * HW + texel) * (NT * 16) + 16 * NWT * wid + 4 * g;
 #pragma unroll
@@ -477,6 +505,7 @@ static int field_common(const avr_field_dims* dims, const avr_view_desc* view, c
   a->n_lin_z = dims->n_lin_z;
   a->num_freqs = dims->num_freqs;
   a->freq_factor = dims->freq_factor;
+  a->beta = dims->beta;
   return AVR_OK;
 }
 
@@ -484,6 +513,7 @@ static int dispatch_field(const avr_field_dims* dims, const FieldArgs& a, hipStr
   const int d_hidden = dims->d_hidden;
   if (dims->precision == AVR_FIELD_X3) return dispatch_field_x3(d_hidden, a, s);
   AVR_REQUIRE(!dims->bn, "field: BatchNorm nets run on the x3 path only");
+  AVR_REQUIRE(!dims->spade && !(dims->beta > 0.f), "field: use_spade / Softplus nets run on the x3 path only");
   AVR_REQUIRE(dims->precision == AVR_FIELD_FP32, "field: unknown precision %d", dims->precision);
   switch (d_hidden) {
     case 64: return launch_field<4>(a, s);
@@ -528,13 +558,21 @@ extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_wei
     if ((rc = pack_linear(w->fc0_w[b], H, H, NT, NT, packed + L.fc0[b], s))) return rc;
     if ((rc = pack_linear(w->fc1_w[b], H, H, NT, NT, packed + L.fc1[b], s))) return rc;
     if ((rc = pack_bias(w->fc0_b[b], nullptr, H, H, packed + L.b_fc0[b], s))) return rc;
-    const float* bz = (b + 1 < dims->n_lin_z) ? w->lin_z_b[b + 1] : nullptr;
+    const float* bz = (b + 1 < dims->n_lin_z && !dims->spade) ? w->lin_z_b[b + 1] : nullptr;
     if ((rc = pack_bias(w->fc1_b[b], bz, H, H, packed + L.b_fc1[b], s))) return rc;
   }
   for (int b = 0; b < dims->n_lin_z; ++b)
     if ((rc = pack_linear(w->lin_z_w[b], H, dims->d_latent, NT, L.KTl, packed + L.lin_z[b], s))) return rc;
-  if ((rc = pack_bias(w->lin_in_b, dims->n_lin_z > 0 ? w->lin_z_b[0] : nullptr, H, H, packed + L.b_in, s)))
+  if ((rc = pack_bias(w->lin_in_b, dims->n_lin_z > 0 && !dims->spade ? w->lin_z_b[0] : nullptr, H, H,
+                      packed + L.b_in, s)))
     return rc;
+  for (int b = 0; dims->spade && b < dims->n_lin_z; ++b) {
+    AVR_REQUIRE(w->scale_z_w[b] && w->scale_z_b[b] && w->lin_z_b[b],
+                "avr_field_pack: use_spade needs scale_z weight / bias and lin_z bias of every lin_z block");
+    if ((rc = pack_linear(w->scale_z_w[b], H, dims->d_latent, NT, L.KTl, packed + L.scale_z[b], s))) return rc;
+    if ((rc = pack_bias(w->lin_z_b[b], nullptr, H, H, packed + L.b_tab[b], s))) return rc;
+    if ((rc = pack_bias(w->scale_z_b[b], nullptr, H, H, packed + L.b_tab[dims->n_lin_z + b], s))) return rc;
+  }
   if ((rc = pack_bias(w->lin_out_b, nullptr, 4, 16, packed + L.b_out, s))) return rc;
   for (int b = 0; dims->bn && b < dims->n_blocks; ++b) {
     AVR_REQUIRE(w->bn_scale[b] && w->bn_shift[b], "avr_field_pack: bn needs bn_scale / bn_shift of every block");
@@ -609,7 +647,8 @@ extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_
   int rc = field_common(dims, views, packed, tables, &a);
   if (rc) return rc;
   AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_fwd_points_train: the training path is x3 only");
-  AVR_REQUIRE(!dims->bn, "avr_field_fwd_points_train: BatchNorm nets train on the module path");
+  AVR_REQUIRE(!dims->bn && !dims->spade && !(dims->beta > 0.f),
+              "avr_field_fwd_points_train: BatchNorm / use_spade / Softplus nets train on the module path");
   AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points_train: bad size");
   AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && out && act && mask), "avr_field_fwd_points_train: null pointer");
   AVR_REQUIRE(act_rows >= n_scenes * n_points, "avr_field_fwd_points_train: act_rows < n_scenes * n_points");
@@ -627,7 +666,7 @@ extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_
   a.act_max = act_max;
   a.n_scenes = n_scenes;
   a.blocks_per_scene = (n_points + kX3Samples - 1) / kX3Samples;
-  a.table_scene_stride = (int64_t)(dims->n_lin_z > 0 ? dims->n_lin_z : 1) * a.table_stride;
+  a.table_scene_stride = (int64_t)(a.L.n_tables > 0 ? a.L.n_tables : 1) * a.table_stride;
   if (a.M == 0) return AVR_OK;
   return dispatch_field_x3(dims->d_hidden, a, as_stream(stream));
 }
@@ -639,7 +678,8 @@ extern "C" int avr_field_bwd(const avr_field_dims* dims, const float* packed, co
   int rc = make_layout(dims, &a.L);
   if (rc) return rc;
   AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_bwd: the training path is x3 only");
-  AVR_REQUIRE(!dims->bn, "avr_field_bwd: BatchNorm nets train on the module path");
+  AVR_REQUIRE(!dims->bn && !dims->spade && !(dims->beta > 0.f),
+              "avr_field_bwd: BatchNorm / use_spade / Softplus nets train on the module path");
   AVR_REQUIRE(n_points >= 0 && n_scenes >= 1, "avr_field_bwd: bad size");
   if (n_points == 0) return AVR_OK;
   AVR_REQUIRE(packed && packed_bwd && out && grad_out && mask && grads, "avr_field_bwd: null pointer");
@@ -667,13 +707,13 @@ extern "C" int avr_field_latent_table(const avr_field_dims* dims, const float* p
   if (rc) return rc;
   AVR_REQUIRE(packed && latent && table, "avr_field_latent_table: null pointer");
   AVR_REQUIRE(H > 0 && W > 0, "avr_field_latent_table: bad latent size");
-  if (dims->n_lin_z == 0) return AVR_OK;
+  if (L.n_tables == 0) return AVR_OK;
   hipStream_t s = as_stream(stream);
   switch (dims->d_hidden) {
-    case 64: return launch_table<4>(packed, L, latent, H * W, dims->n_lin_z, table, s);
-    case 128: return launch_table<8>(packed, L, latent, H * W, dims->n_lin_z, table, s);
-    case 256: return launch_table<16>(packed, L, latent, H * W, dims->n_lin_z, table, s);
-    case 512: return launch_table<32>(packed, L, latent, H * W, dims->n_lin_z, table, s);
+    case 64: return launch_table<4>(packed, L, latent, H * W, L.n_tables, table, s);
+    case 128: return launch_table<8>(packed, L, latent, H * W, L.n_tables, table, s);
+    case 256: return launch_table<16>(packed, L, latent, H * W, L.n_tables, table, s);
+    case 512: return launch_table<32>(packed, L, latent, H * W, L.n_tables, table, s);
   }
   return fail(AVR_E_UNSUPPORTED, "field: d_hidden %d", dims->d_hidden);
 }
@@ -698,7 +738,7 @@ extern "C" int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_des
 }
 
 // Several scenes in one launch (x3 path): scene s's samples are rows s * per_scene .. of the inputs, its lin_z
-// tables at tables + s * max(n_lin_z, 1) * H*W * d_hidden (FusedField.tables_batch), its view views[s].
+// tables at tables + s * max(n_tables, 1) * H*W * d_hidden (FusedField.tables_batch), its view views[s].
 static int field_batch(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes, const float* packed,
                        const float* tables, FieldArgs* a, int64_t per_scene, const char* what) {
   AVR_REQUIRE(views && n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES, "%s: 1..%d scenes per call", what,
@@ -714,7 +754,7 @@ static int field_batch(const avr_field_dims* dims, const avr_view_desc* views, i
   a->M = per_scene;
   a->n_scenes = n_scenes;
   a->blocks_per_scene = (per_scene + kX3Samples - 1) / kX3Samples;
-  a->table_scene_stride = (int64_t)(dims->n_lin_z > 0 ? dims->n_lin_z : 1) * a->table_stride;
+  a->table_scene_stride = (int64_t)(a->L.n_tables > 0 ? a->L.n_tables : 1) * a->table_stride;
   return AVR_OK;
 }
 

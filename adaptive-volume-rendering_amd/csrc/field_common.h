@@ -30,6 +30,10 @@ struct Layout {
   int64_t x3_hdr, x3_in, x3_out, x3_fc0[AVR_MAX_BLOCKS], x3_fc1[AVR_MAX_BLOCKS];
   int64_t bn_a[AVR_MAX_BLOCKS], bn_c[AVR_MAX_BLOCKS];   // eval BatchNorm affine of block b (bn != 0)
   int bn;
+  // use_spade: scale_z[b] fp32 fragments (like lin_z); the per-texel tables carry their biases
+  // (b_tab[t]: table t = lin_z[t] for t < n_lin_z, scale_z[t - n_lin_z] after)
+  int spade, n_lin_z, n_tables;
+  int64_t scale_z[AVR_MAX_BLOCKS], b_tab[2 * AVR_MAX_BLOCKS];
   int64_t total;          // floats
 };
 
@@ -75,6 +79,7 @@ struct FieldArgs {
   View v;
   int n_blocks, n_lin_z, num_freqs;
   float freq_factor;
+  float beta;            // > 0: Softplus(beta) activation (x3 inference), 0: ReLU
   // sample source: rays (z != null) or explicit points
   const float* ro; const float* rd; const float* z; int n_samples;
   const float* xyz; const float* vd;

@@ -130,12 +130,12 @@ __device__ __forceinline__ void gemm(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], co
 }
 
 // h += S * sum_c w_c * row(slot_c) over the corners whose slot is in [lo, lo+n).
-// PREP: also v = relu(h * f) and the running max for the next publish (the
-// fc_0 input of the block), from the same register read of h.
-template <int FT, bool PREP, bool STOREV = true>
+// PREP: also v = act(h * f) and the running max of max(0, h * f) for the next
+// publish (the fc_0 input of the block), from the same register read of h.
+template <int FT, bool PREP, bool STOREV = true, int ACT = 0>
 __device__ __forceinline__ void blend_stage(floatx4 (&h)[FT][4], floatx4 (&v)[FT][4], float& mx, const char* stage_g,
                                             const ZTail* tail, int lo, int n, int RS, float S, float f, int wid, int g,
-                                            int j) {
+                                            int j, float beta = 0.f) {
   const lds_char* stage = (const lds_char*)stage_g;
   const unsigned fo = 64u * FT * wid + 16u * g;   // this lane's feature offset in a row
 #pragma unroll
@@ -160,8 +160,9 @@ __device__ __forceinline__ void blend_stage(floatx4 (&h)[FT][4], floatx4 (&v)[FT
       if (PREP) {
         floatx4 x = hn * f;
         if (STOREV) {
-          x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
-          v[ft][sg] = x;
+          const floatx4 y = act4<ACT>(x, beta);
+          v[ft][sg] = y;
+          if (ACT == 0) x = y;   // ReLU: the max from the stored values
         }
         // mx starts at 0: max relu(x_i) = max(0, max x_i)
         mx = fmaxf(mx, fmaxf(x.x, x.y));
@@ -236,7 +237,12 @@ __device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const 
 // other); wave w owns the FT 16-row feature tiles FT*w .. FT*w + FT-1.
 // SAVE (training forward): also write every GEMM input and its relu mask.
 // BN: eval-mode BatchNorm nets (x3_gemm.h max_relu_bn): the block input is relu(a * h + c).
-template <int FT, int NW, bool SAVE, bool BN = false>
+// SPADE: use_spade nets (models.py:585-587): before block b < n_lin_z, h = scale_z[b](z) * h + lin_z[b](z);
+// the scale table is staged and blended first (into t, free between blocks), h is scaled, then the lin_z
+// table follows as for every net (its bias is in the table, not folded into the previous layer).
+// ACT: the MLP's activation (x3_gemm.h act1: 0 ReLU, 1 Softplus(a.beta)); the split scale of a layer input
+// comes from act_bound of the max of max(0, pre-activation), its epilogue's usual reduction.
+template <int FT, int NW, bool SAVE, bool BN = false, bool SPADE = false, int ACT = 0>
 __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   constexpr int HID = 16 * FT * NW;
   using P = LdsPlan<HID>;
@@ -248,6 +254,9 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   constexpr int NPF = TWO ? FT : kPrefetch;   // chunk-0 weight tiles loaded ahead of each layer's publish
   static_assert(!(SAVE && TWO), "the training forward keeps the 4-wave layout");
   static_assert(!(SAVE && BN), "BatchNorm nets train on the module path");
+  static_assert(!(SAVE && SPADE) && !(BN && SPADE), "use_spade: inference without BatchNorm only");
+  static_assert(ACT == 0 || (!SAVE && !BN), "Softplus: inference without BatchNorm only");
+  const float beta = a.beta;
   const floatx4 bz[FT] = {};
   // 8 waves: waves 0-3 at priority 1 leave each GEMM first, so their epilogue VALU overlaps the last MFMAs of
   // waves 4-7 on the same SIMDs (measured against no priority, priority for waves 4-7, and a barrier every one
@@ -385,7 +394,9 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   // 8 waves: block 0's lin_z stage rows that do not overlap lin_in's X are DMA'd before the lin_in GEMM
   constexpr bool PRE0 = TWO;
   if (PRE0 && a.n_lin_z > 0 && D <= P::CAP && D > P::IN_ROWS0) {
-    stage_rows<HID, NW>(stage, a.table + scene * a.table_scene_stride, tail, P::IN_ROWS0, D - P::IN_ROWS0, P::RS, lane, wid, P::IN_ROWS0);
+    // the first table block 0 blends: lin_z[0], or scale_z[0] (table n_lin_z) with use_spade
+    stage_rows<HID, NW>(stage, a.table + (SPADE ? a.n_lin_z : 0) * a.table_stride + scene * a.table_scene_stride,
+                        tail, P::IN_ROWS0, D - P::IN_ROWS0, P::RS, lane, wid, P::IN_ROWS0);
     p0 = P::IN_ROWS0;
     p1 = D;
   }
@@ -396,6 +407,36 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     // + lin_z[b](interp latent) (models.py ResnetFC: x = x + lin_z[b](z) before block b)
     // (fused with the fc_0 input prep: v = relu(h), mx)
     if (b < a.n_lin_z) lds_barrier();  // every wave is done reading X (the stage aliases it)
+    if constexpr (SPADE) {
+      if (b < a.n_lin_z) {
+        // t = sum_c w_c * scale_z row_c (all passes), then h *= t (h's scale S_h is unchanged)
+        const float* stab = a.table + (a.n_lin_z + b) * a.table_stride + scene * a.table_scene_stride;
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+          for (int sg = 0; sg < 4; ++sg) t[ft][sg] = floatx4{0.f, 0.f, 0.f, 0.f};
+        float unused = 0.f;
+        for (int lo = 0; lo < D; lo += P::CAP) {
+          const int n = D - lo < P::CAP ? D - lo : P::CAP;
+          if (lo > 0) __syncthreads();
+          if (p0 > 0) stage_rows<HID, NW>(stage, stab, tail, 0, p0, P::RS, lane, wid, 0);
+          if (p0 > 0 || p1 > 0) {   // pass 0 of a single-pass set, partly staged before lin_in
+            if (p1 < n) stage_rows<HID, NW>(stage, stab, tail, p1, n - p1, P::RS, lane, wid, p1);
+          } else {
+            stage_rows<HID, NW>(stage, stab, tail, lo, n, P::RS, lane, wid);
+          }
+          p0 = p1 = 0;
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          blend_stage<FT, false>(t, v, unused, stage, tail, lo, n, P::RS, 1.0f, 1.0f, wid, g, j);
+        }
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+          for (int sg = 0; sg < 4; ++sg) h[ft][sg] *= t[ft][sg];
+        __syncthreads();   // every wave is done with the scale rows before the lin_z rows replace them
+      }
+    }
     const float* table = a.table + b * a.table_stride + scene * a.table_scene_stride;
     if (b < a.n_lin_z && D <= P::CAP) {
       if (p0 > 0) stage_rows<HID, NW>(stage, table, tail, 0, p0, P::RS, lane, wid, 0);
@@ -407,7 +448,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       AVR_STAMP(30);
       mx = 0.f;
 #ifndef AVR_DIAG_NO_BLEND   // timing-only diagnostic: the lin_z blend skipped (wrong results)
-      blend_stage<FT, true, !TWO>(h, v, mx, stage, tail, 0, D, P::RS, S_h, 1.0f / S_h, wid, g, j);
+      blend_stage<FT, true, !TWO, ACT>(h, v, mx, stage, tail, 0, D, P::RS, S_h, 1.0f / S_h, wid, g, j, beta);
 #else
       mx = max_relu_affine<FT, false>(h, 1.0f / S_h, bz);
 #endif
@@ -421,8 +462,10 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
         __syncthreads();
         blend_stage<FT, false>(h, v, mx, stage, tail, lo, n, P::RS, S_h, 1.0f / S_h, wid, g, j);
       }
-      mx = TWO ? max_relu_affine<FT, false>(h, 1.0f / S_h, bz) : prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
+      mx = TWO ? max_relu_affine<FT, false>(h, 1.0f / S_h, bz)
+               : prep_input<FT, false, ACT>(v, h, 1.0f / S_h, nullptr, wid, g, beta);
     }
+    mx = act_bound<ACT>(mx, beta);   // (BN nets are ReLU only: their max below replaces this)
     const float* bn_a = a.packed + L.bn_a[b];
     const float* bn_c = a.packed + L.bn_c[b];
     if constexpr (BN) {   // the block input is relu(bn_0(h)) (models.py:456-458), not relu(h)
@@ -436,20 +479,20 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     if constexpr (TWO) {
       // the fc_1 bias loads are issued before the t publish, whose barriers cover their latency
       if constexpr (BN) s_x = publish_bn<FT, NW>(X16, h, 1.0f / S_h, bn_a, bn_c, mx, red, wid, lane, g, j);
-      else s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
+      else s_x = publish_affine<FT, NW, false, ACT>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j, beta);
       AVR_STAMP(6 + 5 * (b & 3));
       const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
       gemm<FT, true, TWO>(t, A0, W0, KC, 64 * NTT, X16, lane);
       AVR_STAMP(7 + 5 * (b & 3));
       floatx4 bv[FT];
       load_bias<FT, true>(bv, a.packed + L.b_fc0[b], wid, g);
-      mx = max_relu_affine<FT, true>(t, 1.0f / S_t, bv);
+      mx = act_bound<ACT>(max_relu_affine<FT, true>(t, 1.0f / S_t, bv), beta);
       if (b == 1) AVR_STAMP(20);
       floatx4 bb[FT];
       load_bias<FT, true>(bb, a.packed + L.b_fc1[b], wid, g);
       prefetch_a<FT, NPF>(A0, W1, lane);
       if (b == 1) AVR_STAMP(21);
-      s_x = publish_affine<FT, NW, true>(X16, t, 1.0f / S_t, bv, mx, red, wid, lane, g, j);
+      s_x = publish_affine<FT, NW, true, ACT>(X16, t, 1.0f / S_t, bv, mx, red, wid, lane, g, j, beta);
       AVR_STAMP(8 + 5 * (b & 3));
       // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
       const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
@@ -469,7 +512,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       gemm<FT, true, TWO>(t, A0, W0, KC, 64 * NTT, X16, lane);
       AVR_STAMP(7 + 5 * (b & 3));
       // fc_1 input relu(t + b0)
-      mx = prep_input<FT, true>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g);
+      mx = act_bound<ACT>(prep_input<FT, true, ACT>(v, t, 1.0f / S_t, a.packed + L.b_fc0[b], wid, g, beta), beta);
       prefetch_a<FT, NPF>(A0, W1, lane);
       if (SAVE) save_layer<FT, NW>(a, 2 * b + 1, v, base, roff, wid, g, j, lane);
       s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j, SAVE ? &tail->lmax[2 * b + 1] : nullptr);
@@ -502,7 +545,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) Aw[cc] = load_frag(wo + 2 * 64 * (2 * wid + cc));
     const float f = 1.0f / S_h;
-    const float mxw = max_relu_affine<FT, false>(h, f, bz);
+    const float mxw = act_bound<ACT>(max_relu_affine<FT, false>(h, f, bz), beta);
     const float s_w = pow2_scale_for(mxw);
     floatx4 part[4];
 #pragma unroll
@@ -511,8 +554,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc) {
         uint2 h0, l0, h1, l1;
-        split4(relu_affine<false>(h[2 * cc][sg], f, bz[0]), s_w, h0, l0);
-        split4(relu_affine<false>(h[2 * cc + 1][sg], f, bz[0]), s_w, h1, l1);
+        split4(relu_affine<false, ACT>(h[2 * cc][sg], f, bz[0], beta), s_w, h0, l0);
+        split4(relu_affine<false, ACT>(h[2 * cc + 1][sg], f, bz[0], beta), s_w, h1, l1);
         const half8 bh = __builtin_bit_cast(half8, make_uint4(h0.x, h0.y, h1.x, h1.y));
         const half8 bl = __builtin_bit_cast(half8, make_uint4(l0.x, l0.y, l1.x, l1.y));
         part[sg] = mfma32h(Aw[cc].hi, bh, part[sg]);
@@ -556,10 +599,10 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     for (int c = 0; c < KC / 4; ++c) Ao[c] = load_frag(wo + (wlo + 2 * 64 * c));
   }
   if constexpr (TWO) {
-    mx = max_relu_affine<FT, false>(h, 1.0f / S_h, bz);
-    s_x = publish_affine<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j);
+    mx = act_bound<ACT>(max_relu_affine<FT, false>(h, 1.0f / S_h, bz), beta);
+    s_x = publish_affine<FT, NW, false, ACT>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j, beta);
   } else {
-    mx = prep_input<FT, false>(v, h, 1.0f / S_h, nullptr, wid, g);
+    mx = act_bound<ACT>(prep_input<FT, false, ACT>(v, h, 1.0f / S_h, nullptr, wid, g, beta), beta);
     if (SAVE) save_layer<FT, NW>(a, 2 * a.n_blocks, v, base, roff, wid, g, j, lane);
     s_x = publish<FT, NW>(X16, v, mx, red, wid, lane, g, j, SAVE ? &tail->lmax[2 * a.n_blocks] : nullptr);
   }
@@ -595,12 +638,12 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   }
 }
 
-template <int FT, int NW, bool SAVE, bool BN = false>
+template <int FT, int NW, bool SAVE, bool BN = false, bool SPADE = false, int ACT = 0>
 static int launch_x3(const FieldArgs& a, hipStream_t s) {
   const size_t shm = LdsPlan<16 * FT * NW>::BYTES;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT, NW, SAVE, BN>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_x3_kernel<FT, NW, SAVE, BN, SPADE, ACT>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
       return fail(AVR_E_HIP, "field_x3_kernel: cannot set dynamic LDS to %zu", shm);
     attr = true;
@@ -608,7 +651,7 @@ static int launch_x3(const FieldArgs& a, hipStream_t s) {
   const int64_t blocks = (SAVE || a.n_scenes > 1) ? a.blocks_per_scene * a.n_scenes
                                                   : (a.M + kX3Samples - 1) / kX3Samples;
   AVR_REQUIRE(blocks < (1ll << 31), "field: too many points");
-  field_x3_kernel<FT, NW, SAVE, BN><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
+  field_x3_kernel<FT, NW, SAVE, BN, SPADE, ACT><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("field_x3_kernel");
 }
 
@@ -629,6 +672,24 @@ int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s) {
       case 256: return launch_x3<4, 4, false, true>(a, s);
       case 512: return x3_waves() == 8 ? launch_x3<4, 8, false, true>(a, s) : launch_x3<8, 4, false, true>(a, s);
     }
+    return fail(AVR_E_UNSUPPORTED, "field x3: d_hidden %d", d_hidden);
+  }
+  if (a.L.spade || a.beta > 0.f) {   // use_spade and / or Softplus (inference only)
+    AVR_REQUIRE(!a.act, "field x3: use_spade / Softplus nets train on the module path");
+    const int v = (a.L.spade ? 1 : 0) | (a.beta > 0.f ? 2 : 0);
+#define AVR_X3_OPT(FT, NW)                                      \
+  switch (v) {                                                  \
+    case 1: return launch_x3<FT, NW, false, false, true, 0>(a, s);  \
+    case 2: return launch_x3<FT, NW, false, false, false, 1>(a, s); \
+    default: return launch_x3<FT, NW, false, false, true, 1>(a, s); \
+  }
+    switch (d_hidden) {
+      case 64: AVR_X3_OPT(1, 4)
+      case 128: AVR_X3_OPT(2, 4)
+      case 256: AVR_X3_OPT(4, 4)
+      case 512: AVR_X3_OPT(4, 8)
+    }
+#undef AVR_X3_OPT
     return fail(AVR_E_UNSUPPORTED, "field x3: d_hidden %d", d_hidden);
   }
   if (d_hidden == 512 && !a.act && x3_waves() == 8) return launch_x3<4, 8, false>(a, s);

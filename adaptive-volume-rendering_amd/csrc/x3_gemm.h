@@ -272,10 +272,40 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// v = relu(acc * f [+ bias]) (one read of the accumulators), returns the wave max
-template <int FT, bool BIAS>
+// The MLP's activation (models.py:442-445, 536-537): ACT 0 = ReLU, 1 = Softplus(beta) as torch computes it in
+// fp32 (x where beta * x > 20, else log1p(exp(beta * x)) / beta).
+template <int ACT>
+__device__ __forceinline__ float act1(float x, float beta) {
+  if constexpr (ACT == 0) {
+    return fmaxf(x, 0.f);
+  } else {
+    const float bx = x * beta;
+    return bx > 20.f ? x : log1pf(expf(bx)) / beta;
+  }
+}
+
+template <int ACT>
+__device__ __forceinline__ floatx4 act4(floatx4 x, float beta) {
+  if constexpr (ACT == 0) {
+    x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
+    return x;
+  } else {
+    return floatx4{act1<1>(x.x, beta), act1<1>(x.y, beta), act1<1>(x.z, beta), act1<1>(x.w, beta)};
+  }
+}
+
+// Upper bound of act over values whose max(0, max) is m (both activations increase monotonically): the
+// operand scale of a layer input from the max-of-relu its epilogue reduces.
+template <int ACT>
+__device__ __forceinline__ float act_bound(float m, float beta) {
+  return ACT == 0 ? m : act1<1>(m, beta);
+}
+
+// v = act(acc * f [+ bias]) (one read of the accumulators), returns the wave max of max(0, acc * f [+ bias])
+// (act_bound gives the bound of v)
+template <int FT, bool BIAS, int ACT = 0>
 __device__ __forceinline__ float prep_input(floatx4 (&v)[FT][4], const floatx4 (&acc)[FT][4], float f,
-                                            const float* __restrict__ bias, int wid, int g) {
+                                            const float* __restrict__ bias, int wid, int g, float beta = 0.f) {
   float mx = 0.f;
   floatx4 bv[FT];   // all bias loads first (one wait, not one per tile)
 #pragma unroll
@@ -287,10 +317,11 @@ __device__ __forceinline__ float prep_input(floatx4 (&v)[FT][4], const floatx4 (
     const floatx4 b = bv[ft];
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) {
-      floatx4 x = BIAS ? acc[ft][sg] * f + b : acc[ft][sg] * f;
-      x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
-      v[ft][sg] = x;
-      mx = fmaxf(fmaxf(mx, x.x), fmaxf(fmaxf(x.y, x.z), x.w));
+      const floatx4 x = BIAS ? acc[ft][sg] * f + b : acc[ft][sg] * f;
+      const floatx4 y = act4<ACT>(x, beta);
+      v[ft][sg] = y;
+      const floatx4 m = ACT == 0 ? y : x;   // mx starts at 0: max relu (ReLU: from the stored values)
+      mx = fmaxf(fmaxf(mx, m.x), fmaxf(fmaxf(m.y, m.z), m.w));
     }
   }
   return wave_max(mx);
@@ -324,11 +355,9 @@ __device__ __forceinline__ void load_bias(floatx4 (&bv)[FT], const float* __rest
     bv[ft] = BIAS ? *reinterpret_cast<const floatx4*>(bias + 16 * (FT * wid + ft) + 4 * g) : floatx4{0.f, 0.f, 0.f, 0.f};
 }
 
-template <bool BIAS>
-__device__ __forceinline__ floatx4 relu_affine(const floatx4& a, float f, const floatx4& b) {
-  floatx4 x = BIAS ? a * f + b : a * f;
-  x.x = fmaxf(x.x, 0.f); x.y = fmaxf(x.y, 0.f); x.z = fmaxf(x.z, 0.f); x.w = fmaxf(x.w, 0.f);
-  return x;
+template <bool BIAS, int ACT = 0>
+__device__ __forceinline__ floatx4 relu_affine(const floatx4& a, float f, const floatx4& b, float beta = 0.f) {
+  return act4<ACT>(BIAS ? a * f + b : a * f, beta);
 }
 
 // max relu(x_i) = max(0, max x_i): no per-value relu (mx starts at 0)
@@ -346,10 +375,11 @@ __device__ __forceinline__ float max_relu_affine(const floatx4 (&acc)[FT][4], fl
   return wave_max(mx);
 }
 
-// X <- split(relu(acc * f + b) * s_x) for this wave's feature tiles
-template <int FT, bool BIAS>
+// X <- split(act(acc * f + b) * s_x) for this wave's feature tiles
+template <int FT, bool BIAS, int ACT = 0>
 __device__ __forceinline__ void store_split_affine(uint4* X16, const floatx4 (&acc)[FT][4], float f,
-                                                   const floatx4 (&bv)[FT], float s_x, int wid, int g, int j) {
+                                                   const floatx4 (&bv)[FT], float s_x, int wid, int g, int j,
+                                                   float beta = 0.f) {
   char* base = reinterpret_cast<char*>(X16);
 #pragma unroll
   for (int ft = 0; ft < FT; ++ft) {
@@ -357,7 +387,7 @@ __device__ __forceinline__ void store_split_affine(uint4* X16, const floatx4 (&a
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) {
       uint2 hi, lo;
-      split4(relu_affine<BIAS>(acc[ft][sg], f, bv[ft]), s_x, hi, lo);
+      split4(relu_affine<BIAS, ACT>(acc[ft][sg], f, bv[ft], beta), s_x, hi, lo);
       const int s = 16 * sg + j;
       *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 0, g, s) * 16 + (ftg & 1) * 8) = hi;
       *reinterpret_cast<uint2*>(base + xidx(ftg >> 1, 1, g, s) * 16 + (ftg & 1) * 8) = lo;
@@ -473,15 +503,15 @@ __device__ __forceinline__ float publish_bn(uint4* X16, const floatx4 (&acc)[FT]
   return s_x;
 }
 
-// Two-pass publish of relu(acc * f + b) (mx from max_relu_affine); returns s_x
-template <int FT, int NW, bool BIAS>
+// Two-pass publish of act(acc * f + b) (mx: a bound of the values, act_bound of max_relu_affine); returns s_x
+template <int FT, int NW, bool BIAS, int ACT = 0>
 __device__ __forceinline__ float publish_affine(uint4* X16, const floatx4 (&acc)[FT][4], float f,
                                                 const floatx4 (&bv)[FT], float mx, float* red, int wid, int lane,
-                                                int g, int j) {
+                                                int g, int j, float beta = 0.f) {
   if (lane == 0) red[wid] = mx;
   lds_barrier();
   const float s_x = pow2_scale_for(red_max<NW>(red));
-  store_split_affine<FT, BIAS>(X16, acc, f, bv, s_x, wid, g, j);
+  store_split_affine<FT, BIAS, ACT>(X16, acc, f, bv, s_x, wid, g, j, beta);
   lds_barrier();
   return s_x;
 }

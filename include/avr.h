@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 7
+#define AVR_ABI_VERSION 8
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -156,7 +156,8 @@ int avr_march_finish(const void* state, int64_t n_rays, int white_back, float* r
  * SpatialEncoder.index :245-274 (bilinear, border, align_corners=True),
  * ResnetFC :541-592, ResnetBlockFC :454-470 — for the default.conf family:
  * use_encoder, use_xyz, normalize_z, PE on xyz only (include_input), raw
- * viewdirs, ReLU, NS = 1, and (x3 inference) eval-mode BatchNorm (dims->bn).
+ * viewdirs, ReLU, NS = 1, and (x3 inference) eval-mode BatchNorm (dims->bn)
+ * and use_spade (dims->spade).
  *
  * The lin_z projections are applied to the latent map once per texel
  * (avr_field_latent_table) and bilinearly interpolated per sample: the
@@ -177,6 +178,14 @@ typedef struct {
                       The caller folds the second one into fc_0 (fc0_w := diag(a) W0, fc0_b := a*b0 + c) and
                       passes the per-feature affine y = a*x + c of bn_0 as bn_scale / bn_shift; the kernel
                       applies it to the residual stream in front of fc_0's relu. x3 inference only.       */
+  int spade;       /* 1: ResnetFC(use_spade=True) (models.py:528-534, 585-587): before block b < n_lin_z the
+                      residual stream becomes scale_z[b](z) * x + lin_z[b](z). Both projections are per-texel
+                      tables with their biases included (avr_field_latent_table writes 2 * n_lin_z tables:
+                      lin_z then scale_z), so the lin_z biases are NOT folded into lin_in / fc_1 here.
+                      x3 inference only, not with bn.                                                      */
+  float beta;      /* > 0: ResnetFC(beta=beta) — every ReLU of the MLP is Softplus(beta) (models.py:442-445,
+                      536-537; torch: x where beta*x > 20, else log1p(exp(beta*x)) / beta). 0: ReLU.
+                      x3 inference only, not with bn.                                                      */
 } avr_field_dims;
 
 #define AVR_FIELD_FP32 0
@@ -192,6 +201,8 @@ typedef struct {
   /* dims->bn only: eval BatchNorm1d bn_0 of block b as a per-feature affine (d_hidden floats each):
      a = weight / sqrt(running_var + eps), c = bias - running_mean * a                                 */
   const float* bn_scale[AVR_MAX_BLOCKS]; const float* bn_shift[AVR_MAX_BLOCKS];
+  /* dims->spade only: ResnetFC.scale_z[b] (d_hidden, d_latent) and its bias, b < n_lin_z             */
+  const float* scale_z_w[AVR_MAX_BLOCKS]; const float* scale_z_b[AVR_MAX_BLOCKS];
 } avr_resnetfc_weights;
 
 /* Source-view buffers set by NewPixelNeRFNet.encode (models.py:705-734) and
@@ -210,7 +221,9 @@ int avr_field_packed_floats(const avr_field_dims* dims, int64_t* n_floats);
 /* Repack one ResnetFC into MFMA fragment order (device -> device). */
 int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed, void* stream);
 /* table (n_lin_z, H*W, d_hidden) = lin_z[b].weight @ latent[:, texel] (no bias;
- * the bias is folded into the packed biases). latent (d_latent, H, W).        */
+ * the bias is folded into the packed biases). latent (d_latent, H, W).
+ * dims->spade: (2 * n_lin_z, H*W, d_hidden) — lin_z[b] tables, then scale_z[b]
+ * tables, each with its bias added.                                            */
 int avr_field_latent_table(const avr_field_dims* dims, const float* packed, const float* latent, int H, int W,
                            float* table, void* stream);
 /* Field at xyz = ro[r] + rd[r] * z[r, s], viewdir = rd[r]; out (n_rays*n_samples, 4)

@@ -217,17 +217,37 @@ def batch_norm_eval(x, p, prefix, eps=1e-5):
     return (np.asarray(x, F32) * alpha + beta).astype(F32)
 
 
-def resnetfc_forward(zx, p, d_latent, n_blocks, combine_layer):
-    """ResnetFC.forward (models.py:541-592) with ResnetBlockFC (:454-470), ReLU,
-    use_spade=False, NS=1 (combine_interleaved is the identity). With bn
-    parameters in `p` (train.py --bn, eval mode) every block applies bn_0 in
-    front of BOTH relus, as the reference does (models.py:456-461: bn_1 unused)."""
+def softplus(v, beta):
+    """nn.Softplus(beta) (threshold 20) as ATen evaluates it in fp32:
+    x where x * beta > 20, else log1p(exp(x * beta)) / beta."""
+    v = np.asarray(v, F32)
+    bx = (v * F32(beta)).astype(F32)
+    with np.errstate(over="ignore"):
+        sp = (np.log1p(np.exp(bx)) / F32(beta)).astype(F32)
+    return np.where(bx > F32(20), v, sp).astype(F32)
+
+
+def resnetfc_forward(zx, p, d_latent, n_blocks, combine_layer, beta=0.0):
+    """ResnetFC.forward (models.py:541-592) with ResnetBlockFC (:454-470),
+    NS=1 (combine_interleaved is the identity). beta > 0: every ReLU is
+    Softplus(beta) (models.py:442-445, 536-537). With scale_z parameters in `p`
+    (use_spade, :528-534) block b < combine_layer starts from
+    scale_z[b](z) * x + lin_z[b](z) (:585-587). With bn parameters in `p`
+    (train.py --bn, eval mode) every block applies bn_0 in front of BOTH relus,
+    as the reference does (models.py:456-461: bn_1 unused)."""
     z = zx[:, :d_latent]
     x = _linear(zx[:, d_latent:], p["lin_in.weight"], p["lin_in.bias"])
-    relu = lambda v: np.maximum(v, F32(0))  # noqa: E731
+    if beta > 0:
+        relu = lambda v: softplus(v, beta)  # noqa: E731
+    else:
+        relu = lambda v: np.maximum(v, F32(0))  # noqa: E731
     for b in range(n_blocks):
         if d_latent > 0 and b < combine_layer:
-            x = x + _linear(z, p[f"lin_z.{b}.weight"], p[f"lin_z.{b}.bias"])
+            tz = _linear(z, p[f"lin_z.{b}.weight"], p[f"lin_z.{b}.bias"])
+            if f"scale_z.{b}.weight" in p:
+                x = (_linear(z, p[f"scale_z.{b}.weight"], p[f"scale_z.{b}.bias"]) * x).astype(F32) + tz
+            else:
+                x = x + tz
         bn = f"blocks.{b}.bn_0"
         if bn + ".running_mean" in p:
             net = _linear(relu(batch_norm_eval(x, p, bn)), p[f"blocks.{b}.fc_0.weight"], p[f"blocks.{b}.fc_0.bias"])
@@ -245,7 +265,7 @@ class PixelNeRFField:
     use_viewdirs without PE, no global encoder, NS = 1."""
 
     def __init__(self, params_coarse, params_fine, latent, poses, focal, c, image_shape, latent_scaling,
-                 n_blocks=3, combine_layer=1000, num_freqs=6, freq_factor=1.5):
+                 n_blocks=3, combine_layer=1000, num_freqs=6, freq_factor=1.5, beta=0.0):
         self.pc, self.pf = params_coarse, params_fine
         self.latent = np.asarray(latent, F32).reshape(np.asarray(latent).shape[-3:])
         L_, H_, W_ = self.latent.shape
@@ -257,6 +277,7 @@ class PixelNeRFField:
         self.latent_scaling = np.asarray(latent_scaling, F32)
         self.n_blocks, self.combine_layer = n_blocks, combine_layer
         self.num_freqs, self.freq_factor = num_freqs, freq_factor
+        self.beta = beta
         self.d_latent = self.latent.shape[0]
 
     def features(self, xyz, viewdirs):
@@ -277,7 +298,8 @@ class PixelNeRFField:
         shp = np.asarray(xyz).shape
         lat, zf = self.features(xyz, viewdirs)
         p = self.pc if coarse else self.pf
-        out = resnetfc_forward(np.concatenate([lat, zf], -1), p, self.d_latent, self.n_blocks, self.combine_layer)
+        out = resnetfc_forward(np.concatenate([lat, zf], -1), p, self.d_latent, self.n_blocks, self.combine_layer,
+                               self.beta)
         res = np.concatenate([1.0 / (1.0 + np.exp(-out[:, :3].astype(np.float64))), np.maximum(out[:, 3:4], 0)], -1)
         return res.astype(F32).reshape(shp[:-1] + (4,))
 

@@ -59,11 +59,12 @@ def pow2_scale(fan_in):
     return float(2.0 ** np.round(np.log2(target)))
 
 
-def resnetfc_params(d_in, d_latent, d_hidden, n_blocks, combine_layer, seed, d_out=4):
+def resnetfc_params(d_in, d_latent, d_hidden, n_blocks, combine_layer, seed, d_out=4, spade=False):
     """Hash-generated parameters for a reference ResnetFC (models.py:473-606),
     keyed by the reference's state_dict names. fc_1 weights are NON-zero on
     purpose (the reference zero-inits them at models.py:440, which would make
-    every block an identity and hide bugs)."""
+    every block an identity and hide bugs). spade: also scale_z[b]
+    (models.py:528-534), with biases around 1 so scale_z(z) * x keeps x's size."""
     p = {}
     s = seed * 1000
     p["lin_in.weight"] = hashed_centered((d_hidden, d_in), s + 1, pow2_scale(d_in))
@@ -79,6 +80,10 @@ def resnetfc_params(d_in, d_latent, d_hidden, n_blocks, combine_layer, seed, d_o
         for b in range(min(combine_layer, n_blocks)):
             p[f"lin_z.{b}.weight"] = hashed_centered((d_hidden, d_latent), s + 100 + 2 * b, pow2_scale(d_latent))
             p[f"lin_z.{b}.bias"] = hashed_centered((d_hidden,), s + 101 + 2 * b, 0.0625)
+            if spade:
+                p[f"scale_z.{b}.weight"] = hashed_centered((d_hidden, d_latent), s + 200 + 2 * b,
+                                                           0.5 * pow2_scale(d_latent))
+                p[f"scale_z.{b}.bias"] = (1.0 + hashed_centered((d_hidden,), s + 201 + 2 * b, 0.25)).astype(np.float32)
     return p
 
 
@@ -136,8 +141,9 @@ def field_from_meta(g):
         pf = {k[len("fine."):]: g[k] for k in g if k.startswith("fine.")}
         latent = g["latent"]
     else:
-        pc = resnetfc_params(d_in, L, d_hidden, n_blocks, combine, int(g["weight_seed_coarse"]))
-        pf = resnetfc_params(d_in, L, d_hidden, n_blocks, combine, int(g["weight_seed_fine"]))
+        spade = bool(int(g["spade"])) if "spade" in g else False
+        pc = resnetfc_params(d_in, L, d_hidden, n_blocks, combine, int(g["weight_seed_coarse"]), spade=spade)
+        pf = resnetfc_params(d_in, L, d_hidden, n_blocks, combine, int(g["weight_seed_fine"]), spade=spade)
         latent = hashed_normalish((1, L) + hw, int(g["latent_seed"]), 1.0)
     # eval-mode BatchNorm statistics / affine of bn=True nets (stored explicitly in the fixture)
     for tag, p in (("coarse", pc), ("fine", pf)):

@@ -91,8 +91,12 @@ class Conf(dict):
         return Conf(v) if isinstance(v, dict) and not isinstance(v, Conf) else v
 
 
-def model_conf(d_hidden, n_blocks, combine_layer, num_layers):
+def model_conf(d_hidden, n_blocks, combine_layer, num_layers, spade=False, beta=0.0):
     mlp = {"type": "resnet", "n_blocks": n_blocks, "d_hidden": d_hidden, "combine_layer": combine_layer}
+    if spade:
+        mlp["use_spade"] = True
+    if beta > 0:
+        mlp["beta"] = beta
     return Conf({
         "use_encoder": True, "use_global_encoder": False, "use_xyz": True, "canon_xyz": False,
         "use_code": True, "code": {"num_freqs": 6, "freq_factor": 1.5, "include_input": True},
@@ -142,13 +146,14 @@ def import_reference():
     return ref_utils, ref_renderers, ref_models
 
 
-def build_field(ref_models, d_hidden, n_blocks, combine_layer, num_layers, latent_hw, seed, store_weights, bn=False):
-    net = ref_models.NewPixelNeRFNet(model_conf(d_hidden, n_blocks, combine_layer, num_layers), bn=bn)
+def build_field(ref_models, d_hidden, n_blocks, combine_layer, num_layers, latent_hw, seed, store_weights, bn=False,
+                spade=False, beta=0.0):
+    net = ref_models.NewPixelNeRFNet(model_conf(d_hidden, n_blocks, combine_layer, num_layers, spade, beta), bn=bn)
     L = net.latent_size
     d_in = net.d_in
     params = {}
     for tag, mlp, s in (("coarse", net.mlp_coarse, seed), ("fine", net.mlp_fine, seed + 17)):
-        p = synth.resnetfc_params(d_in, L, d_hidden, n_blocks, combine_layer, s)
+        p = synth.resnetfc_params(d_in, L, d_hidden, n_blocks, combine_layer, s, spade=spade)
         bnp = synth.bn_params(d_hidden, n_blocks, s) if bn else {}
         sd = mlp.state_dict()
         for k, v in list(p.items()) + list(bnp.items()):
@@ -176,6 +181,9 @@ def build_field(ref_models, d_hidden, n_blocks, combine_layer, num_layers, laten
                 latent_scaling=latent_scaling)
     if store_weights:
         meta["latent"] = latent
+    if spade or beta > 0:   # (absent from the older fixtures: ReLU, no spade)
+        meta["spade"] = int(spade)
+        meta["beta"] = np.float32(beta)
     return net.eval(), meta, params
 
 
@@ -321,9 +329,16 @@ def g4_field():
         "bn_small": (64, 3, 1000, 1, (8, 8), True),
         "bn512": (512, 3, 1000, 4, (64, 64), False),
         "bn_mv512": (512, 5, 3, 4, (64, 64), False),
+        # ResnetFC options no shipped conf sets (models.py:442-445 Softplus(beta), :528-534 use_spade)
+        "spade_small": (64, 3, 1000, 1, (8, 8), True),
+        "spade512": (512, 3, 1000, 4, (64, 64), False),
+        "sp_small": (64, 3, 1000, 1, (8, 8), True),
+        "sp512": (512, 3, 1000, 4, (64, 64), False),
+        "spade_sp_mv": (64, 5, 3, 1, (8, 8), True),
     }.items():
+        beta = {"sp_small": 3.0, "sp512": 100.0, "spade_sp_mv": 1.0}.get(tag, 0.0)
         net, meta, params = build_field(REF_M, d_hidden, n_blocks, combine, num_layers, lhw, 40, store,
-                                        bn=tag.startswith("bn"))
+                                        bn=tag.startswith("bn"), spade=tag.startswith("spade"), beta=beta)
         xyz = synth.hashed_uniform((1, B, 3), 41, -0.5, 0.5)
         vd = synth.hashed_uniform((1, B, 3), 42, -1.0, 1.0)
         vd /= np.linalg.norm(vd, axis=-1, keepdims=True).astype(np.float32)

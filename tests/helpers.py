@@ -7,10 +7,11 @@ from oracle import avr_oracle as O
 from oracle import synth
 
 
-def model_conf(d_hidden, n_blocks, combine_layer, d_latent):
+def model_conf(d_hidden, n_blocks, combine_layer, d_latent, spade=False, beta=0.0):
     from avr.conf import Conf
     num_layers = {64: 1, 128: 2, 256: 3, 512: 4, 1024: 5}[d_latent]
-    mlp = {"type": "resnet", "n_blocks": n_blocks, "d_hidden": d_hidden, "combine_layer": combine_layer}
+    mlp = {"type": "resnet", "n_blocks": n_blocks, "d_hidden": d_hidden, "combine_layer": combine_layer,
+           "use_spade": bool(spade), "beta": float(beta)}
     return Conf({"use_encoder": True, "use_global_encoder": False, "use_xyz": True, "use_code": True,
                  "code": {"num_freqs": 6, "freq_factor": 1.5, "include_input": True}, "use_viewdirs": True,
                  "use_code_viewdirs": False, "mlp_coarse": dict(mlp), "mlp_fine": dict(mlp),
@@ -22,7 +23,8 @@ def build_net(g, device, precision="x3"):
     from avr.models import NewPixelNeRFNet
     pc, pf, latent = synth.field_from_meta(g)
     net = NewPixelNeRFNet(model_conf(int(g["d_hidden"]), int(g["n_blocks"]), int(g["combine_layer"]),
-                                     int(g["d_latent"])), bn=bool(int(g["bn"])) if "bn" in g else False)
+                                     int(g["d_latent"]), _spade(g), _beta(g)),
+                          bn=bool(int(g["bn"])) if "bn" in g else False)
     for mlp, p in ((net.mlp_coarse, pc), (net.mlp_fine, pf)):
         sd = mlp.state_dict()
         for k, v in p.items():
@@ -42,10 +44,18 @@ def build_net(g, device, precision="x3"):
     return net
 
 
+def _spade(g):
+    return bool(int(g["spade"])) if "spade" in g else False
+
+
+def _beta(g):
+    return float(g["beta"]) if "beta" in g else 0.0
+
+
 def oracle_field(g):
     pc, pf, latent = synth.field_from_meta(g)
     return O.PixelNeRFField(pc, pf, latent, g["poses"], g["focal"], g["c"], g["image_shape"], g["latent_scaling"],
-                            n_blocks=int(g["n_blocks"]), combine_layer=int(g["combine_layer"]))
+                            n_blocks=int(g["n_blocks"]), combine_layer=int(g["combine_layer"]), beta=_beta(g))
 
 
 def oracle_field_from_net(net):

@@ -283,6 +283,65 @@ def test_field_points_golden_batchnorm(golden, tag, waves, monkeypatch):
     _field_points_golden(golden, tag, "x3")
 
 
+@pytest.mark.parametrize("tag", ["spade_small", "spade512", "sp_small", "sp512", "spade_sp_mv"])
+def test_field_points_golden_spade_softplus(golden, tag):
+    """ResnetFC options on the fused x3 kernel against the reference's own forward (g4):
+    use_spade (scale_z[b](z) * x + lin_z[b](z), models.py:528-534, 585-587) and Softplus(beta)
+    in place of every ReLU (models.py:442-445, 536-537), alone and together."""
+    g = golden(f"g4_field_{tag}.npz")
+    net = build_net(g, DEV, "x3")
+    with torch.no_grad():
+        assert net.can_fuse(T(g["xyz"]))
+    _field_points_golden(golden, tag, "x3")
+
+
+@pytest.mark.parametrize("tag", ["spade_small", "spade512", "sp512", "spade_sp_mv"])
+def test_field_spade_softplus_many_texels_and_rays(golden, tag):
+    """Random points (a workgroup's 256 bilinear corners touch more distinct texels than one
+    LDS stage holds: the multi-pass staging of both spade tables) and the rays mode, against the
+    module's PyTorch graph of the same net; two scenes in one launch equal two launches."""
+    g = golden(f"g4_field_{tag}.npz")
+    net = build_net(g, DEV, "x3")
+    gen = torch.Generator(device="cpu").manual_seed(7)
+    xyz = (torch.rand(1, 6000, 3, generator=gen) - 0.5).to(DEV)
+    vd = torch.nn.functional.normalize(torch.randn(1, 6000, 3, generator=gen), dim=-1).to(DEV)
+    with torch.no_grad():
+        a = net(xyz, coarse=False, viewdirs=vd)
+        b = net.forward_torch(xyz, coarse=False, viewdirs=vd)
+    np.testing.assert_allclose(to_np(a), to_np(b), atol=5e-5, rtol=1e-4)
+    R, N = 200, 19
+    ro = torch.tensor([[0.3, -1.1, 0.5]], device=DEV).expand(R, 3).contiguous()
+    rd = torch.nn.functional.normalize(-ro + 0.2 * torch.randn(R, 3, device=DEV, generator=None), dim=-1)
+    z = torch.sort(0.8 + torch.rand(R, N, device=DEV), -1)[0]
+    with torch.no_grad():
+        fr = net.fused().forward_rays(ro, rd, z, coarse=True)
+        pts = ro[:, None, :] + rd[:, None, :] * z[..., None]
+        fp = net(pts.reshape(1, -1, 3), coarse=True, viewdirs=rd[:, None, :].expand(R, N, 3).reshape(1, -1, 3))
+    np.testing.assert_array_equal(to_np(fr), to_np(fp[0]))
+    # two scenes (same latent) in one batched launch = one launch per scene
+    with torch.no_grad():
+        two = net.fused().forward_points(xyz[:, :3000].expand(2, 3000, 3).contiguous(),
+                                         vd[:, :3000].expand(2, 3000, 3).contiguous(), False)
+    np.testing.assert_array_equal(to_np(two[0]), to_np(two[1]))
+    np.testing.assert_array_equal(to_np(two[0]), to_np(a[0, :3000]))
+
+
+def test_field_spade_softplus_routes(golden):
+    """use_spade / Softplus nets: fused on the x3 path for inference; precision fp32 and
+    autograd run the module's PyTorch graph (which matches the reference's forward too)."""
+    g = golden("g4_field_spade_sp_mv.npz")
+    net = build_net(g, DEV, "fp32")
+    xyz, vd = T(g["xyz"]), T(g["viewdirs"])
+    with torch.no_grad():
+        assert not net.can_fuse(xyz)
+        np.testing.assert_allclose(to_np(net(xyz, coarse=True, viewdirs=vd)), g["out_coarse"], atol=5e-5, rtol=1e-4)
+        net.field_precision = "x3"
+        assert net.can_fuse(xyz)
+    for p in net.parameters():
+        p.requires_grad_(True)
+    assert not net.can_train_fused(xyz, vd)
+
+
 def test_field_batchnorm_routes(golden):
     """BatchNorm nets: fused only on the x3 path in eval mode. precision fp32,
     train-mode BN (batch statistics) and autograd run the module's PyTorch

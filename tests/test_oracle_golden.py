@@ -62,12 +62,18 @@ def test_geometry(golden):
     np.testing.assert_allclose(O.opencv_pixel_coordinates(8, 8), g["opencv_pix_8"], atol=0)
 
 
-@pytest.mark.parametrize("tag", ["small", "small_mv", "full", "mv512", "d256", "bn_small", "bn512", "bn_mv512"])
+@pytest.mark.parametrize("tag", ["small", "small_mv", "full", "mv512", "d256", "bn_small", "bn512", "bn_mv512",
+                                 "spade_small", "spade512", "sp_small", "sp512", "spade_sp_mv"])
 def test_field(golden, tag):
+    """The oracle field against the reference's own NewPixelNeRFNet forward (g4), including the
+    ResnetFC options: eval BatchNorm, use_spade (scale_z), Softplus(beta)."""
     g = golden(f"g4_field_{tag}.npz")
     pc, pf, latent = synth.field_from_meta(g)
     f = O.PixelNeRFField(pc, pf, latent, g["poses"], g["focal"], g["c"], g["image_shape"], g["latent_scaling"],
-                         n_blocks=int(g["n_blocks"]), combine_layer=int(g["combine_layer"]))
+                         n_blocks=int(g["n_blocks"]), combine_layer=int(g["combine_layer"]),
+                         beta=float(g["beta"]) if "beta" in g else 0.0)
+    if tag.startswith("spade"):
+        assert any(k.startswith("scale_z.") for k in pc)
     lat, _ = f.features(g["xyz"], g["viewdirs"])
     np.testing.assert_allclose(lat[:64], g["latent_at_points"], atol=2e-6)
     np.testing.assert_allclose(f(g["xyz"], g["viewdirs"], coarse=True), g["out_coarse"], atol=2e-5)
