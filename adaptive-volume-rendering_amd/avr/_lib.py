@@ -93,6 +93,8 @@ _SIGS = {
                                  c_void_p, c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p],
     "avr_field_fwd_points_batch": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p, i64, c_void_p, c_void_p],
+    "avr_field_fwd_points_split": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_field_train_sizes": [ctypes.POINTER(FieldDims), c_int, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)],
     "avr_field_bwd_packed_floats": [ctypes.POINTER(FieldDims), ctypes.POINTER(i64)],
     "avr_field_pack_bwd": [ctypes.POINTER(FieldDims), ctypes.POINTER(ResnetFCWeights), c_void_p, c_void_p],

@@ -66,17 +66,27 @@ def _resnetfc_ok(mlp, d_in, d_latent, precision="x3"):
     return all(not blk.bn or _bn_ok(blk) for blk in mlp.blocks)
 
 
-def fused_eligible(net):
+def fused_eligible(net, multiview=False):
     """True when `net` is a NewPixelNeRFNet configured like conf/default*.conf:
     local encoder, xyz + PE(xyz) + raw viewdirs, normalize_z, bilinear/border
-    latent lookup, ResNet MLPs (eval-mode BatchNorm allowed on the x3 path),
-    one source view."""
+    latent lookup, ResNet MLPs (eval-mode BatchNorm, use_spade and Softplus
+    allowed on the x3 path), one source view. multiview: instead NS > 1 source
+    views, x3, every MLP combining them (combine_layer < n_blocks, mean or max):
+    FusedField.forward_points_multiview."""
     try:
+        ns = net.num_views_per_obj
+        if multiview:
+            mlps = [net.mlp_coarse] + ([net.mlp_fine] if net.mlp_fine is not None else [])
+            if not (ns > 1 and getattr(net, "field_precision", "x3") == "x3"
+                    and all(m.combine_layer < m.n_blocks and m.combine_type in ("average", "max") for m in mlps)):
+                return False
+        elif ns != 1:
+            return False
         code = getattr(net, "code", None)
         enc = net.encoder
         ok = (net.use_encoder and net.use_xyz and net.normalize_z and net.use_code and net.use_viewdirs
               and not net.use_code_viewdirs and not getattr(net, "use_global_encoder", False)
-              and net.num_views_per_obj == 1 and code is not None and code.include_input and code.d_in == 3
+              and code is not None and code.include_input and code.d_in == 3
               and getattr(enc, "index_interp", "bilinear") == "bilinear"
               and getattr(enc, "index_padding", "border") == "border"
               and enc.latent.dim() == 4 and enc.latent.shape[1] % 16 == 0 and enc.latent.shape[1] <= 1024
@@ -239,22 +249,24 @@ class FusedField:
         entry.batch_tables = (key, out, lat)
         return out
 
-    def view(self, sb=0):
+    def view(self, sb=0, ns=1):
+        """Source view sb (pose sb; with ns > 1 views per object, focal / principal point of
+        object sb // ns, as models.py:796-801 repeat_interleaves them)."""
         net = self.net
         srcs = [net.poses, net.focal, net.c, net.image_shape, net.encoder.latent_scaling]
-        key = (sb, _version_key(srcs), tuple(net.encoder.latent.shape))
-        hit = self._view_cache.get(sb)
+        key = (sb, ns, _version_key(srcs), tuple(net.encoder.latent.shape))
+        hit = self._view_cache.get((sb, ns))
         if hit is not None and hit[0] == key:
             return hit[1]
-        pick = lambda t: t[min(sb, t.shape[0] - 1)] if t.dim() > 1 else t  # noqa: E731
+        pick = lambda t, i=sb: t[min(i, t.shape[0] - 1)] if t.dim() > 1 else t  # noqa: E731
         v = ViewDesc()
         v.poses[:] = [float(x) for x in pick(net.poses).reshape(-1)[:12].tolist()]
-        v.focal[:] = [float(x) for x in pick(net.focal).reshape(-1)[:2].tolist()]
-        v.c[:] = [float(x) for x in pick(net.c).reshape(-1)[:2].tolist()]
+        v.focal[:] = [float(x) for x in pick(net.focal, sb // ns).reshape(-1)[:2].tolist()]
+        v.c[:] = [float(x) for x in pick(net.c, sb // ns).reshape(-1)[:2].tolist()]
         v.image_shape[:] = [float(x) for x in net.image_shape.reshape(-1)[:2].tolist()]
         v.latent_scaling[:] = [float(x) for x in net.encoder.latent_scaling.reshape(-1)[:2].tolist()]
         v.latent_h, v.latent_w = int(net.encoder.latent.shape[-2]), int(net.encoder.latent.shape[-1])
-        self._view_cache[sb] = (key, v, srcs)  # holding the sources keeps (ptr, version) keys sound
+        self._view_cache[(sb, ns)] = (key, v, srcs)  # holding the sources keeps (ptr, version) keys sound
         return v
 
     # ----------------------------------------------------------- evaluation
@@ -297,8 +309,46 @@ class FusedField:
                  ptr(ro[g0]), ptr(rd[g0]), ptr(z[g0 * R]), R, N, ptr(out[g0 * R * N]), stream_of(z))
         return out
 
+    def forward_points_multiview(self, xyz, viewdirs, coarse):
+        """NS = net.num_views_per_obj > 1 source views per object (models.py:749-853): the MLP's
+        first combine_layer blocks run on every (object, view) pair (avr_field_fwd_points_split,
+        first launch), the residual streams are combined over the views exactly as ResnetFC does
+        (combine_interleaved, models.py:566-579 / utils.py:71-81: mean or max over NS), and the
+        remaining blocks + lin_out run once per object (second launch). (SB, B, 3) -> (SB, B, 4)."""
+        from .models import combine_interleaved
+        net = self.net
+        NS = net.num_views_per_obj
+        SB, B, _ = xyz.shape
+        mlp = self._mlp(coarse)
+        entry = self.packed(coarse)
+        dims = entry.dims
+        H, nb, cl = dims.d_hidden, dims.n_blocks, mlp.combine_layer
+        dev = xyz.device
+        p = xyz.to(F32).repeat_interleave(NS, 0).contiguous()              # (SB*NS, B, 3), views of an object adjacent
+        v = viewdirs.reshape(SB, B, 3).to(F32).repeat_interleave(NS, 0).contiguous()
+        require_device(p, v)
+        K = SB * NS
+        tables = self.tables_batch(coarse, K)
+        h = torch.empty(K * B, H, device=dev, dtype=F32)
+        out = torch.empty(SB, B, 4, device=dev, dtype=F32)
+        entry.dims.precision = _lib.FIELD_X3
+        for g0 in range(0, K, _lib.AVR_MAX_SCENES):
+            n = min(_lib.AVR_MAX_SCENES, K - g0)
+            views = (ViewDesc * n)(*[self.view(k, NS) for k in range(g0, g0 + n)])
+            call("avr_field_fwd_points_split", ctypes.byref(entry.dims), views, n, ptr(entry.packed), ptr(tables[g0]),
+                 ptr(p[g0]), ptr(v[g0]), B, 0, cl, None, ptr(h[g0 * B]), None, stream_of(p))
+        hc = combine_interleaved(h, (NS, B), mlp.combine_type).reshape(SB * B, H).contiguous()
+        for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
+            n = min(_lib.AVR_MAX_SCENES, SB - g0)
+            views = (ViewDesc * n)(*[self.view(s * NS, NS) for s in range(g0, g0 + n)])
+            call("avr_field_fwd_points_split", ctypes.byref(entry.dims), views, n, ptr(entry.packed), ptr(tables[0]),
+                 None, None, B, cl, nb, ptr(hc[g0 * B]), None, ptr(out[g0]), stream_of(p))
+        return out
+
     def forward_points(self, xyz, viewdirs, coarse):
         """The rf(xyz (SB,B,3), viewdirs, coarse) protocol -> (SB, B, 4)."""
+        if getattr(self.net, "num_views_per_obj", 1) > 1:
+            return self.forward_points_multiview(xyz, viewdirs, coarse)
         SB, B, _ = xyz.shape
         out = torch.empty(SB, B, 4, device=xyz.device, dtype=F32)
         entry = self.packed(coarse)

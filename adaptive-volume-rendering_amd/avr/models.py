@@ -277,9 +277,19 @@ class NewPixelNeRFNet(nn.Module):
                 and viewdirs is not None and not viewdirs.requires_grad and fused_eligible(self)
                 and not any(inference_only(m) for m in (self.mlp_coarse, self.mlp_fine) if m is not None))
 
+    def can_fuse_multiview(self, xyz):
+        """NS > 1 source views, inference: the fused x3 field in two launches around the
+        views' combine (FusedField.forward_points_multiview)."""
+        from .field import fused_eligible
+        return (self.use_fused and xyz.is_cuda and self.num_views_per_obj > 1
+                and not (torch.is_grad_enabled() and (self._needs_grad() or xyz.requires_grad))
+                and fused_eligible(self, multiview=True))
+
     def forward(self, xyz, coarse=True, viewdirs=None, far=False, return_features=False):
         if not return_features and self.can_fuse(xyz):
             return self.fused().forward_points(xyz, viewdirs, coarse)
+        if not return_features and self.can_fuse_multiview(xyz):
+            return self.fused().forward_points_multiview(xyz, viewdirs, coarse)
         if not return_features and self.can_train_fused(xyz, viewdirs):
             return self.fused().forward_train(xyz, viewdirs, coarse)
         return self.forward_torch(xyz, coarse, viewdirs, far, return_features)

@@ -506,6 +506,10 @@ static int field_common(const avr_field_dims* dims, const avr_view_desc* view, c
   a->num_freqs = dims->num_freqs;
   a->freq_factor = dims->freq_factor;
   a->beta = dims->beta;
+  a->b_begin = 0;
+  a->b_end = dims->n_blocks;
+  a->h_out = nullptr;
+  a->h_in = nullptr;
   return AVR_OK;
 }
 
@@ -781,6 +785,34 @@ extern "C" int avr_field_fwd_points_batch(const avr_field_dims* dims, const avr_
   if (rc) return rc;
   AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && out), "avr_field_fwd_points_batch: null pointer");
   a.xyz = xyz; a.vd = viewdirs; a.n_samples = 1;
+  a.out = reinterpret_cast<float4*>(out);
+  if (a.M == 0) return AVR_OK;
+  return dispatch_field_x3(dims->d_hidden, a, as_stream(stream));
+}
+
+extern "C" int avr_field_fwd_points_split(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
+                                          const float* packed, const float* tables, const float* xyz,
+                                          const float* viewdirs, int64_t n_points, int b_begin, int b_end,
+                                          const float* h_in, float* h_out, float* out, void* stream) {
+  FieldArgs a{};
+  AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points_split: bad size");
+  int rc = field_batch(dims, views, n_scenes, packed, tables, &a, n_points, "avr_field_fwd_points_split");
+  if (rc) return rc;
+  const bool first = b_begin == 0;
+  if (first) {
+    AVR_REQUIRE(b_end > 0 && b_end < dims->n_blocks && b_end >= dims->n_lin_z,
+                "avr_field_fwd_points_split: first launch needs n_lin_z <= b_end < n_blocks (got %d)", b_end);
+    AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && h_out), "avr_field_fwd_points_split: null pointer");
+  } else {
+    AVR_REQUIRE(b_begin >= dims->n_lin_z && b_begin < dims->n_blocks && b_end == dims->n_blocks,
+                "avr_field_fwd_points_split: second launch needs n_lin_z <= b_begin < b_end == n_blocks");
+    AVR_REQUIRE(n_points == 0 || (h_in && out), "avr_field_fwd_points_split: null pointer");
+  }
+  a.xyz = xyz; a.vd = viewdirs; a.n_samples = 1;
+  a.b_begin = b_begin;
+  a.b_end = b_end;
+  a.h_in = first ? nullptr : h_in;
+  a.h_out = first ? h_out : nullptr;
   a.out = reinterpret_cast<float4*>(out);
   if (a.M == 0) return AVR_OK;
   return dispatch_field_x3(dims->d_hidden, a, as_stream(stream));

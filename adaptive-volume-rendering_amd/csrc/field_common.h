@@ -80,6 +80,11 @@ struct FieldArgs {
   int n_blocks, n_lin_z, num_freqs;
   float freq_factor;
   float beta;            // > 0: Softplus(beta) activation (x3 inference), 0: ReLU
+  // split passes (NS > 1 source views, x3 inference): blocks [b_begin, b_end); h_out: store the residual stream
+  // after block b_end - 1 instead of running lin_out; h_in: start from those rows instead of lin_in
+  int b_begin, b_end;
+  float* h_out;
+  const float* h_in;
   // sample source: rays (z != null) or explicit points
   const float* ro; const float* rd; const float* z; int n_samples;
   const float* xyz; const float* vd;

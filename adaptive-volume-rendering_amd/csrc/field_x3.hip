@@ -288,122 +288,135 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   const Layout& L = a.L;
   const uint4* P16 = reinterpret_cast<const uint4*>(a.packed);  // 16-B units
 
-  AVR_STAMP(0);
-  // ---- prologue: waves w and w+4 prepare samples 16 (w & 3) + j (the lanes
-  // share the geometry). The 6 * num_freqs sines of a sample are spread over
-  // its NW sub-lanes gg (PE entries gg, gg + NW, ...; sub-lanes 0-2 also own
-  // xyz_rot[gg] / R viewdir[gg]), then each value is written as fp16 hi/lo
-  // into its B-fragment slot; the padding features d_in .. 63 stay zero.
-  {
-    for (int i = threadIdx.x; i < 2 * kX3InChunks * 256; i += 64 * NW) X16[i] = make_uint4(0u, 0u, 0u, 0u);
-    for (int i = threadIdx.x; i < 512; i += 64 * NW) { tail->ht_key[i] = kEmpty; tail->ht_min[i] = kEmpty; }
-  }
-  const int npe = 6 * a.num_freqs;
-  float xr[3], vr[3];
-  {
-    const int s = 16 * (wid & 3) + j;
-    const int64_t m = base + s;
-    const int64_t mm = m < a.M ? m : a.M - 1;
-    const SampleGeom geo = SAVE ? sample_geom_pts(a.views[scene], a.xyz + 3 * roff, a.vd + 3 * roff, mm)
-                                : sample_geom_scene(a, multi ? a.views[scene] : a.v, roff, mm);
-    if (g == 0 && wid < 4) {
-      *reinterpret_cast<int4*>(tail->tex + 4 * s) = make_int4(geo.bl.tex[0], geo.bl.tex[1], geo.bl.tex[2], geo.bl.tex[3]);
-      *reinterpret_cast<float4*>(tail->w + 4 * s) = make_float4(geo.bl.w[0], geo.bl.w[1], geo.bl.w[2], geo.bl.w[3]);
-    }
-#pragma unroll
-    for (int d = 0; d < 3; ++d) { xr[d] = geo.xr[d]; vr[d] = geo.vr[d]; }
-  }
-  AVR_STAMP(27);
-  const int D = a.n_lin_z > 0 ? dedup_texels(tail, lane, wid) : 0;
-  AVR_STAMP(28);
-#ifdef AVR_STAMPS
-  if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 64 + 31] = (unsigned long long)D;
-#endif
-  float pe[PES], xo = 0.f, vo = 0.f;
-  float mx = 0.f;
-  {
-    // straight-line: every slot computes (selects, no branches); slots past
-    // npe are zeroed; the rare |argument| > 8192 takes sinf (uniform branch)
-    float arg[PES];
-    bool big = false;
-#pragma unroll
-    for (int i = 0; i < PES; ++i) {
-      const int q = gg + NW * i, jj = q / 3, dd = q - 3 * jj;
-      const float x = dd == 0 ? xr[0] : (dd == 1 ? xr[1] : xr[2]);
-      const float freq = fmul(a.freq_factor, __builtin_ldexpf(1.0f, jj >> 1));
-      const float phase = (jj & 1) ? 1.5707963705062866f : 0.f;  // fp32(pi/2)
-      arg[i] = fadd(phase, fmul(x, freq));
-      pe[i] = pe_sin_fast(arg[i]);
-      big |= q < npe && fabsf(arg[i]) > 8192.f;
-    }
-    if (__builtin_expect(__any(big), 0)) {
-#pragma unroll
-      for (int i = 0; i < PES; ++i)
-        if (fabsf(arg[i]) > 8192.f) pe[i] = sinf(arg[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < PES; ++i) {
-      pe[i] = gg + NW * i < npe ? pe[i] : 0.f;
-      mx = fmaxf(mx, fabsf(pe[i]));
-    }
-    if (gg < 3) { xo = gg == 0 ? xr[0] : (gg == 1 ? xr[1] : xr[2]); vo = gg == 0 ? vr[0] : (gg == 1 ? vr[1] : vr[2]); }
-    mx = fmaxf(mx, fmaxf(fabsf(xo), fabsf(vo)));
-    mx = wave_max(mx);
-  }
-  FragX3 A0[FT];   // chunk 0 of the next GEMM's weights, prefetched before the publish ahead of it
-  const uint4* Win = P16 + L.x3_in / 4 + 2 * 64 * FT * wid;
-  prefetch_a<FT, NPF>(A0, Win, lane);
-  AVR_STAMP(1);
-  float s_x;
-  {
-    if (lane == 0) red[wid] = mx;
-    lds_barrier();
-    s_x = pow2_scale_for(red_max<NW>(red));
-    const int s = 16 * (wid & 3) + j;
-    char* xb = reinterpret_cast<char*>(X16);
-    // feature k -> chunk k>>5, lane group (k>>2)&3, element 4*((k>>4)&1) + (k&3)
-    const auto put = [&](int k, float val) {
-      const int c = k >> 5, gg = (k >> 2) & 3, e = 4 * ((k >> 4) & 1) + (k & 3);
-      const float y = val * s_x;
-      const _Float16 hi = (_Float16)y;
-      *reinterpret_cast<_Float16*>(xb + xidx(c, 0, gg, s) * 16 + 2 * e) = hi;
-      *reinterpret_cast<_Float16*>(xb + xidx(c, 1, gg, s) * 16 + 2 * e) = (_Float16)(y - (float)hi);
-    };
-#pragma unroll
-    for (int i = 0; i < PES; ++i)
-      if (gg + NW * i < npe) put(3 + gg + NW * i, pe[i]);
-    if (gg < 3) { put(gg, xo); put(3 + npe + gg, vo); }
-    lds_barrier();
-  }
-
-  AVR_STAMP(2);
   floatx4 h[FT][4], t[FT][4], v[FT][4];
-
-  // ---- lin_in: h = (b_in + W_in . X) * S_h ; h stays scaled by S_h
-  float S_h = layer_scale(a.packed, L, 0) * s_x;
-#pragma unroll
-  for (int ft = 0; ft < FT; ++ft) {
-    const floatx4 b = *reinterpret_cast<const floatx4*>(a.packed + L.b_in + 16 * (FT * wid + ft) + 4 * g);
-#pragma unroll
-    for (int sg = 0; sg < 4; ++sg) h[ft][sg] = b * S_h;
-  }
-  AVR_STAMP(3);
+  FragX3 A0[FT];   // chunk 0 of the next GEMM's weights, prefetched before the publish ahead of it
+  float S_h = 1.0f, s_x = 1.0f, mx = 0.f;
   // 8 waves: stage rows of the next lin_z table that are already in flight
   // ([p0, p1), issued while the preceding GEMM still read other parts of X)
-  int p0 = 0, p1 = 0;
-  // 8 waves: block 0's lin_z stage rows that do not overlap lin_in's X are DMA'd before the lin_in GEMM
-  constexpr bool PRE0 = TWO;
-  if (PRE0 && a.n_lin_z > 0 && D <= P::CAP && D > P::IN_ROWS0) {
-    // the first table block 0 blends: lin_z[0], or scale_z[0] (table n_lin_z) with use_spade
-    stage_rows<HID, NW>(stage, a.table + (SPADE ? a.n_lin_z : 0) * a.table_stride + scene * a.table_scene_stride,
-                        tail, P::IN_ROWS0, D - P::IN_ROWS0, P::RS, lane, wid, P::IN_ROWS0);
-    p0 = P::IN_ROWS0;
-    p1 = D;
-  }
-  gemm<FT, false, TWO>(h, A0, Win, kX3InChunks, 64 * NTT, X16, lane);
-  AVR_STAMP(4);
+  int p0 = 0, p1 = 0, D = 0;
+  if (a.h_in == nullptr) {
+    AVR_STAMP(0);
+    // ---- prologue: waves w and w+4 prepare samples 16 (w & 3) + j (the lanes
+    // share the geometry). The 6 * num_freqs sines of a sample are spread over
+    // its NW sub-lanes gg (PE entries gg, gg + NW, ...; sub-lanes 0-2 also own
+    // xyz_rot[gg] / R viewdir[gg]), then each value is written as fp16 hi/lo
+    // into its B-fragment slot; the padding features d_in .. 63 stay zero.
+    {
+      for (int i = threadIdx.x; i < 2 * kX3InChunks * 256; i += 64 * NW) X16[i] = make_uint4(0u, 0u, 0u, 0u);
+      for (int i = threadIdx.x; i < 512; i += 64 * NW) { tail->ht_key[i] = kEmpty; tail->ht_min[i] = kEmpty; }
+    }
+    const int npe = 6 * a.num_freqs;
+    float xr[3], vr[3];
+    {
+      const int s = 16 * (wid & 3) + j;
+      const int64_t m = base + s;
+      const int64_t mm = m < a.M ? m : a.M - 1;
+      const SampleGeom geo = SAVE ? sample_geom_pts(a.views[scene], a.xyz + 3 * roff, a.vd + 3 * roff, mm)
+                                  : sample_geom_scene(a, multi ? a.views[scene] : a.v, roff, mm);
+      if (g == 0 && wid < 4) {
+        *reinterpret_cast<int4*>(tail->tex + 4 * s) = make_int4(geo.bl.tex[0], geo.bl.tex[1], geo.bl.tex[2], geo.bl.tex[3]);
+        *reinterpret_cast<float4*>(tail->w + 4 * s) = make_float4(geo.bl.w[0], geo.bl.w[1], geo.bl.w[2], geo.bl.w[3]);
+      }
+  #pragma unroll
+      for (int d = 0; d < 3; ++d) { xr[d] = geo.xr[d]; vr[d] = geo.vr[d]; }
+    }
+    AVR_STAMP(27);
+    D = a.n_lin_z > 0 ? dedup_texels(tail, lane, wid) : 0;
+    AVR_STAMP(28);
+  #ifdef AVR_STAMPS
+    if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 64 + 31] = (unsigned long long)D;
+  #endif
+    float pe[PES], xo = 0.f, vo = 0.f;
+    {
+      // straight-line: every slot computes (selects, no branches); slots past
+      // npe are zeroed; the rare |argument| > 8192 takes sinf (uniform branch)
+      float arg[PES];
+      bool big = false;
+  #pragma unroll
+      for (int i = 0; i < PES; ++i) {
+        const int q = gg + NW * i, jj = q / 3, dd = q - 3 * jj;
+        const float x = dd == 0 ? xr[0] : (dd == 1 ? xr[1] : xr[2]);
+        const float freq = fmul(a.freq_factor, __builtin_ldexpf(1.0f, jj >> 1));
+        const float phase = (jj & 1) ? 1.5707963705062866f : 0.f;  // fp32(pi/2)
+        arg[i] = fadd(phase, fmul(x, freq));
+        pe[i] = pe_sin_fast(arg[i]);
+        big |= q < npe && fabsf(arg[i]) > 8192.f;
+      }
+      if (__builtin_expect(__any(big), 0)) {
+  #pragma unroll
+        for (int i = 0; i < PES; ++i)
+          if (fabsf(arg[i]) > 8192.f) pe[i] = sinf(arg[i]);
+      }
+  #pragma unroll
+      for (int i = 0; i < PES; ++i) {
+        pe[i] = gg + NW * i < npe ? pe[i] : 0.f;
+        mx = fmaxf(mx, fabsf(pe[i]));
+      }
+      if (gg < 3) { xo = gg == 0 ? xr[0] : (gg == 1 ? xr[1] : xr[2]); vo = gg == 0 ? vr[0] : (gg == 1 ? vr[1] : vr[2]); }
+      mx = fmaxf(mx, fmaxf(fabsf(xo), fabsf(vo)));
+      mx = wave_max(mx);
+    }
+    const uint4* Win = P16 + L.x3_in / 4 + 2 * 64 * FT * wid;
+    prefetch_a<FT, NPF>(A0, Win, lane);
+    AVR_STAMP(1);
+    {
+      if (lane == 0) red[wid] = mx;
+      lds_barrier();
+      s_x = pow2_scale_for(red_max<NW>(red));
+      const int s = 16 * (wid & 3) + j;
+      char* xb = reinterpret_cast<char*>(X16);
+      // feature k -> chunk k>>5, lane group (k>>2)&3, element 4*((k>>4)&1) + (k&3)
+      const auto put = [&](int k, float val) {
+        const int c = k >> 5, gg = (k >> 2) & 3, e = 4 * ((k >> 4) & 1) + (k & 3);
+        const float y = val * s_x;
+        const _Float16 hi = (_Float16)y;
+        *reinterpret_cast<_Float16*>(xb + xidx(c, 0, gg, s) * 16 + 2 * e) = hi;
+        *reinterpret_cast<_Float16*>(xb + xidx(c, 1, gg, s) * 16 + 2 * e) = (_Float16)(y - (float)hi);
+      };
+  #pragma unroll
+      for (int i = 0; i < PES; ++i)
+        if (gg + NW * i < npe) put(3 + gg + NW * i, pe[i]);
+      if (gg < 3) { put(gg, xo); put(3 + npe + gg, vo); }
+      lds_barrier();
+    }
 
-  for (int b = 0; b < a.n_blocks; ++b) {
+    AVR_STAMP(2);
+    // ---- lin_in: h = (b_in + W_in . X) * S_h ; h stays scaled by S_h
+    S_h = layer_scale(a.packed, L, 0) * s_x;
+  #pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      const floatx4 b = *reinterpret_cast<const floatx4*>(a.packed + L.b_in + 16 * (FT * wid + ft) + 4 * g);
+  #pragma unroll
+      for (int sg = 0; sg < 4; ++sg) h[ft][sg] = b * S_h;
+    }
+    AVR_STAMP(3);
+    // 8 waves: stage rows of the next lin_z table that are already in flight
+    // ([p0, p1), issued while the preceding GEMM still read other parts of X)
+    // 8 waves: block 0's lin_z stage rows that do not overlap lin_in's X are DMA'd before the lin_in GEMM
+    constexpr bool PRE0 = TWO;
+    if (PRE0 && a.n_lin_z > 0 && D <= P::CAP && D > P::IN_ROWS0) {
+      // the first table block 0 blends: lin_z[0], or scale_z[0] (table n_lin_z) with use_spade
+      stage_rows<HID, NW>(stage, a.table + (SPADE ? a.n_lin_z : 0) * a.table_stride + scene * a.table_scene_stride,
+                          tail, P::IN_ROWS0, D - P::IN_ROWS0, P::RS, lane, wid, P::IN_ROWS0);
+      p0 = P::IN_ROWS0;
+      p1 = D;
+    }
+    gemm<FT, false, TWO>(h, A0, Win, kX3InChunks, 64 * NTT, X16, lane);
+    AVR_STAMP(4);
+  } else {
+    // the second half of a split pass (NS > 1 source views: avr_field_fwd_points_split): h = the combined
+    // residual stream at block b_begin's input, fp32 rows (scale 1); no geometry, no lin_z (b >= n_lin_z)
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        const int64_t m = base + 16 * sg + j;
+        const int64_t mm = m < a.M ? m : a.M - 1;
+        h[ft][sg] = *reinterpret_cast<const floatx4*>(a.h_in + (roff + mm) * HID + 16 * (FT * wid + ft) + 4 * g);
+      }
+  }
+
+  for (int b = a.b_begin; b < a.b_end; ++b) {
     // + lin_z[b](interp latent) (models.py ResnetFC: x = x + lin_z[b](z) before block b)
     // (fused with the fc_0 input prep: v = relu(h), mx)
     if (b < a.n_lin_z) lds_barrier();  // every wave is done reading X (the stage aliases it)
@@ -533,6 +546,21 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       gemm<FT, false, TWO>(h, A0, W1, KC, 64 * NTT, X16, lane);
     }
     AVR_STAMP(9 + 5 * (b & 3));
+  }
+  if (a.h_out) {
+    // the first half of a split pass: the residual stream after block b_end - 1, fp32 rows (h / S_h), for the
+    // caller's combine over the source views (combine_interleaved, models.py:566-579 / utils.py:71-81)
+    const float f = 1.0f / S_h;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        const int64_t m = base + 16 * sg + j;
+        if (m < a.M)
+          __builtin_nontemporal_store(h[ft][sg] * f, reinterpret_cast<floatx4*>(a.h_out + (roff + m) * HID +
+                                                                                16 * (FT * wid + ft) + 4 * g));
+      }
+    return;
   }
 
   if constexpr (TWO) {

@@ -243,6 +243,21 @@ int avr_field_fwd_points(const avr_field_dims* dims, const avr_view_desc* view, 
  * or s * n_points (points) of the inputs and of out. The same results as one
  * avr_field_fwd_rays / _points call per scene (the VolumeRenderer's SB > 1
  * batches, renderers.py:171-174 over models.py:739-863 per object).           */
+/* NS > 1 source views per object (NewPixelNeRFNet.num_views_per_obj, models.py:749-853; the MLP combines
+ * the views at combine_layer, ResnetFC.forward :566-579 with combine_interleaved, utils.py:71-81): x3
+ * inference as two launches around the caller's combine.
+ *   b_begin == 0 < b_end < n_blocks (b_end >= n_lin_z): lin_in and blocks [0, b_end) of n_scenes
+ *     (object, source view) pairs laid out as avr_field_fwd_points_batch's scenes (view s's pose, focal,
+ *     principal point and lin_z tables); h_out (n_scenes * n_points, d_hidden) receives the residual
+ *     stream entering block b_end instead of an output.
+ *   n_lin_z <= b_begin < b_end == n_blocks: blocks [b_begin, n_blocks) and lin_out of n_scenes objects
+ *     from h_in rows (the combined stream); out (n_scenes * n_points, 4). views / tables are checked as
+ *     in the batch call but not read; xyz / viewdirs may be NULL.                                      */
+int avr_field_fwd_points_split(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
+                               const float* packed, const float* tables, const float* xyz, const float* viewdirs,
+                               int64_t n_points, int b_begin, int b_end, const float* h_in, float* h_out, float* out,
+                               void* stream);
+
 int avr_field_fwd_rays_batch(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
                              const float* packed, const float* tables, const float* ro, const float* rd,
                              const float* z, int64_t n_rays, int n_samples, float* out, void* stream);

@@ -227,14 +227,30 @@ def softplus(v, beta):
     return np.where(bx > F32(20), v, sp).astype(F32)
 
 
-def resnetfc_forward(zx, p, d_latent, n_blocks, combine_layer, beta=0.0):
+def combine_interleaved(x, ns, agg_type="average"):
+    """utils.py:71-81 for one object: rows (ns, B) -> (B): mean or max over the source views
+    (fp32; the views are summed in order, then divided, as ATen's CPU mean does for small ns)."""
+    x = np.asarray(x, F32).reshape(ns, -1, x.shape[-1])
+    if agg_type == "average":
+        acc = x[0].copy()
+        for v in range(1, ns):
+            acc = (acc + x[v]).astype(F32)
+        return (acc / F32(ns)).astype(F32)
+    if agg_type == "max":
+        return x.max(axis=0)
+    raise NotImplementedError(agg_type)
+
+
+def resnetfc_forward(zx, p, d_latent, n_blocks, combine_layer, beta=0.0, ns=1, combine_type="average"):
     """ResnetFC.forward (models.py:541-592) with ResnetBlockFC (:454-470),
     NS=1 (combine_interleaved is the identity). beta > 0: every ReLU is
     Softplus(beta) (models.py:442-445, 536-537). With scale_z parameters in `p`
     (use_spade, :528-534) block b < combine_layer starts from
     scale_z[b](z) * x + lin_z[b](z) (:585-587). With bn parameters in `p`
     (train.py --bn, eval mode) every block applies bn_0 in front of BOTH relus,
-    as the reference does (models.py:456-461: bn_1 unused)."""
+    as the reference does (models.py:456-461: bn_1 unused). ns > 1: rows are
+    (source view, point) of one object; block combine_layer starts from the
+    views' combine (models.py:566-579)."""
     z = zx[:, :d_latent]
     x = _linear(zx[:, d_latent:], p["lin_in.weight"], p["lin_in.bias"])
     if beta > 0:
@@ -242,6 +258,8 @@ def resnetfc_forward(zx, p, d_latent, n_blocks, combine_layer, beta=0.0):
     else:
         relu = lambda v: np.maximum(v, F32(0))  # noqa: E731
     for b in range(n_blocks):
+        if b == combine_layer and ns > 1:
+            x = combine_interleaved(x, ns, combine_type)
         if d_latent > 0 and b < combine_layer:
             tz = _linear(z, p[f"lin_z.{b}.weight"], p[f"lin_z.{b}.bias"])
             if f"scale_z.{b}.weight" in p:
@@ -300,6 +318,32 @@ class PixelNeRFField:
         p = self.pc if coarse else self.pf
         out = resnetfc_forward(np.concatenate([lat, zf], -1), p, self.d_latent, self.n_blocks, self.combine_layer,
                                self.beta)
+        res = np.concatenate([1.0 / (1.0 + np.exp(-out[:, :3].astype(np.float64))), np.maximum(out[:, 3:4], 0)], -1)
+        return res.astype(F32).reshape(shp[:-1] + (4,))
+
+
+class MultiViewField:
+    """NewPixelNeRFNet.forward with NS > 1 source views of one object (models.py:749-853):
+    every point is transformed into each view (pose v, the object's focal / principal point,
+    view v's latent map), the MLP runs on the (view, point) rows and combines the views at
+    combine_layer."""
+
+    def __init__(self, params_coarse, params_fine, latents, poses, focal, c, image_shape, latent_scaling,
+                 n_blocks=3, combine_layer=1000, combine_type="average", num_freqs=6, freq_factor=1.5, beta=0.0):
+        latents = np.asarray(latents, F32)
+        self.views = [PixelNeRFField(params_coarse, params_fine, latents[v], np.asarray(poses, F32)[v], focal, c,
+                                     image_shape, latent_scaling, n_blocks, combine_layer, num_freqs, freq_factor,
+                                     beta) for v in range(latents.shape[0])]
+        self.pc, self.pf = params_coarse, params_fine
+        self.n_blocks, self.combine_layer, self.combine_type, self.beta = n_blocks, combine_layer, combine_type, beta
+        self.d_latent = latents.shape[1]
+
+    def __call__(self, xyz, viewdirs, coarse=True):
+        shp = np.asarray(xyz).shape
+        rows = [np.concatenate(f.features(xyz, viewdirs), -1) for f in self.views]
+        p = self.pc if coarse else self.pf
+        out = resnetfc_forward(np.concatenate(rows, 0), p, self.d_latent, self.n_blocks, self.combine_layer, self.beta,
+                               ns=len(self.views), combine_type=self.combine_type)
         res = np.concatenate([1.0 / (1.0 + np.exp(-out[:, :3].astype(np.float64))), np.maximum(out[:, 3:4], 0)], -1)
         return res.astype(F32).reshape(shp[:-1] + (4,))
 

@@ -144,7 +144,8 @@ def field_from_meta(g):
         spade = bool(int(g["spade"])) if "spade" in g else False
         pc = resnetfc_params(d_in, L, d_hidden, n_blocks, combine, int(g["weight_seed_coarse"]), spade=spade)
         pf = resnetfc_params(d_in, L, d_hidden, n_blocks, combine, int(g["weight_seed_fine"]), spade=spade)
-        latent = hashed_normalish((1, L) + hw, int(g["latent_seed"]), 1.0)
+        ns = int(g["ns"]) if "ns" in g else 1
+        latent = hashed_normalish((ns, L) + hw, int(g["latent_seed"]), 1.0)
     # eval-mode BatchNorm statistics / affine of bn=True nets (stored explicitly in the fixture)
     for tag, p in (("coarse", pc), ("fine", pf)):
         pre = f"bn_{tag}."

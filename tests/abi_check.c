@@ -112,6 +112,40 @@ int main(void) {
   expect("bn training rejected", avr_field_fwd_points_train(&d, &v, 1, buf, buf, buf, buf, 4, buf, buf, 4,
                                                             (uint32_t*)buf, NULL, NULL), AVR_E_INVALID);
   d.bn = 0;
+  /* use_spade / Softplus (ABI 8): the scale_z fragments and the 2 * n_lin_z table biases; x3 inference only */
+  d.spade = 1;
+  expect("packed_floats spade", avr_field_packed_floats(&d, &n), AVR_OK);
+  check("spade adds scale_z fragments + table biases", n - plain == 3 * (int64_t)512 * 512 + 6 * 512);
+  d.bn = 1;
+  expect("spade with bn rejected", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
+  d.bn = 0;
+  d.spade = 2;
+  expect("bad spade", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
+  d.spade = 0;
+  d.beta = -1.f;
+  expect("negative beta", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
+  d.beta = 2.f;
+  expect("softplus training rejected", avr_field_fwd_points_train(&d, &v, 1, buf, buf, buf, buf, 4, buf, buf, 4,
+                                                                  (uint32_t*)buf, NULL, NULL), AVR_E_INVALID);
+  d.precision = AVR_FIELD_FP32;
+  expect("softplus on fp32 rejected", avr_field_fwd_points(&d, &v, buf, buf, buf, buf, 4, buf, NULL), AVR_E_INVALID);
+  d.precision = AVR_FIELD_X3;
+  d.beta = 0.f;
+  /* NS > 1 split passes */
+  d.n_lin_z = 2;
+  expect("split bad b_end", avr_field_fwd_points_split(&d, &v, 1, buf, buf, buf, buf, 4, 0, 3, NULL, buf, NULL, NULL),
+         AVR_E_INVALID);
+  expect("split b_end < n_lin_z", avr_field_fwd_points_split(&d, &v, 1, buf, buf, buf, buf, 4, 0, 1, NULL, buf, NULL,
+                                                             NULL), AVR_E_INVALID);
+  expect("split first null h_out", avr_field_fwd_points_split(&d, &v, 1, buf, buf, buf, buf, 4, 0, 2, NULL, NULL,
+                                                              NULL, NULL), AVR_E_INVALID);
+  expect("split second null h_in", avr_field_fwd_points_split(&d, &v, 1, buf, buf, NULL, NULL, 4, 2, 3, NULL, NULL,
+                                                               buf, NULL), AVR_E_INVALID);
+  expect("split second before n_lin_z", avr_field_fwd_points_split(&d, &v, 1, buf, buf, NULL, NULL, 4, 1, 3, buf,
+                                                                    NULL, buf, NULL), AVR_E_INVALID);
+  expect("split empty", avr_field_fwd_points_split(&d, &v, 1, buf, buf, NULL, NULL, 0, 2, 3, NULL, NULL, NULL, NULL),
+         AVR_OK);
+  d.n_lin_z = 3;
   int64_t act = 0, mw = 0;
   expect("train sizes", avr_field_train_sizes(&d, 2, 100, &act, &mw), AVR_OK);
   check("train sizes act", act == (int64_t)7 * 2 * 100 * 512);

@@ -351,6 +351,41 @@ def g4_field():
              latent_at_points=lat.numpy()[:64], **meta, **params)
 
 
+def g4_field_multiview():
+    """NewPixelNeRFNet.forward with NS > 1 source views of one object (models.py:749-853): per-view
+    poses rotated about the y axis, one latent map per view, the views combined at combine_layer."""
+    B = 256
+    for tag, (d_hidden, n_blocks, combine, num_layers, lhw, store, ns, ctype) in {
+        "ns2_small": (64, 5, 3, 1, (8, 8), True, 2, "average"),
+        "ns2max_small": (64, 4, 2, 1, (8, 8), True, 2, "max"),
+        "ns3_mv512": (512, 5, 3, 4, (64, 64), False, 3, "average"),
+    }.items():
+        net, meta, params = build_field(REF_M, d_hidden, n_blocks, combine, num_layers, lhw, 40, store)
+        for mlp in (net.mlp_coarse, net.mlp_fine):
+            mlp.combine_type = ctype
+        L = meta["d_latent"]
+        latent = synth.hashed_normalish((ns, L) + tuple(lhw), 45, 1.0)
+        poses = np.zeros((ns, 3, 4), np.float32)
+        for v in range(ns):
+            a = 0.35 * v
+            poses[v, :3, :3] = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]], np.float32)
+            poses[v, 2, 3] = 1.3
+        net.encoder.latent = torch.from_numpy(latent)
+        net.poses = torch.from_numpy(poses)
+        net.num_views_per_obj = ns
+        meta.update(ns=ns, combine_type=ctype, poses=poses, latent_seed=45)
+        if store:
+            meta["latent"] = latent
+        xyz = synth.hashed_uniform((1, B, 3), 46, -0.5, 0.5)
+        vd = synth.hashed_uniform((1, B, 3), 47, -1.0, 1.0)
+        vd = (vd / np.linalg.norm(vd, axis=-1, keepdims=True)).astype(np.float32)
+        with torch.no_grad():
+            oc = net(torch.from_numpy(xyz), coarse=True, viewdirs=torch.from_numpy(vd))
+            of = net(torch.from_numpy(xyz), coarse=False, viewdirs=torch.from_numpy(vd))
+        assert oc.shape == (1, B, 4)
+        save(f"g4_field_{tag}.npz", xyz=xyz, viewdirs=vd, out_coarse=oc.numpy(), out_fine=of.numpy(), **meta, **params)
+
+
 def g5_forward(R):
     for tag, (Nc, Nf, Nd) in {"c64f32d16": (64, 32, 16), "c128f64d0": (128, 64, 0)}.items():
         net, meta, _ = build_field(REF_M, 512, 3, 1000, 4, (64, 64), 40, False)
@@ -505,6 +540,7 @@ if __name__ == "__main__":
     g2_sample_fine(48)
     g3_geometry(64)
     g4_field()
+    g4_field_multiview()
     g5_forward(64)
     g6_adaptive(48)
     g7_encoder()

@@ -37,7 +37,10 @@ def build_net(g, device, precision="x3"):
     net.focal = torch.from_numpy(g["focal"]).to(device)
     net.c = torch.from_numpy(g["c"]).to(device)
     net.image_shape = torch.from_numpy(g["image_shape"]).to(device)
-    net.num_views_per_obj = 1
+    net.num_views_per_obj = int(g["ns"]) if "ns" in g else 1
+    if "combine_type" in g:
+        for mlp in (net.mlp_coarse, net.mlp_fine):
+            mlp.combine_type = str(g["combine_type"])
     net.field_precision = precision
     for p in net.parameters():
         p.requires_grad_(False)
@@ -54,6 +57,10 @@ def _beta(g):
 
 def oracle_field(g):
     pc, pf, latent = synth.field_from_meta(g)
+    if "ns" in g:
+        return O.MultiViewField(pc, pf, latent, g["poses"], g["focal"], g["c"], g["image_shape"], g["latent_scaling"],
+                                n_blocks=int(g["n_blocks"]), combine_layer=int(g["combine_layer"]),
+                                combine_type=str(g["combine_type"]), beta=_beta(g))
     return O.PixelNeRFField(pc, pf, latent, g["poses"], g["focal"], g["c"], g["image_shape"], g["latent_scaling"],
                             n_blocks=int(g["n_blocks"]), combine_layer=int(g["combine_layer"]), beta=_beta(g))
 

@@ -326,6 +326,61 @@ def test_field_spade_softplus_many_texels_and_rays(golden, tag):
     np.testing.assert_array_equal(to_np(two[0]), to_np(a[0, :3000]))
 
 
+@pytest.mark.parametrize("tag", ["ns2_small", "ns2max_small", "ns3_mv512"])
+def test_field_multiview_golden(golden, tag):
+    """NS > 1 source views (models.py:749-853; ResnetFC combines the views at combine_layer,
+    :566-579): the fused x3 field in two launches around the combine (avr_field_fwd_points_split)
+    against the reference's own forward; the module's PyTorch graph agrees too."""
+    g = golden(f"g4_field_{tag}.npz")
+    net = build_net(g, DEV, "x3")
+    xyz, vd = T(g["xyz"]), T(g["viewdirs"])
+    assert net.num_views_per_obj == int(g["ns"]) > 1
+    with torch.no_grad():
+        assert not net.can_fuse(xyz) and net.can_fuse_multiview(xyz)
+        oc = net(xyz, coarse=True, viewdirs=vd)
+        of = net(xyz, coarse=False, viewdirs=vd)
+        tc = net.forward_torch(xyz, coarse=True, viewdirs=vd)
+    np.testing.assert_allclose(to_np(oc), g["out_coarse"], atol=5e-5, rtol=1e-4)
+    np.testing.assert_allclose(to_np(of), g["out_fine"], atol=5e-5, rtol=1e-4)
+    np.testing.assert_allclose(to_np(tc), g["out_coarse"], atol=5e-5, rtol=1e-4)
+
+
+def test_field_multiview_objects_and_renderer(golden):
+    """SB = 2 objects x NS = 2 views (more scenes than points per object would need: 4
+    (object, view) pairs in the first launch, 2 objects in the second), equal to each object
+    alone; a VolumeRenderer over an NS = 2 net routes its field calls to the split path."""
+    from avr.renderers import VolumeRenderer
+    from avr.scene import INTRINSICS
+    g = golden("g4_field_ns2_small.npz")
+    net = build_net(g, DEV, "x3")
+    lat, poses = net.encoder.latent, net.poses
+    net.encoder.latent = torch.cat([lat, lat.flip(-1)], 0)           # (SB * NS, L, H, W)
+    net.poses = torch.cat([poses, poses.flip(0)], 0)
+    gen = torch.Generator(device="cpu").manual_seed(3)
+    xyz = (torch.rand(2, 700, 3, generator=gen) - 0.5).to(DEV)
+    vd = torch.nn.functional.normalize(torch.randn(2, 700, 3, generator=gen), dim=-1).to(DEV)
+    with torch.no_grad():
+        both = net(xyz, coarse=False, viewdirs=vd)
+        ref = net.forward_torch(xyz, coarse=False, viewdirs=vd)
+    np.testing.assert_allclose(to_np(both), to_np(ref), atol=5e-5, rtol=1e-4)
+    for s in range(2):
+        net.encoder.latent = torch.cat([lat, lat.flip(-1)], 0)[2 * s:2 * s + 2]
+        net.poses = torch.cat([poses, poses.flip(0)], 0)[2 * s:2 * s + 2]
+        with torch.no_grad():
+            one = net(xyz[s:s + 1], coarse=False, viewdirs=vd[s:s + 1])
+        np.testing.assert_array_equal(to_np(one[0]), to_np(both[s]))
+    net.encoder.latent, net.poses = lat, poses
+    R = 128
+    x_pix = torch.rand(1, R, 2, generator=gen).to(DEV)
+    c2w = torch.eye(4, device=DEV).reshape(1, 1, 4, 4).expand(1, R, 4, 4).clone()
+    c2w[..., 2, 3] = -1.3
+    rend = VolumeRenderer(0.8, 1.8, 16, 8, 0, 0.01, True)
+    rend.seed = 5
+    with torch.no_grad():
+        rgb_c, rgb_f, depth, _ = rend(c2w, torch.tensor([INTRINSICS], device=DEV), x_pix, net)
+    assert rend.last_path == "module" and torch.isfinite(rgb_f).all() and torch.isfinite(depth).all()
+
+
 def test_field_spade_softplus_routes(golden):
     """use_spade / Softplus nets: fused on the x3 path for inference; precision fp32 and
     autograd run the module's PyTorch graph (which matches the reference's forward too)."""
