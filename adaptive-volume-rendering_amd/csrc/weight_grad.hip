@@ -84,7 +84,11 @@ __device__ __forceinline__ half8 tr_frag(const lds_char* img_full, int col0_full
 // accumulators fill the AGPRs). NW = 8: two waves per SIMD, 128 x 64 per wave
 // (256 registers), so one wave's MFMAs run while the other waits on LDS or
 // the barrier.
-template <int NW>
+//
+// PIPE: the split of chunk c + 1 into its (free) stage and the loads of chunk
+// c + 2 are interleaved with chunk c's MFMAs instead of following them after
+// the barrier, so the two waves of a SIMD never both sit in a split phase.
+template <int NW, bool PIPE = false>
 __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
   constexpr int WI = NW / 2;                 // waves across the 256 input columns
   constexpr int TO = 8, TI = 16 / WI;        // 16 x 16 MFMA tiles per wave: output rows x input columns
@@ -130,8 +134,13 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
     const int64_t row0 = k0 + (int64_t)kDwK * c;
     const int last = chunk_last(c);
     const int r = rb + NW * u < last ? rb + NW * u : last;
+#ifndef AVR_WGRAD_NO_LOAD   // diagnostic build: no global loads (constant operands)
     gn[u] = *reinterpret_cast<const floatx4*>(D.g + row0 * D.ldg + (r * ldg + gcol));
     xn[u] = *reinterpret_cast<const floatx4*>(D.x + row0 * D.ldx + (r * ldx + xcol));
+#else
+    gn[u] = floatx4{1.f, 2.f, 3.f, (float)r};
+    xn[u] = floatx4{(float)row0, 2.f, 1.f, 0.5f};
+#endif
   };
 
   const int wo = wid / WI, wi = wid % WI;
@@ -203,6 +212,64 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
     for (int u = 0; u < NU; ++u) put(c + 2, u);
   };
 
+  // Pipelined chunk c: stage c & 1 holds chunk c (visible since the last
+  // barrier); stage (c + 1) & 1 was last read in chunk c - 1, so row group u
+  // of chunk c + 1 (registers gn / xn, loaded during chunk c - 1) is split into
+  // it beside row tile 2u's MFMAs (TO / NU = 2 row tiles per row group), and
+  // the same registers are refilled with chunk c + 2 beside row tile 2u + 1.
+  // One LDS-only barrier per chunk (the loads stay in flight across it).
+  const auto step_pipe = [&](int c) {
+    const lds_char* st = lds + (c & 1) * kDwStage;
+    half8 bh[TI], bl[TI];
+#pragma unroll
+    for (int u = 0; u < TI; ++u) {
+      bh[u] = tr_frag(st + 2 * kDwImg, (256 / WI) * wi + 16 * u, trb);
+      bl[u] = tr_frag(st + 3 * kDwImg, (256 / WI) * wi + 16 * u, trb);
+    }
+    half8 ah = tr_frag(st, 128 * wo, trb), al = tr_frag(st + kDwImg, 128 * wo, trb);
+#pragma unroll
+    for (int t = 0; t < TO; ++t) {
+      half8 ahn = ah, aln = al;
+      if (t + 1 < TO) {
+        ahn = tr_frag(st, 128 * wo + 16 * (t + 1), trb);
+        aln = tr_frag(st + kDwImg, 128 * wo + 16 * (t + 1), trb);
+      }
+#ifndef AVR_WGRAD_NO_MFMA
+#pragma unroll
+      for (int u = 0; u < TI; ++u) {
+        acc[t][u] = mfma32h(ah, bh[u], acc[t][u]);
+        acc[t][u] = mfma32h(ah, bl[u], acc[t][u]);
+        acc[t][u] = mfma32h(al, bh[u], acc[t][u]);
+      }
+#else
+      acc[t][0][0] += __builtin_bit_cast(floatx4, ah)[0] + __builtin_bit_cast(floatx4, al)[1] +
+                      __builtin_bit_cast(floatx4, bh[t % TI])[2] + __builtin_bit_cast(floatx4, bl[t % TI])[3];
+#endif
+      constexpr int TPU = TO / NU;
+      if (t % TPU == 0) {
+        put(c + 1, t / TPU);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // VALU
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 3 * TI - 8, 0);
+      } else if (t % TPU == 1) {
+        load_u(c + 2, t / TPU);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);     // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3 * TI - 8, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      ah = ahn;
+      al = aln;
+    }
+    lds_barrier();
+  };
+
   if (nch > 0) {
 #pragma unroll
     for (int u = 0; u < NU; ++u) load_u(0, u);
@@ -210,11 +277,18 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
     for (int u = 0; u < NU; ++u) put(0, u);
 #pragma unroll
     for (int u = 0; u < NU; ++u) load_u(1, u);
+    if constexpr (!PIPE) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u) put(1, u);
+      for (int u = 0; u < NU; ++u) put(1, u);
+    }
     __syncthreads();
   }
-  for (int c = 0; c < nch; ++c) step(c);
+  if constexpr (PIPE) {
+    static_assert(TO == 2 * NU, "two row tiles per staged row group");
+    for (int c = 0; c < nch; ++c) step_pipe(c);
+  } else {
+    for (int c = 0; c < nch; ++c) step(c);
+  }
 
   // ---- partial dW: lane holds rows 4 (lane >> 4) + r, column lane & 15 of each 16 x 16 tile
   const float inv = (1.0f / sG) * (1.0f / sX);
@@ -284,14 +358,21 @@ extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel<4>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel<8>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel<8, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess)
       return fail(AVR_E_HIP, "weight_grad_kernel: cannot set dynamic LDS");
     attr = true;
   }
   const char* e = getenv("AVR_WGRAD_WAVES");   // 8 (default) or 4, read per call
+  // AVR_WGRAD_PIPE=0: the 8-wave kernel with the split after the MFMAs (the round-2 schedule, kept for A/B;
+  // the pipelined one is 3-6 % faster, profiles/r03g_wgrad_pipe_ab.txt)
+  const char* pe = getenv("AVR_WGRAD_PIPE");
   if (e && atoi(e) == 4)
     weight_grad_kernel<4><<<(unsigned)blocks, 256, 2 * kDwStage, as_stream(stream)>>>(a);
+  else if (pe && atoi(pe) == 0)
+    weight_grad_kernel<8, false><<<(unsigned)blocks, 512, 2 * kDwStage, as_stream(stream)>>>(a);
   else
-    weight_grad_kernel<8><<<(unsigned)blocks, 512, 2 * kDwStage, as_stream(stream)>>>(a);
+    weight_grad_kernel<8, true><<<(unsigned)blocks, 512, 2 * kDwStage, as_stream(stream)>>>(a);
   return check_launch("weight_grad_kernel");
 }

@@ -176,16 +176,18 @@ def test_volume_renderer_training_step_hip_vs_torch():
     del ops
 
 
-@pytest.mark.parametrize("waves", [8, 4])
+@pytest.mark.parametrize("waves,pipe", [(8, 0), (8, 1), (4, 0)])
 @pytest.mark.parametrize("M,O,I,ld", [(1000, 512, 512, 512), (77, 64, 44, 48), (4096, 4, 512, 512), (0, 128, 64, 64),
                                       (5000, 512, 64, 64)])
-def test_weight_grads_kernel_vs_fp64(M, O, I, ld, waves, monkeypatch):
+def test_weight_grads_kernel_vs_fp64(M, O, I, ld, waves, pipe, monkeypatch):
     """avr_weight_grads (split-K x3 MFMA, transposed LDS reads) against an fp64
     G^T X, with ragged row counts, narrow layers and row strides wider than the
-    layer, in a batch of two layers; both workgroup layouts (8 waves, the
-    default, and 4 via AVR_WGRAD_WAVES)."""
+    layer, in a batch of two layers; every workgroup layout (8 waves with the
+    split pipelined into the MFMAs or after them, 4 waves: AVR_WGRAD_PIPE /
+    AVR_WGRAD_WAVES)."""
     from avr import ops
     monkeypatch.setenv("AVR_WGRAD_WAVES", str(waves))
+    monkeypatch.setenv("AVR_WGRAD_PIPE", str(pipe))
     g = torch.Generator(device="cpu").manual_seed(M + O + I)
     G = (torch.randn(M, O, generator=g) * 1e-3 * (torch.rand(M, 1, generator=g) < 0.7)).to(DEV)
     Xb = torch.relu(torch.randn(M, ld, generator=g)).to(DEV)
