@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -103,6 +103,8 @@ _SIGS = {
     "avr_field_bwd": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_int, i64, c_void_p, c_void_p, c_void_p,
                       c_void_p, i64, c_void_p, c_void_p],
     "avr_weight_grads": [ctypes.POINTER(WGradLayer), c_int, i64, c_int, c_void_p],
+    "avr_weight_grads_reduce": [ctypes.POINTER(WGradLayer), c_int, c_int, ctypes.POINTER(c_void_p),
+                                ctypes.POINTER(c_void_p), c_void_p],
     "avr_latent_features": [ctypes.POINTER(ViewDesc), c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
     "avr_stream_copy": [c_void_p, c_void_p, i64, c_void_p],
 }

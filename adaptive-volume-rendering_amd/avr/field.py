@@ -225,6 +225,7 @@ class FusedField:
         latent = lat[sb].detach().to(F32).contiguous()
         require_device(latent)
         table = torch.empty(max(n_tables(dims), 1), H * W, dims.d_hidden, device=latent.device, dtype=F32)
+        dims.precision = PRECISIONS[self.precision]   # x3 fields: x3 tables (table_x3_kernel); fp32: exact
         call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W, ptr(table),
              stream_of(table))
         entry.tables[sb] = (key, table, lat)  # holding `lat` keeps its address from being reused
@@ -242,6 +243,7 @@ class FusedField:
         dims = entry.dims
         L, H, W = lat.shape[1:]
         out = torch.empty(n_scenes, max(n_tables(dims), 1), H * W, dims.d_hidden, device=lat.device, dtype=F32)
+        dims.precision = PRECISIONS[self.precision]
         for sb in range(n_scenes):
             latent = lat[min(sb, lat.shape[0] - 1)].detach().to(F32).contiguous()
             call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W, ptr(out[sb]),

@@ -398,22 +398,33 @@ def weight_grads(layers, n_rows, n_split=None):
     if n_split is None:
         n_split = _wgrad_splits(tiles, n_rows, dev)
     out = []
+    stream = stream_of(layers[0][0])
     for base in range(0, len(layers), _lib.AVR_WGRAD_MAX_LAYERS):
         chunk = layers[base:base + _lib.AVR_WGRAD_MAX_LAYERS]
         arr = (_lib.WGradLayer * len(chunk))()
-        keep = []
+        # the partials of the whole chunk in one buffer (every piece a multiple of 16 B: O, I multiples of 4)
+        sizes = [n_split * g.shape[1] * (x.shape[1] + (1 if wb else 0)) for g, x, _, _, wb in chunk]
+        flat = torch.empty(sum(sizes), device=dev, dtype=torch.float32)
+        dw_ptrs, db_ptrs = (ctypes.c_void_p * len(chunk))(), (ctypes.c_void_p * len(chunk))()
+        res, off = [], 0
         for k, (g, x, gmax, xmax, want_bias) in enumerate(chunk):
             O, I = g.shape[1], x.shape[1]
             for t in (g, x):
                 if t.dtype != torch.float32 or t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
                     raise _lib.AVRError("weight_grads: operands must be fp32 rows, 16-B aligned, unit column stride")
-            part = torch.empty(n_split, O, I, device=dev, dtype=torch.float32)
-            bpart = torch.empty(n_split, O, device=dev, dtype=torch.float32) if want_bias else None
+            part = flat[off:off + n_split * O * I]
+            bpart = flat[off + n_split * O * I:off + sizes[k]] if want_bias else None
+            off += sizes[k]
             arr[k] = _lib.WGradLayer(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), O, I, gmax.data_ptr(),
                                      xmax.data_ptr(), part.data_ptr(), 0 if bpart is None else bpart.data_ptr())
-            keep.append((part, bpart))
-        call("avr_weight_grads", arr, len(chunk), n_rows, n_split, stream_of(layers[0][0]))
-        out += [(p.sum(0), None if b is None else b.sum(0)) for p, b in keep]
+            dw = torch.empty(O, I, device=dev, dtype=torch.float32)
+            db = torch.empty(O, device=dev, dtype=torch.float32) if want_bias else None
+            dw_ptrs[k], db_ptrs[k] = dw.data_ptr(), (db.data_ptr() if want_bias else None)
+            res.append((dw, db))
+        call("avr_weight_grads", arr, len(chunk), n_rows, n_split, stream)
+        # sum over the splits, every layer in one launch (avr_weight_grads_reduce)
+        call("avr_weight_grads_reduce", arr, len(chunk), n_split, dw_ptrs, db_ptrs, stream)
+        out += res
     return out
 
 

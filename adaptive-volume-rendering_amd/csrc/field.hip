@@ -81,6 +81,12 @@ static int make_layout(const avr_field_dims* d, Layout* L) {
     for (int b = 0; b < d->n_lin_z; ++b) { L->scale_z[b] = o; o += (int64_t)L->KTl * NT * tile; }
     for (int t = 0; t < L->n_tables; ++t) { L->b_tab[t] = o; o += d->d_hidden; }
   }
+  L->x3_tables = d->d_latent % 64 == 0 && d->d_latent <= 512;
+  for (int t = 0; t < 2 * AVR_MAX_BLOCKS; ++t) L->x3_tab[t] = 0;
+  for (int t = 0; L->x3_tables && t < L->n_tables; ++t) {
+    L->x3_tab[t] = o;
+    o += (int64_t)(d->d_latent / 32) * NT * tile16;
+  }
   L->total = o;
   return AVR_OK;
 }
@@ -156,7 +162,7 @@ struct X3PackJob {
   int out_dim, in_dim, FTt;
 };
 struct X3PackBatch {
-  X3PackJob j[kX3MaxLayers];
+  X3PackJob j[kX3PackJobs];
   int count;
 };
 
@@ -412,7 +418,7 @@ static int pack_linear(const float* W, int out_dim, int in_dim, int NTo, int KTi
 static int add_x3(X3PackBatch& bt, const float* W, int out_dim, int in_dim, int KC, int FTt, unsigned* maxbits,
                   float* dst, bool transpose = false) {
   AVR_REQUIRE(W, "avr_field_pack: null weight tensor");
-  AVR_REQUIRE(bt.count < kX3MaxLayers, "avr_field_pack: too many layers");
+  AVR_REQUIRE(bt.count < kX3PackJobs, "avr_field_pack: too many layers");
   X3PackJob& J = bt.j[bt.count++];
   J.W = W;
   J.maxbits = maxbits;
@@ -594,6 +600,12 @@ extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_wei
     if ((rc = add_x3(bt, w->fc0_w[b], H, H, KC, NT, hdr + 2 + 2 * b, packed + L.x3_fc0[b]))) return rc;
     if ((rc = add_x3(bt, w->fc1_w[b], H, H, KC, NT, hdr + 3 + 2 * b, packed + L.x3_fc1[b]))) return rc;
   }
+  // the table weights for the x3 table kernel (lin_z[t], then scale_z with use_spade)
+  for (int t = 0; L.x3_tables && t < L.n_tables; ++t) {
+    const float* Wt = t < dims->n_lin_z ? w->lin_z_w[t] : w->scale_z_w[t - dims->n_lin_z];
+    if ((rc = add_x3(bt, Wt, H, dims->d_latent, dims->d_latent / 32, NT, hdr + kX3TabHdr + t, packed + L.x3_tab[t])))
+      return rc;
+  }
   return run_x3(bt, s);
 }
 
@@ -713,6 +725,9 @@ extern "C" int avr_field_latent_table(const avr_field_dims* dims, const float* p
   AVR_REQUIRE(H > 0 && W > 0, "avr_field_latent_table: bad latent size");
   if (L.n_tables == 0) return AVR_OK;
   hipStream_t s = as_stream(stream);
+  // x3 fields get x3 tables (the same split-fp16 products as their GEMMs); the fp32 field keeps exact ones
+  if (dims->precision == AVR_FIELD_X3 && L.x3_tables)
+    return dispatch_table_x3(packed, L, latent, H * W, dims->d_latent, dims->d_hidden, table, s);
   switch (dims->d_hidden) {
     case 64: return launch_table<4>(packed, L, latent, H * W, L.n_tables, table, s);
     case 128: return launch_table<8>(packed, L, latent, H * W, L.n_tables, table, s);

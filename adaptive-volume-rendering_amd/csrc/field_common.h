@@ -34,8 +34,14 @@ struct Layout {
   // (b_tab[t]: table t = lin_z[t] for t < n_lin_z, scale_z[t - n_lin_z] after)
   int spade, n_lin_z, n_tables;
   int64_t scale_z[AVR_MAX_BLOCKS], b_tab[2 * AVR_MAX_BLOCKS];
+  // x3 fragments of table t's weights (lin_z / scale_z, d_latent a multiple of 64 up to 512: the x3 table
+  // kernel's latent tile fits the LDS), header word kX3TabHdr + t
+  int x3_tables;
+  int64_t x3_tab[2 * AVR_MAX_BLOCKS];
   int64_t total;          // floats
 };
+constexpr int kX3TabHdr = kX3MaxLayers;                        // header words 18 .. 33
+constexpr int kX3PackJobs = kX3MaxLayers + 2 * AVR_MAX_BLOCKS;  // layers of one pack batch
 
 // Backward blob (avr_field_pack_bwd): header (64 words, max|W| bits per layer
 // in the forward's numbering) + x3 fragments of fc_0[b]^T and fc_1[b]^T in the
@@ -283,6 +289,9 @@ __device__ __forceinline__ float pow2_scale_for(float maxabs) {
 }
 
 int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s);
+// lin_z / scale_z tables on the x3 GEMM (L.x3_tables): table[t][texel][d_hidden], t < L.n_tables
+int dispatch_table_x3(const float* packed, const Layout& L, const float* latent, int HW, int d_latent, int d_hidden,
+                      float* table, hipStream_t s);
 
 struct BwdArgs {
   const float* packed;      // forward blob: lin_out fp32 fragments

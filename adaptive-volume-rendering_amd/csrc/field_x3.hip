@@ -666,6 +666,104 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   }
 }
 
+// ---- lin_z / scale_z tables on the same split-fp16 GEMM (x3 fields; the fp32 field keeps
+// latent_table_split_kernel's exact products): table[t][texel][f] = sum_c W_t[f][c] latent[c][texel]
+// (+ the table's bias with use_spade), for the 64 texels of a workgroup. The latent columns (CHW: one
+// coalesced 256-B row per channel) are split into X under one power-of-two scale per workgroup, then
+// KCL = d_latent / 32 K-chunks of the hidden layers' GEMM; blockIdx.y = table.
+template <int FT, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) table_x3_kernel(const float* __restrict__ packed, Layout L,
+                                                              const float* __restrict__ latent, int HW, int d_latent,
+                                                              float* __restrict__ table) {
+  constexpr int HID = 16 * FT * NW, NTT = FT * NW;
+  constexpr bool TWO = NW > 4;
+  constexpr int MAXQ = 512 / 4 / NW;               // 4-channel groups per wave (d_latent <= 512)
+  extern __shared__ float lds[];
+  uint4* X16 = reinterpret_cast<uint4*>(lds);
+  const int KCL = d_latent >> 5;
+  float* red = lds + KCL * 2048;                   // after X (8 KiB per chunk)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int t = blockIdx.y;
+  const int64_t t0 = (int64_t)blockIdx.x * kX3Samples;
+  const uint4* W = reinterpret_cast<const uint4*>(packed) + L.x3_tab[t] / 4 + 2 * 64 * FT * wid;
+  FragX3 A0[FT];
+  prefetch_a<FT, TWO ? FT : kPrefetch>(A0, W, lane);
+  // lane = texel; wave w loads channel groups w, w + NW, ...
+  const int64_t tx = t0 + lane < HW ? t0 + lane : HW - 1;
+  floatx4 xv[MAXQ];
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXQ; ++i) {
+    const int k = 4 * (wid + NW * i);
+    xv[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (k < d_latent) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xv[i][r] = latent[(int64_t)(k + r) * HW + tx];
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(xv[i].x), fabsf(xv[i].y)), fmaxf(fabsf(xv[i].z), fabsf(xv[i].w))));
+    }
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wid] = mx;
+  lds_barrier();
+  const float s_x = pow2_scale_for(red_max<NW>(red));
+  char* xb = reinterpret_cast<char*>(X16);
+#pragma unroll
+  for (int i = 0; i < MAXQ; ++i) {
+    const int k = 4 * (wid + NW * i);
+    if (k < d_latent) {
+      uint2 hi, lo;
+      split4(xv[i], s_x, hi, lo);
+      const int c = k >> 5, gq = (k >> 2) & 3, half = (k >> 4) & 1;
+      *reinterpret_cast<uint2*>(xb + xidx(c, 0, gq, lane) * 16 + 8 * half) = hi;
+      *reinterpret_cast<uint2*>(xb + xidx(c, 1, gq, lane) * 16 + 8 * half) = lo;
+    }
+  }
+  lds_barrier();
+  floatx4 acc[FT][4];
+  gemm<FT, true, TWO>(acc, A0, W, KCL, 64 * NTT, X16, lane);
+  const float inv = 1.0f / (layer_scale(packed, L, kX3TabHdr + t) * s_x);
+  float* dst = table + (int64_t)t * HW * HID;
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    const int f0 = 16 * (FT * wid + ft) + 4 * g;
+    const floatx4 b = L.spade ? *reinterpret_cast<const floatx4*>(packed + L.b_tab[t] + f0) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      const int64_t texel = t0 + 16 * sg + j;
+      if (texel < HW) *reinterpret_cast<floatx4*>(dst + texel * HID + f0) = acc[ft][sg] * inv + b;
+    }
+  }
+}
+
+template <int FT, int NW>
+static int launch_table_x3(const float* packed, const Layout& L, const float* latent, int HW, int d_latent,
+                           float* table, hipStream_t s) {
+  const size_t shm = (size_t)(d_latent / 32) * 8192 + 64;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&table_x3_kernel<FT, NW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 8192 * 4 + 64) != hipSuccess)
+      return fail(AVR_E_HIP, "table_x3_kernel: cannot set dynamic LDS");
+    attr = true;
+  }
+  const dim3 grid((unsigned)((HW + kX3Samples - 1) / kX3Samples), (unsigned)L.n_tables);
+  table_x3_kernel<FT, NW><<<grid, 64 * NW, shm, s>>>(packed, L, latent, HW, d_latent, table);
+  return check_launch("table_x3_kernel");
+}
+
+int dispatch_table_x3(const float* packed, const Layout& L, const float* latent, int HW, int d_latent, int d_hidden,
+                      float* table, hipStream_t s) {
+  AVR_REQUIRE(L.x3_tables && d_latent % 64 == 0 && d_latent <= 512, "table x3: d_latent %d", d_latent);
+  switch (d_hidden) {
+    case 64: return launch_table_x3<1, 4>(packed, L, latent, HW, d_latent, table, s);
+    case 128: return launch_table_x3<2, 4>(packed, L, latent, HW, d_latent, table, s);
+    case 256: return launch_table_x3<4, 4>(packed, L, latent, HW, d_latent, table, s);
+    case 512: return launch_table_x3<4, 8>(packed, L, latent, HW, d_latent, table, s);
+  }
+  return fail(AVR_E_UNSUPPORTED, "table x3: d_hidden %d", d_hidden);
+}
+
 template <int FT, int NW, bool SAVE, bool BN = false, bool SPADE = false, int ACT = 0>
 static int launch_x3(const FieldArgs& a, hipStream_t s) {
   const size_t shm = LdsPlan<16 * FT * NW>::BYTES;

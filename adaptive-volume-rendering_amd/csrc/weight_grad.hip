@@ -319,9 +319,68 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
   }
 }
 
+// ---- dW = sum_k partial[k], db = sum_k bias_partial[k] of every layer in one launch (float4 per thread,
+// the splits summed in order k = 0 .. n_split - 1): one job per output array, jobs laid end to end in
+// float4 units.
+constexpr int kDwRedJobs = 2 * AVR_WGRAD_MAX_LAYERS;
+
+struct DwReduceArgs {
+  const floatx4* src[kDwRedJobs];
+  floatx4* dst[kDwRedJobs];
+  int64_t n4[kDwRedJobs];       // float4 per split
+  int64_t start[kDwRedJobs + 1];
+  int jobs, ksplit;
+};
+
+__global__ void __launch_bounds__(256) weight_grad_reduce_kernel(DwReduceArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.start[a.jobs]) return;
+  int j = 0;
+  while (i >= a.start[j + 1]) ++j;
+  const int64_t e = i - a.start[j], n = a.n4[j];
+  const floatx4* p = a.src[j] + e;
+  floatx4 s = __builtin_nontemporal_load(p);
+  for (int k = 1; k < a.ksplit; ++k) s += __builtin_nontemporal_load(p + k * n);
+  a.dst[j][e] = s;
+}
+
 }  // namespace avr
 
 using namespace avr;
+
+extern "C" int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_split, float* const* dw,
+                                       float* const* db, void* stream) {
+  AVR_REQUIRE(layers && dw && n_layers >= 1 && n_layers <= AVR_WGRAD_MAX_LAYERS,
+              "avr_weight_grads_reduce: bad layer list");
+  AVR_REQUIRE(n_split >= 1, "avr_weight_grads_reduce: n_split must be >= 1");
+  DwReduceArgs a{};
+  a.ksplit = n_split;
+  int64_t total = 0;
+  for (int l = 0; l < n_layers; ++l) {
+    const avr_wgrad_layer& s = layers[l];
+    AVR_REQUIRE(s.partial && dw[l], "avr_weight_grads_reduce: null pointer (layer %d)", l);
+    AVR_REQUIRE(s.out_dim > 0 && s.in_dim > 0 && s.out_dim % 4 == 0 && s.in_dim % 4 == 0,
+                "avr_weight_grads_reduce: layer %d dims must be positive multiples of 4", l);
+    const bool want_b = s.bias_partial != nullptr;
+    AVR_REQUIRE(!want_b || (db && db[l]), "avr_weight_grads_reduce: layer %d has bias partials but no db", l);
+    const float* srcs[2] = {s.partial, s.bias_partial};
+    float* dsts[2] = {dw[l], want_b ? db[l] : nullptr};
+    const int64_t ns[2] = {(int64_t)s.out_dim * s.in_dim / 4, (int64_t)s.out_dim / 4};
+    for (int q = 0; q < (want_b ? 2 : 1); ++q) {
+      AVR_REQUIRE((reinterpret_cast<uintptr_t>(srcs[q]) | reinterpret_cast<uintptr_t>(dsts[q])) % 16 == 0,
+                  "avr_weight_grads_reduce: layer %d buffers must be 16-B aligned", l);
+      a.src[a.jobs] = reinterpret_cast<const floatx4*>(srcs[q]);
+      a.dst[a.jobs] = reinterpret_cast<floatx4*>(dsts[q]);
+      a.n4[a.jobs] = ns[q];
+      a.start[a.jobs] = total;
+      total += ns[q];
+      ++a.jobs;
+    }
+  }
+  a.start[a.jobs] = total;
+  weight_grad_reduce_kernel<<<(unsigned)((total + 255) / 256), 256, 0, as_stream(stream)>>>(a);
+  return check_launch("weight_grad_reduce_kernel");
+}
 
 extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int64_t n_rows, int n_split,
                                 void* stream) {

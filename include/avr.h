@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 8
+#define AVR_ABI_VERSION 9
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -326,6 +326,12 @@ typedef struct {
   float* bias_partial;      /* (n_split, out_dim) or NULL */
 } avr_wgrad_layer;
 int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int64_t n_rows, int n_split, void* stream);
+/* The caller's sum above, for the whole layer list in one launch (ABI 9): dw[l] (out_dim, in_dim) =
+ * sum_k layers[l].partial[k], and db[l] (out_dim) = sum_k layers[l].bias_partial[k] where bias_partial is
+ * not NULL, the splits added in order k = 0 .. n_split - 1 in fp32 (replaces torch's partial.sum(0) per
+ * layer; train.py's loss.backward() fills .grad from these). 16-B aligned buffers. */
+int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_split, float* const* dw,
+                            float* const* db, void* stream);
 
 /* Latent features at points — SpatialEncoder.index (models.py:245-274) as
  * NewPixelNeRFNet.forward uses it (models.py:753-810): bilinear / border /

@@ -115,7 +115,8 @@ int main(void) {
   /* use_spade / Softplus (ABI 8): the scale_z fragments and the 2 * n_lin_z table biases; x3 inference only */
   d.spade = 1;
   expect("packed_floats spade", avr_field_packed_floats(&d, &n), AVR_OK);
-  check("spade adds scale_z fragments + table biases", n - plain == 3 * (int64_t)512 * 512 + 6 * 512);
+  /* fp32 scale_z fragments, their x3 fragments (the x3 table kernel, ABI 9) and the table biases */
+  check("spade adds scale_z fragments + table biases", n - plain == 2 * 3 * (int64_t)512 * 512 + 6 * 512);
   d.bn = 1;
   expect("spade with bn rejected", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
   d.bn = 0;
@@ -152,6 +153,19 @@ int main(void) {
   expect("train sizes bad", avr_field_train_sizes(&d, 0, 100, &act, &mw), AVR_E_INVALID);
   expect("latent_table null", avr_field_latent_table(&d, NULL, NULL, 8, 8, NULL, NULL), AVR_E_INVALID);
   expect("wgrad no layers", avr_weight_grads(NULL, 0, 0, 1, NULL), AVR_E_INVALID);
+  {
+    avr_wgrad_layer wl;
+    memset(&wl, 0, sizeof(wl));
+    wl.out_dim = 8; wl.in_dim = 8; wl.partial = buf; wl.bias_partial = buf;
+    float* dwp[1] = {buf};
+    float* dbp[1] = {NULL};
+    expect("wgrad reduce no layers", avr_weight_grads_reduce(NULL, 0, 1, dwp, dbp, NULL), AVR_E_INVALID);
+    expect("wgrad reduce bad split", avr_weight_grads_reduce(&wl, 1, 0, dwp, dbp, NULL), AVR_E_INVALID);
+    expect("wgrad reduce bias without db", avr_weight_grads_reduce(&wl, 1, 1, dwp, dbp, NULL), AVR_E_INVALID);
+    expect("wgrad reduce null db list", avr_weight_grads_reduce(&wl, 1, 1, dwp, NULL, NULL), AVR_E_INVALID);
+    wl.in_dim = 6;
+    expect("wgrad reduce odd dims", avr_weight_grads_reduce(&wl, 1, 1, dwp, dbp, NULL), AVR_E_INVALID);
+  }
   expect("latent_features null view", avr_latent_features(NULL, NULL, 4, NULL, 3, NULL, NULL), AVR_E_INVALID);
   expect("raymarch null", avr_raymarch(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 4, 10, NULL, NULL,
                                        NULL, NULL), AVR_E_INVALID);

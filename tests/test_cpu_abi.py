@@ -52,8 +52,9 @@ def test_invalid_arguments_return_codes():
     assert lib.avr_field_packed_floats(ctypes.byref(dims), ctypes.byref(n)) == 0
     # fp32 fragments: 3 blocks x 2 x 512^2 + lin_in (3 tiles) + lin_out + 3 lin_z x 512^2 (+ biases)
     fp32 = 3 * 2 * 512 * 512 + 3 * 16 * 512 + 512 * 16 + 3 * 512 * 512 + 512 * 7 + 16
-    # split-fp16 fragments (hi+lo = 4 B per weight): header, lin_in (K 64), 6 x 512^2, lin_out (16 rows)
-    x3 = 64 + 64 * 512 + 6 * 512 * 512 + 16 * 512
+    # split-fp16 fragments (hi+lo = 4 B per weight): header, lin_in (K 64), 6 x 512^2, lin_out (16 rows),
+    # and the 3 lin_z (512 x 512, d_latent 512) for the x3 table kernel
+    x3 = 64 + 64 * 512 + 6 * 512 * 512 + 16 * 512 + 3 * 512 * 512
     assert n.value == ((fp32 + 63) // 64) * 64 + x3
 
 

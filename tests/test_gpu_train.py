@@ -194,15 +194,18 @@ def test_weight_grads_kernel_vs_fp64(M, O, I, ld, waves, pipe, monkeypatch):
     X = Xb[:, :I]
     G2 = (torch.randn(M, O, generator=g) * 5.0).to(DEV)
     mb = ops._max_bits if M else (lambda t: torch.zeros(1, dtype=torch.int32, device=DEV))
-    res = ops.weight_grads([(G, X, mb(G), mb(X), True), (G2, X, mb(G2), mb(X), False)], M)
-    for (dW, db), GG in zip(res, (G, G2)):
-        ref = (GG.double().t() @ X.double()).float().cpu().numpy()
-        got = dW.cpu().numpy()
-        scale = max(float(np.abs(ref).max()), 1e-30)
-        assert float(np.abs(got - ref).max()) <= 2e-6 * scale + 1e-30, float(np.abs(got - ref).max()) / scale
-    bref = G.double().sum(0).float().cpu().numpy()
-    np.testing.assert_allclose(res[0][1].cpu().numpy(), bref, rtol=0, atol=2e-6 * float(np.abs(bref).max(initial=0)) + 1e-30)
-    assert res[1][1] is None
+    lay = [(G, X, mb(G), mb(X), True), (G2, X, mb(G2), mb(X), False)]
+    # the library's own K-split, and an explicit 5-way split (avr_weight_grads_reduce sums the partials)
+    for res in (ops.weight_grads(lay, M), ops.weight_grads(lay, M, n_split=5 if M >= 5 else 1)):
+        for (dW, db), GG in zip(res, (G, G2)):
+            ref = (GG.double().t() @ X.double()).float().cpu().numpy()
+            got = dW.cpu().numpy()
+            scale = max(float(np.abs(ref).max()), 1e-30)
+            assert float(np.abs(got - ref).max()) <= 2e-6 * scale + 1e-30, float(np.abs(got - ref).max()) / scale
+        bref = G.double().sum(0).float().cpu().numpy()
+        np.testing.assert_allclose(res[0][1].cpu().numpy(), bref, rtol=0,
+                                   atol=2e-6 * float(np.abs(bref).max(initial=0)) + 1e-30)
+        assert res[1][1] is None
 
 
 def test_latent_features_kernel_vs_grid_sample():
@@ -290,3 +293,23 @@ def test_encoder_training_step_hip_vs_torch():
         a = net(xyz, coarse=True, viewdirs=vd)
         b = net.forward_torch(xyz, coarse=True, viewdirs=vd)
     np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), atol=5e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("d_hidden,d_latent,hw,combine", [(512, 512, (16, 20), 3), (128, 64, (7, 9), 1000),
+                                                          (64, 256, (5, 13), 2)])
+def test_latent_tables_vs_fp64(d_hidden, d_latent, hw, combine):
+    """The per-texel lin_z tables (table[t][texel] = lin_z[t].weight . latent[:, texel], the
+    bias folded into the layer before): the x3 field's tables (table_x3_kernel, split-fp16
+    GEMM) and the fp32 field's (exact fp32 MFMA products) against float64, ragged texel
+    counts (HW not a multiple of the 64-texel tile)."""
+    from avr.field import FusedField
+    net = _net(d_hidden, n_blocks=3, d_latent=d_latent, hw=hw, combine_layer=combine)
+    lat = net.encoder.latent[0].detach().double().reshape(d_latent, -1)
+    for coarse in (True, False):
+        mlp = net.mlp_coarse if coarse else net.mlp_fine
+        ref = torch.stack([(l.weight.detach().double() @ lat).t() for l in mlp.lin_z]).cpu().numpy()
+        for precision, bar in (("x3", 1e-5), ("fp32", 2e-6)):
+            got = FusedField(net, precision).table(coarse, 0)[:len(mlp.lin_z)].double().cpu().numpy()
+            assert got.shape == ref.shape
+            err = float(np.abs(got - ref).max()) / float(np.abs(ref).max())
+            assert err <= bar, (precision, err)
