@@ -154,7 +154,9 @@ class FusedField:
     def packed(self, coarse):
         mlp = self._mlp(coarse)
         params = [p.detach() for p in mlp.parameters()] + [b for b in mlp.buffers() if b.is_floating_point()]
-        key = (id(mlp), _version_key(params))
+        # the precision is part of the key: an x3 blob holds only the fragments the x3 kernels read
+        # (avr_field_pack), and net.fused() switches a FusedField's precision in place
+        key = (id(mlp), self.precision, _version_key(params))
         hit = self._packed.get(coarse)
         if hit is not None and hit[0] == key:
             return hit[1]
@@ -216,7 +218,7 @@ class FusedField:
     def table(self, coarse, sb=0):
         entry = self.packed(coarse)
         lat = self.net.encoder.latent
-        key = (sb, lat.data_ptr(), lat._version, tuple(lat.shape))
+        key = (sb, self.precision, lat.data_ptr(), lat._version, tuple(lat.shape))
         hit = entry.tables.get(sb)
         if hit is not None and hit[0] == key:
             return hit[1]
@@ -236,7 +238,7 @@ class FusedField:
         max(n_tables, 1), H*W, d_hidden): one buffer for the training launches."""
         entry = self.packed(coarse)
         lat = self.net.encoder.latent
-        key = (n_scenes, lat.data_ptr(), lat._version, tuple(lat.shape))
+        key = (n_scenes, self.precision, lat.data_ptr(), lat._version, tuple(lat.shape))
         hit = getattr(entry, "batch_tables", None)
         if hit is not None and hit[0] == key:
             return hit[1]

@@ -103,26 +103,47 @@ static int make_bwd_layout(const avr_field_dims* d, BwdLayout* LB) {
 }
 
 // ----------------------------------------------------------------- packing
-// dst[(t*NTo + ot)*64 + l][r] = W[16ot + (l&15)][16t + 4(l>>4) + r]  (zero padded)
-__global__ void pack_linear_kernel(const float* __restrict__ W, int out_dim, int in_dim, int NTo, int KTi,
-                                   float* __restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n = (int64_t)KTi * NTo * 256;
-  if (i >= n) return;
-  const int r = (int)(i & 3);
-  const int l = (int)((i >> 2) & 63);
-  const int64_t blk = i >> 8;
-  const int ot = (int)(blk % NTo), t = (int)(blk / NTo);
-  const int row = 16 * ot + (l & 15), col = 16 * t + 4 * (l >> 4) + r;
-  dst[i] = (row < out_dim && col < in_dim) ? W[(int64_t)row * in_dim + col] : 0.f;
+// fp32 fragments: dst[(t*NTo + ot)*64 + l][r] = W[16ot + (l&15)][16t + 4(l>>4) + r] (zero padded);
+// bias vectors: dst[i] = a[i] + b[i] (b may be null), zero beyond n.
+// The fp32 fragments and bias vectors of a pack in two launches (blockIdx.y = job), not one launch each:
+// the pack runs in every training step (the weights change).
+struct LinJob {
+  const float* W;
+  float* dst;
+  int out_dim, in_dim, NTo, KTi;
+};
+struct LinBatch {
+  LinJob j[2 + 4 * AVR_MAX_BLOCKS];
+  int count;
+};
+struct BiasJob {
+  const float* a;
+  const float* b;
+  float* dst;
+  int n, n_pad;
+};
+struct BiasBatch {
+  BiasJob j[2 + 8 * AVR_MAX_BLOCKS];
+  int count;
+};
+
+__global__ void pack_linear_batch_kernel(LinBatch bt) {
+  const LinJob& J = bt.j[blockIdx.y];
+  const int64_t n = (int64_t)J.KTi * J.NTo * 256;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i & 3);
+    const int l = (int)((i >> 2) & 63);
+    const int64_t blk = i >> 8;
+    const int ot = (int)(blk % J.NTo), t = (int)(blk / J.NTo);
+    const int row = 16 * ot + (l & 15), col = 16 * t + 4 * (l >> 4) + r;
+    J.dst[i] = (row < J.out_dim && col < J.in_dim) ? J.W[(int64_t)row * J.in_dim + col] : 0.f;
+  }
 }
 
-// dst[i] = a[i] + b[i] (b may be null), zero beyond n.
-__global__ void pack_bias_kernel(const float* __restrict__ a, const float* __restrict__ b, int n, int n_pad,
-                                 float* __restrict__ dst) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_pad) return;
-  dst[i] = (i < n) ? (b ? fadd(a[i], b[i]) : a[i]) : 0.f;
+__global__ void pack_bias_batch_kernel(BiasBatch bt) {
+  const BiasJob& J = bt.j[blockIdx.y];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < J.n_pad; i += gridDim.x * blockDim.x)
+    J.dst[i] = (i < J.n) ? (J.b ? fadd(J.a[i], J.b[i]) : J.a[i]) : 0.f;
 }
 
 
@@ -406,11 +427,11 @@ __global__ void __launch_bounds__(256) latent_table_split_kernel(const float* __
 }
 
 // ----------------------------------------------------------------- host side
-static int pack_linear(const float* W, int out_dim, int in_dim, int NTo, int KTi, float* dst, hipStream_t s) {
+static int pack_linear(const float* W, int out_dim, int in_dim, int NTo, int KTi, float* dst, LinBatch& bt) {
   AVR_REQUIRE(W, "avr_field_pack: null weight tensor");
-  const int64_t n = (int64_t)KTi * NTo * 256;
-  pack_linear_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(W, out_dim, in_dim, NTo, KTi, dst);
-  return check_launch("pack_linear_kernel");
+  AVR_REQUIRE(bt.count < (int)(sizeof(bt.j) / sizeof(bt.j[0])), "avr_field_pack: too many layers");
+  bt.j[bt.count++] = LinJob{W, dst, out_dim, in_dim, NTo, KTi};
+  return AVR_OK;
 }
 
 // one layer into a batch (W is (out_dim, in_dim) row-major; transpose: (in_dim,
@@ -449,10 +470,30 @@ static int run_x3(const X3PackBatch& bt, hipStream_t s) {
   return check_launch("pack_x3_batch_kernel");
 }
 
-static int pack_bias(const float* a, const float* b, int n, int n_pad, float* dst, hipStream_t s) {
+static int pack_bias(const float* a, const float* b, int n, int n_pad, float* dst, BiasBatch& bt) {
   AVR_REQUIRE(a, "avr_field_pack: null bias tensor");
-  pack_bias_kernel<<<(unsigned)((n_pad + 255) / 256), 256, 0, s>>>(a, b, n, n_pad, dst);
-  return check_launch("pack_bias_kernel");
+  AVR_REQUIRE(bt.count < (int)(sizeof(bt.j) / sizeof(bt.j[0])), "avr_field_pack: too many vectors");
+  bt.j[bt.count++] = BiasJob{a, b, dst, n, n_pad};
+  return AVR_OK;
+}
+
+static int run_fp32_packs(const LinBatch& lb, const BiasBatch& bb, hipStream_t s) {
+  int64_t n = 0;
+  for (int k = 0; k < lb.count; ++k) {
+    const int64_t nk = (int64_t)lb.j[k].KTi * lb.j[k].NTo * 256;
+    n = nk > n ? nk : n;
+  }
+  if (lb.count) {
+    pack_linear_batch_kernel<<<dim3((unsigned)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024), lb.count), 256, 0,
+                               s>>>(lb);
+    const int rc = check_launch("pack_linear_batch_kernel");
+    if (rc) return rc;
+  }
+  int nb = 0;
+  for (int k = 0; k < bb.count; ++k) nb = bb.j[k].n_pad > nb ? bb.j[k].n_pad : nb;
+  if (bb.count == 0) return AVR_OK;
+  pack_bias_batch_kernel<<<dim3((unsigned)((nb + 255) / 256), bb.count), 256, 0, s>>>(bb);
+  return check_launch("pack_bias_batch_kernel");
 }
 
 template <int NT>
@@ -562,33 +603,40 @@ extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_wei
   AVR_REQUIRE(w && packed, "avr_field_pack: null pointer");
   hipStream_t s = as_stream(stream);
   const int H = dims->d_hidden, NT = L.NT;
-  if ((rc = pack_linear(w->lin_in_w, H, dims->d_in, NT, kInTiles, packed + L.w_in, s))) return rc;
-  if ((rc = pack_linear(w->lin_out_w, 4, H, 1, NT, packed + L.w_out, s))) return rc;
+  // the fp32 fragments the x3 kernels never read (lin_in, fc_0, fc_1; lin_z / scale_z when the x3 table
+  // kernel takes the tables) are packed only for an fp32 blob
+  const bool fp32 = dims->precision != AVR_FIELD_X3, fp32_tab = fp32 || !L.x3_tables;
+  LinBatch lb{};
+  BiasBatch bb{};
+  if (fp32 && (rc = pack_linear(w->lin_in_w, H, dims->d_in, NT, kInTiles, packed + L.w_in, lb))) return rc;
+  if ((rc = pack_linear(w->lin_out_w, 4, H, 1, NT, packed + L.w_out, lb))) return rc;   // also the backward's
   for (int b = 0; b < dims->n_blocks; ++b) {
-    if ((rc = pack_linear(w->fc0_w[b], H, H, NT, NT, packed + L.fc0[b], s))) return rc;
-    if ((rc = pack_linear(w->fc1_w[b], H, H, NT, NT, packed + L.fc1[b], s))) return rc;
-    if ((rc = pack_bias(w->fc0_b[b], nullptr, H, H, packed + L.b_fc0[b], s))) return rc;
+    if (fp32 && (rc = pack_linear(w->fc0_w[b], H, H, NT, NT, packed + L.fc0[b], lb))) return rc;
+    if (fp32 && (rc = pack_linear(w->fc1_w[b], H, H, NT, NT, packed + L.fc1[b], lb))) return rc;
+    if ((rc = pack_bias(w->fc0_b[b], nullptr, H, H, packed + L.b_fc0[b], bb))) return rc;
     const float* bz = (b + 1 < dims->n_lin_z && !dims->spade) ? w->lin_z_b[b + 1] : nullptr;
-    if ((rc = pack_bias(w->fc1_b[b], bz, H, H, packed + L.b_fc1[b], s))) return rc;
+    if ((rc = pack_bias(w->fc1_b[b], bz, H, H, packed + L.b_fc1[b], bb))) return rc;
   }
-  for (int b = 0; b < dims->n_lin_z; ++b)
-    if ((rc = pack_linear(w->lin_z_w[b], H, dims->d_latent, NT, L.KTl, packed + L.lin_z[b], s))) return rc;
+  for (int b = 0; fp32_tab && b < dims->n_lin_z; ++b)
+    if ((rc = pack_linear(w->lin_z_w[b], H, dims->d_latent, NT, L.KTl, packed + L.lin_z[b], lb))) return rc;
   if ((rc = pack_bias(w->lin_in_b, dims->n_lin_z > 0 && !dims->spade ? w->lin_z_b[0] : nullptr, H, H,
-                      packed + L.b_in, s)))
+                      packed + L.b_in, bb)))
     return rc;
   for (int b = 0; dims->spade && b < dims->n_lin_z; ++b) {
     AVR_REQUIRE(w->scale_z_w[b] && w->scale_z_b[b] && w->lin_z_b[b],
                 "avr_field_pack: use_spade needs scale_z weight / bias and lin_z bias of every lin_z block");
-    if ((rc = pack_linear(w->scale_z_w[b], H, dims->d_latent, NT, L.KTl, packed + L.scale_z[b], s))) return rc;
-    if ((rc = pack_bias(w->lin_z_b[b], nullptr, H, H, packed + L.b_tab[b], s))) return rc;
-    if ((rc = pack_bias(w->scale_z_b[b], nullptr, H, H, packed + L.b_tab[dims->n_lin_z + b], s))) return rc;
+    if (fp32_tab && (rc = pack_linear(w->scale_z_w[b], H, dims->d_latent, NT, L.KTl, packed + L.scale_z[b], lb)))
+      return rc;
+    if ((rc = pack_bias(w->lin_z_b[b], nullptr, H, H, packed + L.b_tab[b], bb))) return rc;
+    if ((rc = pack_bias(w->scale_z_b[b], nullptr, H, H, packed + L.b_tab[dims->n_lin_z + b], bb))) return rc;
   }
-  if ((rc = pack_bias(w->lin_out_b, nullptr, 4, 16, packed + L.b_out, s))) return rc;
+  if ((rc = pack_bias(w->lin_out_b, nullptr, 4, 16, packed + L.b_out, bb))) return rc;
   for (int b = 0; dims->bn && b < dims->n_blocks; ++b) {
     AVR_REQUIRE(w->bn_scale[b] && w->bn_shift[b], "avr_field_pack: bn needs bn_scale / bn_shift of every block");
-    if ((rc = pack_bias(w->bn_scale[b], nullptr, H, H, packed + L.bn_a[b], s))) return rc;
-    if ((rc = pack_bias(w->bn_shift[b], nullptr, H, H, packed + L.bn_c[b], s))) return rc;
+    if ((rc = pack_bias(w->bn_scale[b], nullptr, H, H, packed + L.bn_a[b], bb))) return rc;
+    if ((rc = pack_bias(w->bn_shift[b], nullptr, H, H, packed + L.bn_c[b], bb))) return rc;
   }
+  if ((rc = run_fp32_packs(lb, bb, s))) return rc;
   // split-fp16 fragments (header word per layer: 0 lin_in, 1 lin_out, 2+2b fc0[b], 3+2b fc1[b])
   unsigned* hdr = reinterpret_cast<unsigned*>(packed + L.x3_hdr);
   if (hipMemsetAsync(hdr, 0, 64 * sizeof(float), s) != hipSuccess) return fail(AVR_E_HIP, "avr_field_pack: memset");

@@ -218,7 +218,9 @@ typedef struct {
 
 /* Floats needed for one packed ResnetFC (fragment-ordered weights + biases). */
 int avr_field_packed_floats(const avr_field_dims* dims, int64_t* n_floats);
-/* Repack one ResnetFC into MFMA fragment order (device -> device). */
+/* Repack one ResnetFC into MFMA fragment order (device -> device). dims->precision selects what is packed:
+ * AVR_FIELD_FP32 both the fp32 and the split-fp16 fragments, AVR_FIELD_X3 only what the x3 kernels read
+ * (ABI 9) -- run a blob with the precision it was packed for. */
 int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed, void* stream);
 /* table (n_lin_z, H*W, d_hidden) = lin_z[b].weight @ latent[:, texel] (no bias;
  * the bias is folded into the packed biases). latent (d_latent, H, W).

@@ -428,6 +428,23 @@ def _field_points_golden(golden, tag, precision):
     np.testing.assert_allclose(to_np(of), g["out_fine"], atol=5e-5, rtol=1e-4)
 
 
+def test_field_precision_switch_on_one_net(golden):
+    """net.field_precision switched back and forth on one net: each precision gets its own
+    packed blob and tables (an x3 blob holds only the x3 fragments, avr_field_pack), and every
+    pass matches the reference's forward (g4 mv512)."""
+    g = golden("g4_field_mv512.npz")
+    net = build_net(g, DEV, "x3")
+    xyz, vd = T(g["xyz"]), T(g["viewdirs"])
+    with torch.no_grad():
+        for precision in ("x3", "fp32", "x3", "fp32"):
+            net.field_precision = precision
+            assert net.can_fuse(xyz)
+            np.testing.assert_allclose(to_np(net(xyz, coarse=True, viewdirs=vd)), g["out_coarse"], atol=5e-5,
+                                       rtol=1e-4)
+            np.testing.assert_allclose(to_np(net(xyz, coarse=False, viewdirs=vd)), g["out_fine"], atol=5e-5,
+                                       rtol=1e-4)
+
+
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("tag", ["small", "small_mv", "full", "mv512", "d256"])
 def test_field_fused_matches_torch_path(golden, tag, precision):
