@@ -99,7 +99,8 @@ _SIGS = {
     "avr_field_bwd_packed_floats": [ctypes.POINTER(FieldDims), ctypes.POINTER(i64)],
     "avr_field_pack_bwd": [ctypes.POINTER(FieldDims), ctypes.POINTER(ResnetFCWeights), c_void_p, c_void_p],
     "avr_field_fwd_points_train": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p,
-                                   c_void_p, c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, c_void_p, c_void_p],
+                                   c_void_p, c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, c_void_p, c_void_p,
+                                   c_int, c_void_p, c_void_p],
     "avr_field_bwd": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_int, i64, c_void_p, c_void_p, c_void_p,
                       c_void_p, i64, c_void_p, c_void_p],
     "avr_weight_grads": [ctypes.POINTER(WGradLayer), c_int, i64, c_int, c_void_p],

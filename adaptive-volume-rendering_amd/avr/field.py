@@ -138,6 +138,26 @@ class FusedField:
         self.net = net
         self._packed = {}     # coarse(bool) -> (key, _Packed)
         self._view_cache = {}
+        self._latent_cache = {}   # per latent version: channels-last copies, max |latent| (both MLPs share them)
+
+    def _latent_cached(self, what, latent, make):
+        key = (latent.data_ptr(), latent._version, tuple(latent.shape))
+        hit = self._latent_cache.get(what)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        val = make()
+        self._latent_cache[what] = (key, val, latent)   # holding `latent` keeps its address from being reused
+        return val
+
+    def latent_hwc(self, latent, s):
+        """Scene s's latent map channels-last (avr_latent_features' operand), once per latent version."""
+        from .ops import latent_hwc
+        return self._latent_cached(("hwc", s), latent, lambda: latent_hwc(latent[s]))
+
+    def latent_max_bits(self, latent):
+        """max |latent| as int32 float bits (the lin_z weight gradients' X scale), once per latent version."""
+        from .ops import _max_bits
+        return self._latent_cached("max", latent, lambda: _max_bits(latent))
 
     # ----------------------------------------------------------- parameters
     def _mlp(self, coarse):
@@ -426,7 +446,9 @@ class _FieldTrain(torch.autograd.Function):
         dev = xyz.device
         out = torch.empty(SB, B, 4, device=dev, dtype=F32)
         act = torch.empty(n_l, Mt, H, device=dev, dtype=F32)
-        act_max = torch.zeros(n_l, device=dev, dtype=torch.int32)
+        act_max = torch.zeros(n_l + 1, device=dev, dtype=torch.int32)   # + max |z_feature|
+        zs = dims.d_in + (-dims.d_in) % 4                                # z_feature rows padded to 16 B
+        zf = torch.empty(Mt, zs, device=dev, dtype=F32)
         p = xyz.detach().to(F32).contiguous()
         v = viewdirs.reshape(SB, B, 3).detach().to(F32).contiguous()
         require_device(p, v)
@@ -441,11 +463,12 @@ class _FieldTrain(torch.autograd.Function):
             mask = torch.empty(max(mask_n.value, 1), device=dev, dtype=torch.int32)
             call("avr_field_fwd_points_train", ctypes.byref(dims), views, n, ptr(entry.packed), ptr(tables[g0]),
                  ptr(p[g0]), ptr(v[g0]), B, ptr(out[g0]), ctypes.c_void_p(act.data_ptr() + g0 * B * H * 4), Mt,
-                 ptr(mask), ptr(act_max), stream_of(p))
+                 ptr(mask), ptr(act_max), ctypes.c_void_p(zf.data_ptr() + g0 * B * zs * 4), zs,
+                 ctypes.c_void_p(act_max.data_ptr() + 4 * n_l), stream_of(p))
             masks.append((g0, n, mask))
         entry.dims.precision = PRECISIONS[fused.precision]
         ctx.fused, ctx.coarse, ctx.names, ctx.entry = fused, coarse, names, entry
-        ctx.act, ctx.act_max, ctx.masks = act, act_max, masks
+        ctx.act, ctx.act_max, ctx.masks, ctx.zf = act, act_max, masks, zf
         ctx.save_for_backward(xyz, viewdirs, latent, out, *params)
         return out
 
@@ -476,20 +499,20 @@ class _FieldTrain(torch.autograd.Function):
                  ptr(grad_out[g0]), ptr(mask), ctypes.c_void_p(G.data_ptr() + g0 * B * H * 4), Mt, ptr(g_max),
                  stream_of(G))
         entry.dims.precision = PRECISIONS[fused.precision]
-        act, act_max = ctx.act, ctx.act_max
-        ctx.act = ctx.act_max = ctx.masks = None
+        act, act_max, zf = ctx.act, ctx.act_max, ctx.zf
+        ctx.act = ctx.act_max = ctx.masks = ctx.zf = None
         # MLP inputs the lin_z / lin_in gradients contract against: the latent
-        # features (avr_latent_features, row-major) and z_feature (forward_torch's code)
+        # features (avr_latent_features, row-major) and z_feature (the training forward
+        # stored it, padded to 16 B, with its max in act_max[n_l])
+        d_in = dims.d_in
         with torch.no_grad():
-            z_feature = net.z_features(xyz.detach(), viewdirs.detach())
-            d_in = z_feature.shape[1]
-            zf = torch.nn.functional.pad(z_feature.to(F32), (0, (-d_in) % 4)).contiguous()
             lat_feat = torch.empty(Mt, net.d_latent, device=dev, dtype=F32)
             for sb in range(SB):
-                latent_features(fused.view(sb), latent[min(sb, latent.shape[0] - 1)], xyz[sb],
-                                out=lat_feat[sb * B:(sb + 1) * B])
-        lat_max = _max_bits(latent)          # |interpolated latent| <= max |latent| (convex blend)
-        zf_max = _max_bits(zf)
+                s = min(sb, latent.shape[0] - 1)
+                latent_features(fused.view(sb), latent[s], xyz[sb], out=lat_feat[sb * B:(sb + 1) * B],
+                                hwc=fused.latent_hwc(latent, s))
+        lat_max = fused.latent_max_bits(latent)   # |interpolated latent| <= max |latent| (convex blend)
+        zf_max = act_max[n_l:n_l + 1]
         Gz = [G[2 * b - 1] if b > 0 else G[2 * nb] for b in range(nz)]
         layers = []
         for b in range(nb):

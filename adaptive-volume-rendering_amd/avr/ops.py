@@ -428,12 +428,19 @@ def weight_grads(layers, n_rows, n_split=None):
     return out
 
 
-def latent_features(view, latent_chw, xyz, out=None):
+def latent_hwc(latent_chw):
+    """(C, H, W) -> the (H*W, C) channels-last fp32 copy avr_latent_features reads."""
+    C, H, W = latent_chw.shape
+    return latent_chw.detach().to(F32).reshape(C, H * W).t().contiguous()
+
+
+def latent_features(view, latent_chw, xyz, out=None, hwc=None):
     """SpatialEncoder.index at world points (models.py:245-274, 753-810):
     latent (C, H, W) of one source view (avr.field.FusedField.view gives the
-    ViewDesc), xyz (N, 3) -> (N, C) row-major (avr_latent_features)."""
+    ViewDesc), xyz (N, 3) -> (N, C) row-major (avr_latent_features). hwc: the
+    latent_hwc copy of latent_chw when the caller already has it."""
     C, H, W = latent_chw.shape
-    lat = latent_chw.detach().to(F32).reshape(C, H * W).t().contiguous()
+    lat = latent_hwc(latent_chw) if hwc is None else hwc
     xyz = _f32c(xyz.reshape(-1, 3))
     n = xyz.shape[0]
     if out is None:

@@ -704,7 +704,8 @@ extern "C" int avr_field_train_sizes(const avr_field_dims* dims, int n_scenes, i
 extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
                                           const float* packed, const float* tables, const float* xyz,
                                           const float* viewdirs, int64_t n_points, float* out, float* act,
-                                          int64_t act_rows, uint32_t* mask, uint32_t* act_max, void* stream) {
+                                          int64_t act_rows, uint32_t* mask, uint32_t* act_max, float* z_feature,
+                                          int ld_z, uint32_t* z_max, void* stream) {
   FieldArgs a{};
   AVR_REQUIRE(views && n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES,
               "avr_field_fwd_points_train: 1..%d scenes per call", AVR_MAX_SCENES);
@@ -728,6 +729,10 @@ extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_
   a.act_stride = act_rows * dims->d_hidden;
   a.mask = mask;
   a.act_max = act_max;
+  AVR_REQUIRE(!z_feature || ld_z >= dims->d_in, "avr_field_fwd_points_train: ld_z %d < d_in %d", ld_z, dims->d_in);
+  a.zf = z_feature;
+  a.zf_ld = ld_z;
+  a.zf_max = z_max;
   a.n_scenes = n_scenes;
   a.blocks_per_scene = (n_points + kX3Samples - 1) / kX3Samples;
   a.table_scene_stride = (int64_t)(a.L.n_tables > 0 ? a.L.n_tables : 1) * a.table_stride;

@@ -100,6 +100,9 @@ struct FieldArgs {
   int64_t act_stride;          //   floats between layers
   unsigned* mask;              //   their relu masks (see mask_words)
   unsigned* act_max;           //   per-layer max |act| as float bits (atomicMax), or null
+  float* zf;                   //   the lin_in input z_feature rows (ld zf_ld, zero padded), or null
+  int zf_ld;
+  unsigned* zf_max;            //   max |z_feature| as float bits (atomicMax), or null
   // training forward over several scenes in one launch: workgroup b works on
   // scene b / blocks_per_scene (M points each, rows scene * M + m), with that
   // scene's view and lin_z tables (table + scene * table_scene_stride)

@@ -49,6 +49,7 @@ struct ZTail {
   float red[16];
   int wtot[4];
   float lmax[kX3MaxLayers];   // training forward: max of each saved layer over the workgroup
+  float zmax;                 //                   and of the z_feature rows
 };
 constexpr unsigned kEmpty = 0xffffffffu;
 
@@ -359,10 +360,27 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     const uint4* Win = P16 + L.x3_in / 4 + 2 * 64 * FT * wid;
     prefetch_a<FT, NPF>(A0, Win, lane);
     AVR_STAMP(1);
+    if (SAVE && a.zf) {
+      // the training forward also keeps z_feature (lin_in's input, the operand of its weight gradient): the
+      // values this lane owns, the padding columns up to zf_ld as zeros
+      const int64_t m = base + 16 * (wid & 3) + j;
+      if (m < a.M) {
+        float* zr = a.zf + (roff + m) * a.zf_ld;
+  #pragma unroll
+        for (int i = 0; i < PES; ++i)
+          if (gg + NW * i < npe) __builtin_nontemporal_store(pe[i], zr + 3 + gg + NW * i);
+        if (gg < 3) {
+          __builtin_nontemporal_store(xo, zr + gg);
+          __builtin_nontemporal_store(vo, zr + 3 + npe + gg);
+        }
+        if (6 + npe + gg < a.zf_ld) __builtin_nontemporal_store(0.f, zr + 6 + npe + gg);
+      }
+    }
     {
       if (lane == 0) red[wid] = mx;
       lds_barrier();
       s_x = pow2_scale_for(red_max<NW>(red));
+      if (SAVE && threadIdx.x == 0) tail->zmax = red_max<NW>(red);
       const int s = 16 * (wid & 3) + j;
       char* xb = reinterpret_cast<char*>(X16);
       // feature k -> chunk k>>5, lane group (k>>2)&3, element 4*((k>>4)&1) + (k&3)
@@ -663,6 +681,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     // one per wave and layer in front of the weight loads cost ~1 ms per default_mv fine pass)
     const int nl = 2 * a.n_blocks + 1;
     if (a.act_max && wid == 0 && lane < nl) atomicMax(a.act_max + lane, __float_as_uint(tail->lmax[lane]));
+    if (a.zf_max && threadIdx.x == 64) atomicMax(a.zf_max, __float_as_uint(tail->zmax));
   }
 }
 

@@ -284,7 +284,10 @@ int avr_field_fwd_points_batch(const avr_field_dims* dims, const avr_view_desc* 
  *        relu(fc_0 out) into fc_1, act[2 n_blocks] = relu(x) into lin_out;
  *   mask (mask_words) their relu masks (opaque, read by avr_field_bwd);
  *   act_max (2 n_blocks + 1) or NULL: atomicMax of max |act[l]| (float bits;
- *        zero it first), the split scales of avr_weight_grads.
+ *        zero it first), the split scales of avr_weight_grads;
+ *   z_feature (rows, ld_z >= d_in) or NULL (ABI 9): lin_in's input rows as the
+ *        kernel computed them (xyz_rot, PE, viewdir_rot, models.py:763-789),
+ *        columns d_in .. ld_z-1 zero; z_max (1 word) or NULL: their max |.|.
  * Backward: avr_field_bwd, given the forward's out and d loss / d out
  * (n_points, 4), writes grads (layer l at grads + l * grads_rows * d_hidden,
  * grads_max as act_max):
@@ -303,7 +306,7 @@ int avr_field_pack_bwd(const avr_field_dims* dims, const avr_resnetfc_weights* w
 int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* views, int n_scenes,
                                const float* packed, const float* tables, const float* xyz, const float* viewdirs,
                                int64_t n_points, float* out, float* act, int64_t act_rows, uint32_t* mask,
-                               uint32_t* act_max, void* stream);
+                               uint32_t* act_max, float* z_feature, int ld_z, uint32_t* z_max, void* stream);
 int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd, int n_scenes,
                   int64_t n_points, const float* out, const float* grad_out, const uint32_t* mask, float* grads,
                   int64_t grads_rows, uint32_t* grads_max, void* stream);

@@ -110,8 +110,10 @@ int main(void) {
   expect("bn on fp32 rejected", avr_field_fwd_points(&d, &v, buf, buf, buf, buf, 4, buf, NULL), AVR_E_INVALID);
   d.precision = AVR_FIELD_X3;
   expect("bn training rejected", avr_field_fwd_points_train(&d, &v, 1, buf, buf, buf, buf, 4, buf, buf, 4,
-                                                            (uint32_t*)buf, NULL, NULL), AVR_E_INVALID);
+                                                            (uint32_t*)buf, NULL, NULL, 0, NULL, NULL), AVR_E_INVALID);
   d.bn = 0;
+  expect("train ld_z < d_in", avr_field_fwd_points_train(&d, &v, 1, buf, buf, buf, buf, 4, buf, buf, 4,
+                                                         (uint32_t*)buf, NULL, buf, 8, NULL, NULL), AVR_E_INVALID);
   /* use_spade / Softplus (ABI 8): the scale_z fragments and the 2 * n_lin_z table biases; x3 inference only */
   d.spade = 1;
   expect("packed_floats spade", avr_field_packed_floats(&d, &n), AVR_OK);
@@ -127,7 +129,7 @@ int main(void) {
   expect("negative beta", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
   d.beta = 2.f;
   expect("softplus training rejected", avr_field_fwd_points_train(&d, &v, 1, buf, buf, buf, buf, 4, buf, buf, 4,
-                                                                  (uint32_t*)buf, NULL, NULL), AVR_E_INVALID);
+                                                                  (uint32_t*)buf, NULL, NULL, 0, NULL, NULL), AVR_E_INVALID);
   d.precision = AVR_FIELD_FP32;
   expect("softplus on fp32 rejected", avr_field_fwd_points(&d, &v, buf, buf, buf, buf, 4, buf, NULL), AVR_E_INVALID);
   d.precision = AVR_FIELD_X3;
