@@ -85,6 +85,8 @@ _SIGS = {
     "avr_field_packed_floats": [ctypes.POINTER(FieldDims), ctypes.POINTER(i64)],
     "avr_field_pack": [ctypes.POINTER(FieldDims), ctypes.POINTER(ResnetFCWeights), c_void_p, c_void_p],
     "avr_field_latent_table": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "avr_field_latent_table_batch": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                     c_void_p],
     "avr_field_fwd_rays": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p],
     "avr_field_fwd_points": [ctypes.POINTER(FieldDims), ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p,
@@ -107,6 +109,7 @@ _SIGS = {
     "avr_weight_grads_reduce": [ctypes.POINTER(WGradLayer), c_int, c_int, ctypes.POINTER(c_void_p),
                                 ctypes.POINTER(c_void_p), c_void_p],
     "avr_latent_features": [ctypes.POINTER(ViewDesc), c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
+    "avr_latent_features_batch": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
     "avr_stream_copy": [c_void_p, c_void_p, i64, c_void_p],
 }
 EXPORTED = ("avr_version", "avr_last_error_string", "avr_device_count") + tuple(_SIGS)

@@ -154,6 +154,13 @@ class FusedField:
         from .ops import latent_hwc
         return self._latent_cached(("hwc", s), latent, lambda: latent_hwc(latent[s]))
 
+    def latent_hwc_all(self, latent):
+        """Every scene's latent map channels-last, (SB, H*W, C), once per latent version."""
+        def make():
+            SB, C, H, W = latent.shape
+            return latent.detach().to(F32).reshape(SB, C, H * W).transpose(1, 2).contiguous()
+        return self._latent_cached("hwc_all", latent, make)
+
     def latent_max_bits(self, latent):
         """max |latent| as int32 float bits (the lin_z weight gradients' X scale), once per latent version."""
         from .ops import _max_bits
@@ -266,10 +273,15 @@ class FusedField:
         L, H, W = lat.shape[1:]
         out = torch.empty(n_scenes, max(n_tables(dims), 1), H * W, dims.d_hidden, device=lat.device, dtype=F32)
         dims.precision = PRECISIONS[self.precision]
-        for sb in range(n_scenes):
-            latent = lat[min(sb, lat.shape[0] - 1)].detach().to(F32).contiguous()
-            call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W, ptr(out[sb]),
-                 stream_of(out))
+        if n_scenes <= lat.shape[0]:   # every scene its own map: one launch
+            latent = lat[:n_scenes].detach().to(F32).contiguous()
+            call("avr_field_latent_table_batch", ctypes.byref(dims), ptr(entry.packed), ptr(latent), n_scenes, H, W,
+                 ptr(out), stream_of(out))
+        else:
+            for sb in range(n_scenes):
+                latent = lat[min(sb, lat.shape[0] - 1)].detach().to(F32).contiguous()
+                call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W,
+                     ptr(out[sb]), stream_of(out))
         entry.batch_tables = (key, out, lat)
         return out
 
@@ -507,10 +519,19 @@ class _FieldTrain(torch.autograd.Function):
         d_in = dims.d_in
         with torch.no_grad():
             lat_feat = torch.empty(Mt, net.d_latent, device=dev, dtype=F32)
-            for sb in range(SB):
-                s = min(sb, latent.shape[0] - 1)
-                latent_features(fused.view(sb), latent[s], xyz[sb], out=lat_feat[sb * B:(sb + 1) * B],
-                                hwc=fused.latent_hwc(latent, s))
+            if SB <= latent.shape[0]:   # every scene its own map: one launch per AVR_MAX_SCENES scenes
+                hwc = fused.latent_hwc_all(latent)
+                p = xyz.detach().to(F32).contiguous()
+                for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
+                    n = min(_lib.AVR_MAX_SCENES, SB - g0)
+                    views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+                    call("avr_latent_features_batch", views, n, ptr(hwc[g0]), net.d_latent, ptr(p[g0]), B,
+                         ptr(lat_feat[g0 * B]), stream_of(lat_feat))
+            else:
+                for sb in range(SB):
+                    s = min(sb, latent.shape[0] - 1)
+                    latent_features(fused.view(sb), latent[s], xyz[sb], out=lat_feat[sb * B:(sb + 1) * B],
+                                    hwc=fused.latent_hwc(latent, s))
         lat_max = fused.latent_max_bits(latent)   # |interpolated latent| <= max |latent| (convex blend)
         zf_max = act_max[n_l:n_l + 1]
         Gz = [G[2 * b - 1] if b > 0 else G[2 * nb] for b in range(nz)]

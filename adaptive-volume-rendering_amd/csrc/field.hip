@@ -780,7 +780,7 @@ extern "C" int avr_field_latent_table(const avr_field_dims* dims, const float* p
   hipStream_t s = as_stream(stream);
   // x3 fields get x3 tables (the same split-fp16 products as their GEMMs); the fp32 field keeps exact ones
   if (dims->precision == AVR_FIELD_X3 && L.x3_tables)
-    return dispatch_table_x3(packed, L, latent, H * W, dims->d_latent, dims->d_hidden, table, s);
+    return dispatch_table_x3(packed, L, latent, H * W, dims->d_latent, dims->d_hidden, table, 1, s);
   switch (dims->d_hidden) {
     case 64: return launch_table<4>(packed, L, latent, H * W, L.n_tables, table, s);
     case 128: return launch_table<8>(packed, L, latent, H * W, L.n_tables, table, s);
@@ -788,6 +788,25 @@ extern "C" int avr_field_latent_table(const avr_field_dims* dims, const float* p
     case 512: return launch_table<32>(packed, L, latent, H * W, L.n_tables, table, s);
   }
   return fail(AVR_E_UNSUPPORTED, "field: d_hidden %d", dims->d_hidden);
+}
+
+extern "C" int avr_field_latent_table_batch(const avr_field_dims* dims, const float* packed, const float* latent,
+                                            int n_scenes, int H, int W, float* table, void* stream) {
+  Layout L;
+  int rc = make_layout(dims, &L);
+  if (rc) return rc;
+  AVR_REQUIRE(n_scenes >= 1, "avr_field_latent_table_batch: n_scenes must be >= 1");
+  AVR_REQUIRE(packed && latent && table, "avr_field_latent_table_batch: null pointer");
+  AVR_REQUIRE(H > 0 && W > 0, "avr_field_latent_table_batch: bad latent size");
+  if (L.n_tables == 0) return AVR_OK;
+  if (dims->precision == AVR_FIELD_X3 && L.x3_tables)
+    return dispatch_table_x3(packed, L, latent, H * W, dims->d_latent, dims->d_hidden, table, n_scenes,
+                             as_stream(stream));
+  const int64_t lat_stride = (int64_t)dims->d_latent * H * W, tab_stride = (int64_t)L.n_tables * H * W * dims->d_hidden;
+  for (int sc = 0; sc < n_scenes; ++sc)
+    if ((rc = avr_field_latent_table(dims, packed, latent + sc * lat_stride, H, W, table + sc * tab_stride, stream)))
+      return rc;
+  return AVR_OK;
 }
 
 extern "C" int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,

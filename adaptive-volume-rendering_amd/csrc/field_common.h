@@ -292,9 +292,10 @@ __device__ __forceinline__ float pow2_scale_for(float maxabs) {
 }
 
 int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s);
-// lin_z / scale_z tables on the x3 GEMM (L.x3_tables): table[t][texel][d_hidden], t < L.n_tables
+// lin_z / scale_z tables on the x3 GEMM (L.x3_tables): table[t][texel][d_hidden], t < L.n_tables, for
+// n_scenes latent maps (stride d_latent * HW) into tables back to back (stride max(n_tables, 1) * HW * d_hidden)
 int dispatch_table_x3(const float* packed, const Layout& L, const float* latent, int HW, int d_latent, int d_hidden,
-                      float* table, hipStream_t s);
+                      float* table, int n_scenes, hipStream_t s);
 
 struct BwdArgs {
   const float* packed;      // forward blob: lin_out fp32 fragments

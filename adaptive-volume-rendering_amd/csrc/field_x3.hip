@@ -693,7 +693,10 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
 template <int FT, int NW>
 __global__ void __launch_bounds__(64 * NW, 1) table_x3_kernel(const float* __restrict__ packed, Layout L,
                                                               const float* __restrict__ latent, int HW, int d_latent,
-                                                              float* __restrict__ table) {
+                                                              float* __restrict__ table, int64_t lat_stride,
+                                                              int64_t tab_stride) {
+  latent += blockIdx.z * lat_stride;   // scene blockIdx.z of a batch
+  table += blockIdx.z * tab_stride;
   constexpr int HID = 16 * FT * NW, NTT = FT * NW;
   constexpr bool TWO = NW > 4;
   constexpr int MAXQ = 512 / 4 / NW;               // 4-channel groups per wave (d_latent <= 512)
@@ -757,7 +760,7 @@ __global__ void __launch_bounds__(64 * NW, 1) table_x3_kernel(const float* __res
 
 template <int FT, int NW>
 static int launch_table_x3(const float* packed, const Layout& L, const float* latent, int HW, int d_latent,
-                           float* table, hipStream_t s) {
+                           float* table, int n_scenes, hipStream_t s) {
   const size_t shm = (size_t)(d_latent / 32) * 8192 + 64;
   static bool attr = false;
   if (!attr) {
@@ -766,19 +769,21 @@ static int launch_table_x3(const float* packed, const Layout& L, const float* la
       return fail(AVR_E_HIP, "table_x3_kernel: cannot set dynamic LDS");
     attr = true;
   }
-  const dim3 grid((unsigned)((HW + kX3Samples - 1) / kX3Samples), (unsigned)L.n_tables);
-  table_x3_kernel<FT, NW><<<grid, 64 * NW, shm, s>>>(packed, L, latent, HW, d_latent, table);
+  const dim3 grid((unsigned)((HW + kX3Samples - 1) / kX3Samples), (unsigned)L.n_tables, (unsigned)n_scenes);
+  const int64_t tab_stride = (int64_t)(L.n_tables > 0 ? L.n_tables : 1) * HW * (16 * FT * NW);
+  table_x3_kernel<FT, NW><<<grid, 64 * NW, shm, s>>>(packed, L, latent, HW, d_latent, table, (int64_t)d_latent * HW,
+                                                     tab_stride);
   return check_launch("table_x3_kernel");
 }
 
 int dispatch_table_x3(const float* packed, const Layout& L, const float* latent, int HW, int d_latent, int d_hidden,
-                      float* table, hipStream_t s) {
+                      float* table, int n_scenes, hipStream_t s) {
   AVR_REQUIRE(L.x3_tables && d_latent % 64 == 0 && d_latent <= 512, "table x3: d_latent %d", d_latent);
   switch (d_hidden) {
-    case 64: return launch_table_x3<1, 4>(packed, L, latent, HW, d_latent, table, s);
-    case 128: return launch_table_x3<2, 4>(packed, L, latent, HW, d_latent, table, s);
-    case 256: return launch_table_x3<4, 4>(packed, L, latent, HW, d_latent, table, s);
-    case 512: return launch_table_x3<4, 8>(packed, L, latent, HW, d_latent, table, s);
+    case 64: return launch_table_x3<1, 4>(packed, L, latent, HW, d_latent, table, n_scenes, s);
+    case 128: return launch_table_x3<2, 4>(packed, L, latent, HW, d_latent, table, n_scenes, s);
+    case 256: return launch_table_x3<4, 4>(packed, L, latent, HW, d_latent, table, n_scenes, s);
+    case 512: return launch_table_x3<4, 8>(packed, L, latent, HW, d_latent, table, n_scenes, s);
   }
   return fail(AVR_E_UNSUPPORTED, "table x3: d_hidden %d", d_hidden);
 }

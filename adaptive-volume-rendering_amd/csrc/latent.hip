@@ -13,13 +13,24 @@
 
 namespace avr {
 
-__global__ void __launch_bounds__(256) latent_features_kernel(View v, const float* __restrict__ lat_hwc, int C,
-                                                              const float* __restrict__ xyz, int64_t n_points,
-                                                              float* __restrict__ out) {
+// Scenes of a batch: blockIdx.y = scene s, its view, map lat_hwc + s * lat_stride, points xyz + 3 s n_points,
+// rows out + s * n_points * C. The rows stream out non-temporally (they are read once, by the weight-gradient
+// kernel, after every other kernel of the backward).
+struct LatBatch {
+  View v[AVR_MAX_SCENES];
+};
+
+__global__ void __launch_bounds__(256) latent_features_kernel(LatBatch vb, const float* __restrict__ lat_hwc,
+                                                              int64_t lat_stride, int C, const float* __restrict__ xyz,
+                                                              int64_t n_points, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= n_points) return;
-  const Bilinear bl = bilinear_at(v, xyz[3 * m], xyz[3 * m + 1], xyz[3 * m + 2]);
+  const int s = blockIdx.y;
+  lat_hwc += s * lat_stride;
+  xyz += 3 * s * n_points;
+  out += s * n_points * C;
+  const Bilinear bl = bilinear_at(vb.v[s], xyz[3 * m], xyz[3 * m + 1], xyz[3 * m + 2]);
   for (int c = 4 * lane; c < C; c += 256) {
     float4 acc;
     const float4 a = *reinterpret_cast<const float4*>(lat_hwc + (int64_t)bl.tex[0] * C + c);
@@ -31,7 +42,7 @@ __global__ void __launch_bounds__(256) latent_features_kernel(View v, const floa
     acc.y = fadd(fadd(fadd(fmul(a.y, bl.w[0]), fmul(b.y, bl.w[1])), fmul(d.y, bl.w[2])), fmul(e.y, bl.w[3]));
     acc.z = fadd(fadd(fadd(fmul(a.z, bl.w[0]), fmul(b.z, bl.w[1])), fmul(d.z, bl.w[2])), fmul(e.z, bl.w[3]));
     acc.w = fadd(fadd(fadd(fmul(a.w, bl.w[0]), fmul(b.w, bl.w[1])), fmul(d.w, bl.w[2])), fmul(e.w, bl.w[3]));
-    *reinterpret_cast<float4*>(out + m * C + c) = acc;
+    __builtin_nontemporal_store(floatx4{acc.x, acc.y, acc.z, acc.w}, reinterpret_cast<floatx4*>(out + m * C + c));
   }
 }
 
@@ -45,9 +56,30 @@ extern "C" int avr_latent_features(const avr_view_desc* view, const float* laten
   if (n_points == 0) return AVR_OK;
   AVR_REQUIRE(view && latent_hwc && xyz && out, "avr_latent_features: null pointer");
   AVR_REQUIRE(view->latent_h > 0 && view->latent_w > 0, "avr_latent_features: bad latent size");
-  View v;
-  view_from_desc(view, &v);
-  latent_features_kernel<<<(unsigned)((n_points + 3) / 4), 256, 0, as_stream(stream)>>>(v, latent_hwc, channels, xyz,
-                                                                                      n_points, out);
+  LatBatch vb;
+  view_from_desc(view, &vb.v[0]);
+  latent_features_kernel<<<dim3((unsigned)((n_points + 3) / 4), 1), 256, 0, as_stream(stream)>>>(
+      vb, latent_hwc, 0, channels, xyz, n_points, out);
+  return check_launch("latent_features_kernel");
+}
+
+extern "C" int avr_latent_features_batch(const avr_view_desc* views, int n_scenes, const float* latent_hwc,
+                                         int channels, const float* xyz, int64_t n_points, float* out,
+                                         void* stream) {
+  AVR_REQUIRE(n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES, "avr_latent_features_batch: 1..%d scenes per call",
+              AVR_MAX_SCENES);
+  AVR_REQUIRE(n_points >= 0 && channels > 0 && channels % 4 == 0, "avr_latent_features_batch: bad sizes");
+  if (n_points == 0) return AVR_OK;
+  AVR_REQUIRE(views && latent_hwc && xyz && out, "avr_latent_features_batch: null pointer");
+  LatBatch vb;
+  for (int s = 0; s < n_scenes; ++s) {
+    AVR_REQUIRE(views[s].latent_h == views[0].latent_h && views[s].latent_w == views[0].latent_w &&
+                    views[s].latent_h > 0 && views[s].latent_w > 0,
+                "avr_latent_features_batch: scenes need latent maps of one (positive) size");
+    view_from_desc(&views[s], &vb.v[s]);
+  }
+  const int64_t stride = (int64_t)views[0].latent_h * views[0].latent_w * channels;
+  latent_features_kernel<<<dim3((unsigned)((n_points + 3) / 4), (unsigned)n_scenes), 256, 0, as_stream(stream)>>>(
+      vb, latent_hwc, stride, channels, xyz, n_points, out);
   return check_launch("latent_features_kernel");
 }

@@ -228,6 +228,10 @@ int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_weights* w, fl
  * tables, each with its bias added.                                            */
 int avr_field_latent_table(const avr_field_dims* dims, const float* packed, const float* latent, int H, int W,
                            float* table, void* stream);
+/* The same for n_scenes maps in one launch (ABI 9): latent (n_scenes, d_latent, H, W), table (n_scenes,
+ * max(n_tables, 1), H*W, d_hidden) -- the layout avr_field_fwd_*_batch / _train read.                   */
+int avr_field_latent_table_batch(const avr_field_dims* dims, const float* packed, const float* latent, int n_scenes,
+                                 int H, int W, float* table, void* stream);
 /* Field at xyz = ro[r] + rd[r] * z[r, s], viewdir = rd[r]; out (n_rays*n_samples, 4)
  * = (sigmoid rgb, relu sigma).                                                 */
 int avr_field_fwd_rays(const avr_field_dims* dims, const avr_view_desc* view, const float* packed,
@@ -345,6 +349,10 @@ int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_s
  * channels). channels multiple of 4.                                           */
 int avr_latent_features(const avr_view_desc* view, const float* latent_hwc, int channels, const float* xyz,
                         int64_t n_points, float* out, void* stream);
+/* n_scenes (<= AVR_MAX_SCENES) views in one launch (ABI 9): latent_hwc (n_scenes, H*W, channels), xyz
+ * (n_scenes, n_points, 3), out (n_scenes * n_points, channels).                                         */
+int avr_latent_features_batch(const avr_view_desc* views, int n_scenes, const float* latent_hwc, int channels,
+                              const float* xyz, int64_t n_points, float* out, void* stream);
 
 /* --------------------------------------------------------- LSTM ray marcher
  * Raymarcher / AdaptiveVolumeRenderer march (renderers.py:313-351, :380-432):

@@ -169,6 +169,14 @@ int main(void) {
     expect("wgrad reduce odd dims", avr_weight_grads_reduce(&wl, 1, 1, dwp, dbp, NULL), AVR_E_INVALID);
   }
   expect("latent_features null view", avr_latent_features(NULL, NULL, 4, NULL, 3, NULL, NULL), AVR_E_INVALID);
+  expect("latent_features_batch too many scenes",
+         avr_latent_features_batch(&v, AVR_MAX_SCENES + 1, buf, 4, buf, 3, buf, NULL), AVR_E_INVALID);
+  expect("latent_features_batch null", avr_latent_features_batch(&v, 1, NULL, 4, buf, 3, buf, NULL), AVR_E_INVALID);
+  expect("latent_features_batch odd channels", avr_latent_features_batch(&v, 1, buf, 6, buf, 3, buf, NULL),
+         AVR_E_INVALID);
+  expect("latent_table_batch null", avr_field_latent_table_batch(&d, NULL, NULL, 2, 8, 8, NULL, NULL), AVR_E_INVALID);
+  expect("latent_table_batch no scenes", avr_field_latent_table_batch(&d, buf, buf, 0, 8, 8, buf, NULL),
+         AVR_E_INVALID);
   expect("raymarch null", avr_raymarch(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 4, 10, NULL, NULL,
                                        NULL, NULL), AVR_E_INVALID);
 

@@ -176,6 +176,37 @@ def test_volume_renderer_training_step_hip_vs_torch():
     del ops
 
 
+def test_volume_renderer_coarse_loss_hip_vs_torch():
+    """The renderer-level step with the loss on the coarse rgb only: no fine-pass bin
+    choice in the gradient path (a ULP-level weight change can move a fine sample to
+    another bin, which is why the two-pass step above is compared at 5e-3), so the HIP
+    field backward and the PyTorch graph must agree to fp32 accuracy: 1e-4 of max |grad|
+    for every coarse-MLP parameter, and the fine MLP gets no gradient on either path."""
+    from avr.renderers import VolumeRenderer
+    from avr.scene import INTRINSICS
+    net = _net(512, 5, 64, (8, 8), combine_layer=3)
+    R = 300
+    g = torch.Generator(device="cpu").manual_seed(6)
+    x_pix = torch.rand(1, R, 2, generator=g).to(DEV)
+    c2w = torch.eye(4).reshape(1, 1, 4, 4).expand(1, R, 4, 4).clone()
+    c2w[..., 2, 3] = -1.3
+    c2w = c2w.to(DEV)
+    K = torch.tensor([INTRINSICS], device=DEV)
+    gt = torch.rand(1, R, 3, generator=g).to(DEV)
+    res = {}
+    for hip in (True, False):
+        net.hip_backward = hip
+        net.zero_grad(set_to_none=True)
+        rend = VolumeRenderer(0.8, 1.8, 64, 32, 0, 0.01, True)
+        rend.seed = 12
+        rgb_c, _, _, _ = rend(c2w, K, x_pix, net)
+        ((rgb_c - gt) ** 2).mean().backward()
+        res[hip] = {n: p.grad.clone() for n, p in net.named_parameters()
+                    if p.grad is not None and float(p.grad.abs().max()) > 0}
+    assert all(n.startswith("mlp_coarse.") for n in res[True]), sorted(res[True])
+    _compare(res[True], res[False], 1e-4)
+
+
 @pytest.mark.parametrize("waves,pipe", [(8, 0), (8, 1), (4, 0)])
 @pytest.mark.parametrize("M,O,I,ld", [(1000, 512, 512, 512), (77, 64, 44, 48), (4096, 4, 512, 512), (0, 128, 64, 64),
                                       (5000, 512, 64, 64)])
@@ -313,3 +344,27 @@ def test_latent_tables_vs_fp64(d_hidden, d_latent, hw, combine):
             assert got.shape == ref.shape
             err = float(np.abs(got - ref).max()) / float(np.abs(ref).max())
             assert err <= bar, (precision, err)
+
+
+def test_batched_latent_features_and_tables_match_per_scene():
+    """avr_latent_features_batch and avr_field_latent_table_batch (every scene of a
+    training batch in one launch) give the per-scene launches' results bit for bit."""
+    from avr import _lib, ops
+    from avr._lib import call, ptr, stream_of
+    from avr.field import FusedField
+    net = _net(512, 5, 64, (9, 11), combine_layer=3, sb=3)
+    xyz, _, _ = _points(3, 777, seed=4)
+    f = FusedField(net, "x3")
+    lat = net.encoder.latent.detach()
+    SB, C = lat.shape[:2]
+    per = torch.cat([ops.latent_features(f.view(s), lat[s], xyz[s]) for s in range(SB)])
+    got = torch.empty_like(per)
+    views = (_lib.ViewDesc * SB)(*[f.view(s) for s in range(SB)])
+    hwc = f.latent_hwc_all(lat)
+    call("avr_latent_features_batch", views, SB, ptr(hwc), C, ptr(xyz.contiguous()), xyz.shape[1], ptr(got),
+         stream_of(got))
+    assert torch.equal(per, got)
+    for coarse in (True, False):
+        batch = f.tables_batch(coarse, SB)
+        for s in range(SB):
+            assert torch.equal(batch[s], f.table(coarse, s)), (coarse, s)
