@@ -107,6 +107,21 @@ def _freq_factor(code):
     return float(ff)
 
 
+class _precision:
+    """dims.precision set for one library call and restored after it."""
+
+    def __init__(self, dims, value):
+        self.dims, self.value = dims, value
+
+    def __enter__(self):
+        self.saved = self.dims.precision
+        self.dims.precision = self.value
+
+    def __exit__(self, *exc):
+        self.dims.precision = self.saved
+        return False
+
+
 def _version_key(tensors):
     return tuple((t.data_ptr(), t._version) for t in tensors)
 
@@ -245,7 +260,7 @@ class FusedField:
     def table(self, coarse, sb=0):
         entry = self.packed(coarse)
         lat = self.net.encoder.latent
-        key = (sb, self.precision, lat.data_ptr(), lat._version, tuple(lat.shape))
+        key = (sb, lat.data_ptr(), lat._version, tuple(lat.shape))
         hit = entry.tables.get(sb)
         if hit is not None and hit[0] == key:
             return hit[1]
@@ -254,35 +269,38 @@ class FusedField:
         latent = lat[sb].detach().to(F32).contiguous()
         require_device(latent)
         table = torch.empty(max(n_tables(dims), 1), H * W, dims.d_hidden, device=latent.device, dtype=F32)
-        dims.precision = PRECISIONS[self.precision]   # x3 fields: x3 tables (table_x3_kernel); fp32: exact
-        call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W, ptr(table),
-             stream_of(table))
+        with _precision(dims, _lib.FIELD_FP32):   # inference: exact fp32 tables, computed once per latent map
+            call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W, ptr(table),
+                 stream_of(table))
         entry.tables[sb] = (key, table, lat)  # holding `lat` keeps its address from being reused
         return table
 
-    def tables_batch(self, coarse, n_scenes):
+    def tables_batch(self, coarse, n_scenes, fast=False):
         """The lin_z tables of scenes 0 .. n_scenes-1 back to back, (n_scenes,
-        max(n_tables, 1), H*W, d_hidden): one buffer for the training launches."""
+        max(n_tables, 1), H*W, d_hidden): one buffer for the multi-scene launches.
+        fast (the training path, which recomputes them every step): on the split-fp16
+        GEMM (table_x3_kernel); otherwise exact fp32 products."""
         entry = self.packed(coarse)
         lat = self.net.encoder.latent
-        key = (n_scenes, self.precision, lat.data_ptr(), lat._version, tuple(lat.shape))
-        hit = getattr(entry, "batch_tables", None)
+        key = (n_scenes, bool(fast), lat.data_ptr(), lat._version, tuple(lat.shape))
+        cache = entry.__dict__.setdefault("batch_tables", {})
+        hit = cache.get(bool(fast))
         if hit is not None and hit[0] == key:
             return hit[1]
         dims = entry.dims
         L, H, W = lat.shape[1:]
         out = torch.empty(n_scenes, max(n_tables(dims), 1), H * W, dims.d_hidden, device=lat.device, dtype=F32)
-        dims.precision = PRECISIONS[self.precision]
-        if n_scenes <= lat.shape[0]:   # every scene its own map: one launch
-            latent = lat[:n_scenes].detach().to(F32).contiguous()
-            call("avr_field_latent_table_batch", ctypes.byref(dims), ptr(entry.packed), ptr(latent), n_scenes, H, W,
-                 ptr(out), stream_of(out))
-        else:
-            for sb in range(n_scenes):
-                latent = lat[min(sb, lat.shape[0] - 1)].detach().to(F32).contiguous()
-                call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W,
-                     ptr(out[sb]), stream_of(out))
-        entry.batch_tables = (key, out, lat)
+        with _precision(dims, _lib.FIELD_X3 if fast else _lib.FIELD_FP32):
+            if n_scenes <= lat.shape[0]:   # every scene its own map: one launch
+                latent = lat[:n_scenes].detach().to(F32).contiguous()
+                call("avr_field_latent_table_batch", ctypes.byref(dims), ptr(entry.packed), ptr(latent), n_scenes,
+                     H, W, ptr(out), stream_of(out))
+            else:
+                for sb in range(n_scenes):
+                    latent = lat[min(sb, lat.shape[0] - 1)].detach().to(F32).contiguous()
+                    call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W,
+                         ptr(out[sb]), stream_of(out))
+        cache[bool(fast)] = (key, out, lat)
         return out
 
     def view(self, sb=0, ns=1):
@@ -464,7 +482,7 @@ class _FieldTrain(torch.autograd.Function):
         p = xyz.detach().to(F32).contiguous()
         v = viewdirs.reshape(SB, B, 3).detach().to(F32).contiguous()
         require_device(p, v)
-        tables = fused.tables_batch(coarse, SB)
+        tables = fused.tables_batch(coarse, SB, fast=True)
         masks = []
         for g0 in range(0, SB, _lib.AVR_MAX_SCENES):     # one launch per group of scenes
             n = min(_lib.AVR_MAX_SCENES, SB - g0)

@@ -603,9 +603,9 @@ extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_wei
   AVR_REQUIRE(w && packed, "avr_field_pack: null pointer");
   hipStream_t s = as_stream(stream);
   const int H = dims->d_hidden, NT = L.NT;
-  // the fp32 fragments the x3 kernels never read (lin_in, fc_0, fc_1; lin_z / scale_z when the x3 table
-  // kernel takes the tables) are packed only for an fp32 blob
-  const bool fp32 = dims->precision != AVR_FIELD_X3, fp32_tab = fp32 || !L.x3_tables;
+  // the fp32 fragments the x3 kernels never read (lin_in, fc_0, fc_1) are packed only for an fp32 blob; the
+  // lin_z / scale_z ones always (the exact-fp32 tables)
+  const bool fp32 = dims->precision != AVR_FIELD_X3, fp32_tab = true;
   LinBatch lb{};
   BiasBatch bb{};
   if (fp32 && (rc = pack_linear(w->lin_in_w, H, dims->d_in, NT, kInTiles, packed + L.w_in, lb))) return rc;
@@ -778,7 +778,8 @@ extern "C" int avr_field_latent_table(const avr_field_dims* dims, const float* p
   AVR_REQUIRE(H > 0 && W > 0, "avr_field_latent_table: bad latent size");
   if (L.n_tables == 0) return AVR_OK;
   hipStream_t s = as_stream(stream);
-  // x3 fields get x3 tables (the same split-fp16 products as their GEMMs); the fp32 field keeps exact ones
+  // AVR_FIELD_X3: tables on the split-fp16 GEMM (the training path, which recomputes them every step);
+  // AVR_FIELD_FP32: exact fp32 products (inference: computed once per latent map)
   if (dims->precision == AVR_FIELD_X3 && L.x3_tables)
     return dispatch_table_x3(packed, L, latent, H * W, dims->d_latent, dims->d_hidden, table, 1, s);
   switch (dims->d_hidden) {

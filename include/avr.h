@@ -219,13 +219,15 @@ typedef struct {
 /* Floats needed for one packed ResnetFC (fragment-ordered weights + biases). */
 int avr_field_packed_floats(const avr_field_dims* dims, int64_t* n_floats);
 /* Repack one ResnetFC into MFMA fragment order (device -> device). dims->precision selects what is packed:
- * AVR_FIELD_FP32 both the fp32 and the split-fp16 fragments, AVR_FIELD_X3 only what the x3 kernels read
- * (ABI 9) -- run a blob with the precision it was packed for. */
+ * AVR_FIELD_FP32 both the fp32 and the split-fp16 fragments, AVR_FIELD_X3 only what the x3 kernels and the
+ * tables read (ABI 9) -- run the field kernels with the precision the blob was packed for. */
 int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed, void* stream);
 /* table (n_lin_z, H*W, d_hidden) = lin_z[b].weight @ latent[:, texel] (no bias;
  * the bias is folded into the packed biases). latent (d_latent, H, W).
  * dims->spade: (2 * n_lin_z, H*W, d_hidden) — lin_z[b] tables, then scale_z[b]
- * tables, each with its bias added.                                            */
+ * tables, each with its bias added. dims->precision: AVR_FIELD_FP32 exact fp32
+ * products, AVR_FIELD_X3 the split-fp16 GEMM (d_latent a multiple of 64 up to
+ * 512; ABI 9 -- the training path, which recomputes the tables every step).    */
 int avr_field_latent_table(const avr_field_dims* dims, const float* packed, const float* latent, int H, int W,
                            float* table, void* stream);
 /* The same for n_scenes maps in one launch (ABI 9): latent (n_scenes, d_latent, H, W), table (n_scenes,

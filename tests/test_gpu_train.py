@@ -3,6 +3,8 @@ loss.backward() through NewPixelNeRFNet, models.py:739-863): the x3 training
 forward + HIP backward chain + sample-GEMM weight gradients against PyTorch
 fp32 autograd of the same module (forward_torch), parameter by parameter,
 including the latent map's gradient and a VolumeRenderer training step."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -339,11 +341,14 @@ def test_latent_tables_vs_fp64(d_hidden, d_latent, hw, combine):
     for coarse in (True, False):
         mlp = net.mlp_coarse if coarse else net.mlp_fine
         ref = torch.stack([(l.weight.detach().double() @ lat).t() for l in mlp.lin_z]).cpu().numpy()
-        for precision, bar in (("x3", 1e-5), ("fp32", 2e-6)):
-            got = FusedField(net, precision).table(coarse, 0)[:len(mlp.lin_z)].double().cpu().numpy()
-            assert got.shape == ref.shape
-            err = float(np.abs(got - ref).max()) / float(np.abs(ref).max())
-            assert err <= bar, (precision, err)
+        for precision in ("x3", "fp32"):
+            f = FusedField(net, precision)
+            # the training path's tables (split-fp16 GEMM) and inference's (exact fp32 products)
+            for got, bar in ((f.tables_batch(coarse, 1, fast=True)[0], 1e-5), (f.table(coarse, 0), 2e-6)):
+                got = got[:len(mlp.lin_z)].double().cpu().numpy()
+                assert got.shape == ref.shape
+                err = float(np.abs(got - ref).max()) / float(np.abs(ref).max())
+                assert err <= bar, (precision, bar, err)
 
 
 def test_batched_latent_features_and_tables_match_per_scene():
@@ -368,3 +373,17 @@ def test_batched_latent_features_and_tables_match_per_scene():
         batch = f.tables_batch(coarse, SB)
         for s in range(SB):
             assert torch.equal(batch[s], f.table(coarse, s)), (coarse, s)
+        # the split-fp16 tables: one launch over the scenes = one launch per scene
+        fast = f.tables_batch(coarse, SB, fast=True)
+        entry = f.packed(coarse)
+        saved = entry.dims.precision
+        entry.dims.precision = _lib.FIELD_X3
+        try:
+            for s in range(SB):
+                one = torch.empty_like(fast[s])
+                H, W = lat.shape[2:]
+                call("avr_field_latent_table", ctypes.byref(entry.dims), ptr(entry.packed), ptr(lat[s].contiguous()),
+                     H, W, ptr(one), stream_of(one))
+                assert torch.equal(fast[s], one), (coarse, s)
+        finally:
+            entry.dims.precision = saved
