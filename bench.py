@@ -660,6 +660,67 @@ def config5_leg(args, net, fused, K, device):
                         f"x ({args.n_coarse} coarse + {args.n_fine} fine), the per-rank renderer call of --gpus N"}
 
 
+def config2_leg(args, net, fused, K, c2w, x_pix, device):
+    """BASELINE configs[1]: the coarse pass alone on the headline rays (65536 x 128: rays, stratified z,
+    field, composite), one launch chain per step."""
+    import avr
+
+    def step():
+        fused._packed.clear()
+        with torch.no_grad():
+            ro, rd, zc, _, _ = avr.ops.rays_sample_coarse(x_pix, K, c2w, 0.8, 1.8, args.n_coarse, seed=1234)
+            rgb_c, _, _ = avr.ops.composite(zc, fused.forward_rays(ro[0], rd[0], zc, True), True, want_weights=False)
+        return rgb_c
+
+    steps = max(args.config5_steps, 3)
+    elapsed, out = time_steps(step, steps, 1, 1, device)
+    assert bool(torch.isfinite(out).all())
+    R = x_pix.shape[1]
+    return {"value": round(R * steps / elapsed, 1), "unit": "rays/s", "steps": steps, "warmup": 1,
+            "ms_per_step": round(elapsed / steps * 1e3, 3),
+            "workload": f"BASELINE config 2: {R} rays x {args.n_coarse} coarse samples, coarse pass only"}
+
+
+def config4_leg(args, net, K, device):
+    """BASELINE configs[3]: one 800x800 frame per step with fine-pass early termination at T_stop 1e-5, on the
+    bench's field (a fog that never reaches T < 1e-5 in [0.8, 1.8]: every sample is evaluated) and on the same
+    field with its density biased by +30 (rays saturate as on an opaque scene: the tail is skipped)."""
+    from avr.renderers import VolumeRenderer
+    from avr.video import get_opencv_pixel_coordinates
+    x_pix = get_opencv_pixel_coordinates(args.frame, args.frame).reshape(1, -1, 2).to(device)
+    R = x_pix.shape[1]
+    c2w = orbit_c2w(0.7).to(device).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
+    res = {}
+    for bias in (0.0, 30.0):
+        n = net if bias == args.sigma_bias else build_scene(device, sigma_bias=bias)
+        n.field_precision = args.precision
+        rend = VolumeRenderer(0.8, 1.8, args.n_coarse, args.n_fine, 0, 0.01, True)
+        rend.seed = 1234
+        rend.t_stop = 1e-5
+        evaluated = [0]
+
+        def step():
+            with torch.no_grad():
+                out = rend(c2w, K, x_pix, n)[1]
+            evaluated[0] += rend.last_fine_samples
+            return out
+
+        steps = args.config5_steps
+        step()
+        evaluated[0] = 0
+        elapsed, out = time_steps(step, steps, 0, 1, device)
+        assert rend.last_path == "fused" and bool(torch.isfinite(out).all())
+        res[f"sigma_bias_{int(bias)}"] = {
+            "value": round(R * steps / elapsed, 1), "unit": "rays/s", "steps": steps, "warmup": 1,
+            "ms_per_step": round(elapsed / steps * 1e3, 3),
+            "fine_samples_evaluated_fraction": round(evaluated[0] / (steps * R * (args.n_coarse + args.n_fine)), 4)}
+    out = dict(res["sigma_bias_0"])
+    out["workload"] = (f"BASELINE config 4: one {args.frame}x{args.frame} frame ({R} rays) per step x "
+                       f"({args.n_coarse} coarse + {args.n_fine} fine), fine-pass early termination T_stop 1e-5")
+    out["sigma_bias_30"] = res["sigma_bias_30"]
+    return out
+
+
 def fp32_leg(args, net, fused, timer, K, c2w, x_pix, device):
     """The strict-fp32 field (v_mfma_f32_16x16x4_f32) on the headline workload,
     same box and process: a measured anchor for the x3 number."""
@@ -705,8 +766,8 @@ def main():
                     help="field MFMA path: split-fp16 (3 products, fp32 accumulate) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic leg")
-    ap.add_argument("--no-legs", action="store_true", help="skip the config-5 and fp32 legs of the N=1 line")
-    ap.add_argument("--config5-steps", type=int, default=2, help="N=1: timed steps of the config-5 leg")
+    ap.add_argument("--no-legs", action="store_true", help="skip the config-2/4/5 and fp32 legs of the N=1 line")
+    ap.add_argument("--config5-steps", type=int, default=2, help="N=1: timed steps of the config-4 / 5 legs")
     ap.add_argument("--fp32-steps", type=int, default=3, help="N=1: timed steps of the strict-fp32 leg")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dist", action="store_true",
@@ -938,6 +999,8 @@ def main():
         line["config"]["fine_samples_evaluated_fraction"] = round(
             fine_evaluated[0] / (args.steps * R * (args.n_coarse + args.n_fine)), 4)
     if world == 1 and config == 3 and not args.no_legs:
+        line["config2"] = config2_leg(args, net, fused, K, c2w, x_pix, device)
+        line["config4"] = config4_leg(args, net, K, device)
         line["config5"] = config5_leg(args, net, fused, K, device)
         if args.precision == "x3":
             line["fp32"] = fp32_leg(args, net, fused, timer, K, c2w, x_pix, device)
