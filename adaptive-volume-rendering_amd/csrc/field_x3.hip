@@ -229,8 +229,10 @@ __device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const 
       bits[idx >> 5] |= nib << (idx & 31);
     }
   unsigned* mk = a.mask + (((int64_t)layer * gridDim.x + blockIdx.x) * NW + wid) * MW * 64 + lane;
+#ifndef AVR_DIAG_NO_MASK_STORE   // timing-only diagnostic: the mask words are not written
 #pragma unroll
   for (int q = 0; q < MW; ++q) mk[q * 64] = bits[q];
+#endif
 }
 
 // Work split: NW waves (4: one per SIMD; 8: two per SIMD, which doubles the

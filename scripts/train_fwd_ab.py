@@ -3,7 +3,7 @@ forward on the same points, at train.py's fine-pass shape (4 scenes x 512 rays x
 96 samples) on the default_mv.conf field. Not part of the product or the bench.
 
 env: AVR_LIB_PATH (library to load), CONF (default_mv | default), B (points per scene),
-     REPS (timed launches per variant)
+     REPS (timed launches per variant), VARIANTS (comma list of the tags to run)
 """
 import os
 import sys
@@ -65,7 +65,10 @@ def train_bwd():
 
 
 variants = [("infer8", infer, "8"), ("infer4", infer, "4"), ("train", train, "8"), ("train+bwd", train_bwd, "8")]
+want = os.environ.get("VARIANTS")
 for tag, fn, waves in variants:
+    if want and tag not in want.split(","):
+        continue
     os.environ["AVR_X3_WAVES"] = waves
     ms = timed(fn)
     print(f"[{tag}] {conf} SB={SB} B={B}: {ms:.3f} ms  {flops / (ms * 1e-3) / 1e12:.1f} TF/s", flush=True)
