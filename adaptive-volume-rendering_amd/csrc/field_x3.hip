@@ -375,7 +375,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
           __builtin_nontemporal_store(xo, zr + gg);
           __builtin_nontemporal_store(vo, zr + 3 + npe + gg);
         }
-        if (6 + npe + gg < a.zf_ld) __builtin_nontemporal_store(0.f, zr + 6 + npe + gg);
+        for (int k = 6 + npe + gg; k < a.zf_ld; k += NW) __builtin_nontemporal_store(0.f, zr + k);   // sub-lanes gg < NW
       }
     }
     {

@@ -387,3 +387,46 @@ def test_batched_latent_features_and_tables_match_per_scene():
                 assert torch.equal(fast[s], one), (coarse, s)
         finally:
             entry.dims.precision = saved
+
+
+def test_training_forward_stores_z_feature():
+    """avr_field_fwd_points_train's z_feature rows (ABI 9: lin_in's weight-gradient operand, so the backward
+    does not recompute the positional encoding) against the module's z_features (PE / rotation in torch),
+    two scenes, a ragged point count, the padding columns zero, and their max |.|."""
+    from avr import _lib
+    from avr._lib import ViewDesc, call, ptr, stream_of
+    from avr.field import FusedField
+    net = _net(128, 3, 64, (8, 8), sb=2)
+    xyz, vd, _ = _points(2, 333, seed=8)
+    f = FusedField(net, "x3")
+    entry = f.packed(True)
+    dims = entry.dims
+    SB, B = 2, 333
+    H, nb = dims.d_hidden, dims.n_blocks
+    act_n, mask_n = ctypes.c_int64(0), ctypes.c_int64(0)
+    _lib.check(_lib.load().avr_field_train_sizes(ctypes.byref(dims), SB, B, ctypes.byref(act_n),
+                                                 ctypes.byref(mask_n)), "avr_field_train_sizes")
+    out = torch.empty(SB * B, 4, device=DEV)
+    act = torch.empty(act_n.value, device=DEV)
+    mask = torch.empty(max(mask_n.value, 1), device=DEV, dtype=torch.int32)
+    act_max = torch.zeros(2 * nb + 2, device=DEV, dtype=torch.int32)
+    zs = dims.d_in + (-dims.d_in) % 4 + 4                        # two more padding columns than needed
+    zf = torch.full((SB * B, zs), float("nan"), device=DEV)
+    views = (ViewDesc * SB)(*[f.view(s) for s in range(SB)])
+    tables = f.tables_batch(True, SB, fast=True)
+    saved = dims.precision
+    dims.precision = _lib.FIELD_X3
+    try:
+        call("avr_field_fwd_points_train", ctypes.byref(dims), views, SB, ptr(entry.packed), ptr(tables),
+             ptr(xyz.contiguous()), ptr(vd.contiguous()), B, ptr(out), ptr(act), SB * B, ptr(mask), ptr(act_max),
+             ptr(zf), zs, ctypes.c_void_p(act_max.data_ptr() + 4 * (2 * nb + 1)), stream_of(out))
+    finally:
+        dims.precision = saved
+    with torch.no_grad():
+        ref = net.z_features(xyz, vd).float()
+    d_in = dims.d_in
+    assert ref.shape == (SB * B, d_in)
+    np.testing.assert_allclose(zf[:, :d_in].cpu().numpy(), ref.cpu().numpy(), atol=2e-6, rtol=1e-6)
+    assert bool((zf[:, d_in:] == 0).all())
+    zmax = act_max[2 * nb + 1:].view(torch.float32)
+    assert float(zmax) == float(zf[:, :d_in].abs().max())
