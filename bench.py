@@ -569,7 +569,8 @@ def pmc_traffic(args, timeout=240):
     env.setdefault("TMPDIR", "/tmp")
     per = {}
     try:
-        for counters in (["FETCH_SIZE"], ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"]):
+        durs = []
+        for counters in (["FETCH_SIZE", "GRBM_GUI_ACTIVE"], ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"]):
             d = os.path.join(tmp, counters[0])
             cmd = [prof, "--pmc", *counters, "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
                    os.path.abspath(__file__), "--pmc-child", "--precision", args.precision,
@@ -588,6 +589,8 @@ def pmc_traffic(args, timeout=240):
                 for r in rows:
                     if r["Counter_Name"] == c:
                         vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+                        if c == "GRBM_GUI_ACTIVE" and "End_Timestamp" in r:
+                            durs.append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
                 if not vals:
                     return None, f"no {c} rows for the field kernel"
                 per[c] = (sum(vals.values()) / len(vals), len(vals))
@@ -596,8 +599,12 @@ def pmc_traffic(args, timeout=240):
     fetch, n = per["FETCH_SIZE"]
     write, _ = per["WRITE_SIZE"]
     hit, miss = per["TCC_HIT_sum"][0], per["TCC_MISS_sum"][0]
+    # the shader clock the field kernel ran at: GRBM_GUI_ACTIVE (summed over the 8 XCDs) per dispatch time
+    clock = None
+    if durs and per.get("GRBM_GUI_ACTIVE"):
+        clock = per["GRBM_GUI_ACTIVE"][0] / 8.0 / (sum(durs) / len(durs))   # cycles per ns = GHz
     return {"bytes_per_launch": int((2 * fetch + write) * 1024), "fetch_size_kb_raw": fetch, "write_size_kb": write,
-            "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None, "dispatches": n}, "ok"
+            "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None, "dispatches": n, "clock_ghz": clock}, "ok"
 
 
 def time_steps(step, steps, warmup, world, device):
@@ -988,6 +995,13 @@ def main():
             "Infinity-Cache hits")
         line["roofline"]["traffic_over_algorithmic"] = round(pmc["bytes_per_launch"] / alg_bytes, 1)
         line["roofline"]["l2_hit_rate"] = None if pmc["l2_hit_rate"] is None else round(pmc["l2_hit_rate"], 4)
+        if pmc.get("clock_ghz"):
+            # the MFMA peak scales with the clock the board's power limit allows (2.4 GHz nominal)
+            c = pmc["clock_ghz"]
+            line["roofline"]["clock"] = {
+                "ghz": round(c, 3), "peak_at_clock": round(peak * c / 2.4, 1),
+                "frac_at_clock": round(achieved_tflops / (peak * c / 2.4), 4),
+                "source": "the --pmc pass of this run: GRBM_GUI_ACTIVE / 8 XCDs / field dispatch time"}
     else:
         line["roofline"]["traffic_source"] = f"not measured in this run ({pmc_note})"
     # the renderer's HBM-bound kernels (the metric's "achieved HBM GB/s vs roofline"), HIP events per launch,
