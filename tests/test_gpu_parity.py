@@ -481,10 +481,9 @@ def test_field_rays_mode_matches_points_mode(golden, precision):
 @pytest.mark.parametrize("tag", ["c64f32d16", "c128f64d0"])
 def test_volume_renderer_golden(golden, tag, precision):
     """Full VolumeRenderer.forward with the reference's captured noise: coarse
-    rgb <= 1e-4; the inverse-CDF bins of the HIP chain against the reference's
-    own searchsorted result (g5 `idx`); fine rgb / depth <= 1e-4 on every ray
-    whose bins equal the reference's (a bin flip from a ULP-level weight
-    change is the only allowed outlier, and at most 1 % of the bins)."""
+    rgb <= 1e-4; the inverse-CDF bins of the HIP chain equal the reference's
+    own searchsorted result (g5 `idx`) on every ray, and fine rgb / depth are
+    within 1e-4 on every ray."""
     from avr.renderers import VolumeRenderer
     g = golden(f"g5_forward_{tag}.npz")
     net = build_net(g, DEV, precision)
@@ -510,10 +509,15 @@ def test_volume_renderer_golden(golden, tag, precision):
                                     float(g["depth_std"]), u=noise["u"][0], u2=noise["u2"][0],
                                     noise_depth=noise["depth"][0], want_idx=True)
     same = (to_np(idx) == g["idx"][0]).all(-1)
-    assert (to_np(idx) == g["idx"][0]).mean() >= 0.99
     ok = (np.abs(to_np(rgb_f) - g["rgb_fine"]).max(-1) <= 1e-4) & (np.abs(to_np(depth) - g["depth"]) <= 1e-4)
+    print(f"{tag} {precision}: bins equal {(to_np(idx) == g['idx'][0]).mean():.4f}, rays with the reference's "
+          f"bins {same.mean():.4f}, rays within 1e-4 {ok.mean():.4f}")
+    # every ray takes the reference's own bins and lands within 1e-4 (both precisions, both configs: measured
+    # 64 / 64). The bar is strict on purpose: a bin flip here would come from a ULP-level change of the coarse
+    # weights, which the C3 test (test_gpu_scale.py) bounds statistically on 4 096 rays.
+    assert same.all(), np.nonzero(~same)
     assert ok[0][same].all(), np.nonzero(~ok[0] & same)
-    assert ok.mean() >= 0.95, ok.mean()
+    assert ok.all(), ok.mean()
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
