@@ -1,0 +1,58 @@
+"""HIP-graph replay of the inference renderer for fixed shapes (serving).
+
+`VolumeRenderer.forward` on the fused path is a fixed chain of launches (rays + stratified z, coarse field,
+composite, inverse-CDF sampling + merge, fine field, composite + depth) whose host side -- argument packing,
+ctypes calls, tensor allocation -- costs tens of microseconds per launch. For small ray batches that host time
+is a large part of a frame. `GraphedRenderer` captures the chain once into a HIP graph (torch.cuda.CUDAGraph,
+hipGraph on ROCm) and replays it: new cameras / pixels are copied into the captured input buffers, the outputs
+are the captured output buffers.
+
+Noise: with `renderer.seed = None` the reference's draws (torch.rand / randn, renderers.py:14, :41, :45, :63)
+are captured too and advance on every replay like eager calls. With an integer seed the in-kernel Philox draws
+are keyed by the offset the renderer held at capture time, so every replay draws the same noise (eager calls
+advance the offset per call).
+"""
+import torch
+
+__all__ = ["GraphedRenderer"]
+
+
+class GraphedRenderer:
+    """renderer(cam2world, intrinsics, x_pix, net) captured for the shapes of the example inputs.
+
+    __call__(cam2world, intrinsics, x_pix) -> (rgb_coarse, rgb_fine, depth, depth), the captured buffers
+    (overwritten by the next replay; clone to keep). Inference only (no autograd), fused field only.
+    """
+
+    def __init__(self, renderer, net, cam2world, intrinsics, x_pix, warmup=2):
+        if renderer.t_stop is not None:
+            raise ValueError("GraphedRenderer: early termination sizes its launches on the host (t_stop must be None)")
+        self.renderer, self.net = renderer, net
+        self.c2w = cam2world.detach().clone().contiguous()
+        self.K = intrinsics.detach().clone().contiguous()
+        self.x_pix = x_pix.detach().clone().contiguous()
+        stream = torch.cuda.Stream(device=self.x_pix.device)
+        stream.wait_stream(torch.cuda.current_stream())
+        with torch.no_grad(), torch.cuda.stream(stream):
+            # warm-up outside the capture: packs the weights, builds the lin_z tables, caches the views, sets the
+            # kernels' LDS attributes -- everything that touches the host or allocates outside the graph pool
+            for _ in range(warmup):
+                renderer(self.c2w, self.K, self.x_pix, net)
+            if renderer.last_path != "fused":
+                raise ValueError("GraphedRenderer: the net must take the fused field path (net.can_fuse)")
+        torch.cuda.current_stream().wait_stream(stream)
+        self.offset = renderer._offset
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self.out = renderer(self.c2w, self.K, self.x_pix, net)
+        renderer._offset = self.offset   # the captured launches keep the offset they were recorded with
+
+    def __call__(self, cam2world=None, intrinsics=None, x_pix=None):
+        if cam2world is not None:
+            self.c2w.copy_(cam2world)
+        if intrinsics is not None:
+            self.K.copy_(intrinsics)
+        if x_pix is not None:
+            self.x_pix.copy_(x_pix)
+        self.graph.replay()
+        return self.out
