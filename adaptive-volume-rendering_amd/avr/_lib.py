@@ -14,12 +14,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
 i64 = ctypes.c_int64
 u64 = ctypes.c_uint64
+c_uint32 = ctypes.c_uint32
 c_int = ctypes.c_int
 c_float = ctypes.c_float
 
@@ -111,6 +112,7 @@ _SIGS = {
     "avr_latent_features": [ctypes.POINTER(ViewDesc), c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
     "avr_latent_features_batch": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
     "avr_stream_copy": [c_void_p, c_void_p, i64, c_void_p],
+    "avr_stream_fill": [c_void_p, i64, c_uint32, c_void_p],
 }
 EXPORTED = ("avr_version", "avr_last_error_string", "avr_device_count") + tuple(_SIGS)
 

@@ -459,3 +459,11 @@ def stream_copy(src, dst):
         raise _lib.AVRError("stream_copy: size mismatch")
     call("avr_stream_copy", ptr(src), ptr(dst), nb, stream_of(src))
     return dst
+
+
+def stream_fill(dst, word):
+    """Every 32-bit word of dst <- word (16-B aligned): the write-only yardstick
+    bench.py reports store-dominated kernels against (avr_stream_fill)."""
+    require_device(dst)
+    call("avr_stream_fill", ptr(dst), dst.numel() * dst.element_size(), int(word) & 0xFFFFFFFF, stream_of(dst))
+    return dst

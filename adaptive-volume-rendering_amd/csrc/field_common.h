@@ -7,7 +7,6 @@
 
 namespace avr {
 
-typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 constexpr int kFieldWaves = 4;   // 256-thread workgroups, one wave per SIMD

@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(256) sample_coarse_kernel(float near_, float f
   }
   float* zr = z + r * n + 4 * q;
   if ((n & 3) == 0) {
-    *reinterpret_cast<float4*>(zr) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<floatx4*>(zr) = floatx4{o[0], o[1], o[2], o[3]};   // one 16-B store (not x3 + x1)
   } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -109,14 +109,91 @@ __global__ void __launch_bounds__(256) sample_coarse_rays_kernel(const float* __
 // launch, plus each ray's depth row for the composite epilogue. A workgroup
 // owns kRaysPerBlock (64) consecutive rays: wave 0 builds ro, rd with one lane
 // per ray (and, if asked, row 2 of inverse(cam2world) in fp64: depth = -(row .
-// [x, 1]), utils.py:358-361) while waves 1-3 write the rays' z in 4-sample
+// [x, 1]), utils.py:358-361) while waves 1-7 write the rays' z in 4-sample
 // quads, consecutive threads on consecutive quads (coalesced 16-B stores): z
 // does not depend on the geometry, so the fp64 latency of wave 0 overlaps the
 // z stores instead of preceding them.
 constexpr int kRaysPerBlock = 64;
+#ifndef AVR_RAYS_THREADS
+#define AVR_RAYS_THREADS 512
+#endif
+constexpr int kRaysThreads = AVR_RAYS_THREADS;   // wave 0 geometry + 7 z waves (13.0-13.5 vs 13.9 us with 3)
+
+struct CoarseQuads {
+  float near_, span, inv_n;
+  int n, nq, lg_nq;
+  bool tab;
+  const float* noise;
+  uint64_t seed, offset;
+  const int64_t* ray_ids;
+  float* z;
+  const float* base_tab;
+};
+
+// the 4 z of quad `it` (ray r0 + it / nq, samples 4q..4q+3)
+template <bool POW2>
+__device__ __forceinline__ void coarse_quad(const CoarseQuads& c, int64_t r0, int it, int64_t& ray, int& q,
+                                            float (&o)[4]) {
+  const int rl = POW2 && c.n >= 4 ? it >> c.lg_nq : it / c.nq;
+  q = it - rl * c.nq;
+  ray = r0 + rl;
+  float u[4];
+  if (c.noise) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] = 4 * q + k < c.n ? c.noise[ray * c.n + 4 * q + k] : 0.f;
+  } else {
+    const uint64_t key = c.offset + (uint64_t)(c.ray_ids ? c.ray_ids[ray] : ray);
+    const float4 v = philox_uniform4(c.seed, key, (uint32_t)q, kStreamCoarse);
+    u[0] = v.x; u[1] = v.y; u[2] = v.z; u[3] = v.w;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int s = 4 * q + k;
+    o[k] = c.tab ? fadd(c.base_tab[s < c.n ? s : 0], div_count<POW2>(fmul(u[k], c.span), (float)c.n, c.inv_n))
+                 : coarse_z<POW2>(c.near_, c.span, s, c.n, u[k], c.inv_n);
+  }
+}
+
+template <bool V4>
+__device__ __forceinline__ void store_quad(const CoarseQuads& c, int64_t ray, int q, const float (&o)[4]) {
+  float* zr = c.z + ray * c.n + 4 * q;
+  if constexpr (V4) {
+    *reinterpret_cast<floatx4*>(zr) = floatx4{o[0], o[1], o[2], o[3]};
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (4 * q + k < c.n) zr[k] = o[k];
+  }
+}
+
+// quads it0, it0 + stride, ... < items; AVR_COARSE_ILP quads per pass (independent Philox chains in flight)
+#ifndef AVR_COARSE_ILP
+#define AVR_COARSE_ILP 1
+#endif
+template <bool POW2, bool V4>
+__device__ __forceinline__ void coarse_quad_loop(const CoarseQuads& c, int64_t r0, int it0, int stride, int items) {
+  constexpr int P = AVR_COARSE_ILP;
+  int it = it0;
+  for (; it + (P - 1) * stride < items; it += P * stride) {
+    int64_t ray[P];
+    int q[P];
+    float o[P][4];
+#pragma unroll
+    for (int p = 0; p < P; ++p) coarse_quad<POW2>(c, r0, it + p * stride, ray[p], q[p], o[p]);
+#pragma unroll
+    for (int p = 0; p < P; ++p) store_quad<V4>(c, ray[p], q[p], o[p]);
+  }
+  for (; it < items; it += stride) {
+    int64_t ray;
+    int q;
+    float o[4];
+    coarse_quad<POW2>(c, r0, it, ray, q, o);
+    store_quad<V4>(c, ray, q, o);
+  }
+}
 
 template <bool POW2>
-__global__ void __launch_bounds__(256) rays_coarse_kernel(
+__global__ void __launch_bounds__(kRaysThreads) rays_coarse_kernel(
     const float* __restrict__ x_pix, const float* __restrict__ K, const float* __restrict__ c2w, int64_t sb_stride,
     int64_t ray_stride, int64_t n_sb, int64_t n_rays, float near_, float far_, int n, const float* __restrict__ noise,
     uint64_t seed, uint64_t offset, const int64_t* __restrict__ ray_ids, float* __restrict__ ro,
@@ -135,6 +212,9 @@ __global__ void __launch_bounds__(256) rays_coarse_kernel(
     __syncthreads();   // base_tab
   }
   if (threadIdx.x < 64) {   // wave 0: the rays' geometry, one lane per ray
+#ifdef AVR_DIAG_NO_GEOM
+    return;
+#endif
     if (threadIdx.x >= kRaysPerBlock || r0 + threadIdx.x >= total) return;
     const int64_t i = r0 + threadIdx.x;
     const int64_t sb = i / n_rays, r = i - sb * n_rays;
@@ -177,34 +257,11 @@ __global__ void __launch_bounds__(256) rays_coarse_kernel(
   const int lg_nq = POW2 && n >= 4 ? __builtin_ctz((unsigned)nq) : 0;   // nq a power of two too
   const int64_t nr_blk = total - r0 < kRaysPerBlock ? total - r0 : kRaysPerBlock;
   const int items = (int)nr_blk * nq;
-  for (int it = threadIdx.x - 64; it < items; it += blockDim.x - 64) {   // waves 1-3: z
-    const int rl = POW2 && n >= 4 ? it >> lg_nq : it / nq, q = it - rl * nq;
-    const int64_t ray = r0 + rl;
-    float u[4];
-    if (noise) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) u[k] = 4 * q + k < n ? noise[ray * n + 4 * q + k] : 0.f;
-    } else {
-      const uint64_t key = offset + (uint64_t)(ray_ids ? ray_ids[ray] : ray);
-      const float4 v = philox_uniform4(seed, key, (uint32_t)q, kStreamCoarse);
-      u[0] = v.x; u[1] = v.y; u[2] = v.z; u[3] = v.w;
-    }
-    float o[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int s = 4 * q + k;
-      o[k] = tab ? fadd(base_tab[s < n ? s : 0], div_count<POW2>(fmul(u[k], span), (float)n, inv_n))
-                 : coarse_z<POW2>(near_, span, s, n, u[k], inv_n);
-    }
-    float* zr = z + ray * n + 4 * q;
-    if ((n & 3) == 0) {
-      *reinterpret_cast<float4*>(zr) = make_float4(o[0], o[1], o[2], o[3]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (4 * q + k < n) zr[k] = o[k];
-    }
-  }
+  const CoarseQuads cq{near_, span, inv_n, n, nq, lg_nq, tab, noise, seed, offset, ray_ids, z, base_tab};
+  // waves 1-7: z. The whole-quad store is chosen once for the loop, not per quad (a per-quad branch let
+  // the compiler merge the 16-B store with the ragged path's scalar stores into x3 + x1 stores)
+  if ((n & 3) == 0) coarse_quad_loop<POW2, true>(cq, r0, threadIdx.x - 64, blockDim.x - 64, items);
+  else coarse_quad_loop<POW2, false>(cq, r0, threadIdx.x - 64, blockDim.x - 64, items);
 }
 
 // torch-CPU fp32 row sum (ATen vectorised reduction): four 8-lane accumulators
@@ -586,7 +643,7 @@ extern "C" int avr_rays_sample_coarse(const float* x_pix, const float* K, const 
   const int64_t blocks = (total + kRaysPerBlock - 1) / kRaysPerBlock;
   AVR_REQUIRE(blocks < (1ll << 31), "avr_rays_sample_coarse: too many rays");
   auto* kern = (n_samples & (n_samples - 1)) == 0 ? rays_coarse_kernel<true> : rays_coarse_kernel<false>;
-  kern<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(x_pix, K, c2w, c2w_sb_stride, c2w_ray_stride, n_sb, n_rays,
+  kern<<<(unsigned)blocks, kRaysThreads, 0, as_stream(stream)>>>(x_pix, K, c2w, c2w_sb_stride, c2w_ray_stride, n_sb, n_rays,
                                                         near_, far_, n_samples, noise, seed, offset, ray_ids, ro, rd,
                                                         depth_row, z);
   return check_launch("rays_coarse_kernel");

@@ -124,38 +124,47 @@ class HbmKernelTimer:
         def timed(*a, **k):
             out = orig(*a, **k)
             if self.on:
-                nb, what = nbytes(a, k, out)
+                nb, nw, what = nbytes(a, k, out)
                 label = f"{kernel} ({what})" if what else kernel
-                self.calls.setdefault(label, (orig, a, k, nb))
+                self.calls.setdefault(label, (orig, a, k, (nb, nw)))
             return out
 
         setattr(self.ops, name, timed)
 
     def install(self):
+        # each returns (bytes, of which written, label)
         def composite_bytes(a, k, out):
             R, N = a[0].shape
             ww = out[2] is not None
-            return R * (N * (4 + 16 + (4 if ww else 0)) + 16), f"N={N}, weights {'stored' if ww else 'not stored'}"
+            return (R * (N * (4 + 16 + (4 if ww else 0)) + 16), R * ((4 * N if ww else 0) + 16),
+                    f"N={N}, weights {'stored' if ww else 'not stored'}")
 
         def sample_fine_bytes(a, k, out):
             w, zc = a[0], a[1]
-            return w.numel() * 4 + zc.numel() * 4 + out[0].numel() * 4, f"Nc={zc.shape[1]}, out {out[0].shape[1]}"
+            nw = out[0].numel() * 4
+            return w.numel() * 4 + zc.numel() * 4 + nw, nw, f"Nc={zc.shape[1]}, out {out[0].shape[1]}"
 
         def rays_coarse_bytes(a, k, out):
             R, N = out[2].shape
-            return R * (8 + 24 + 4 * N + (32 if out[3] is not None else 0)), f"N={N}, depth rows"
+            nw = R * (24 + 4 * N + (32 if out[3] is not None else 0))
+            return R * 8 + nw, nw, f"N={N}, depth rows"
 
         def composite_depth_bytes(a, k, out):
             R, N = a[0].shape
-            return R * (N * (4 + 16) + 16 + 24 + 32 + 4), f"N={N}, + depth"
+            return R * (N * (4 + 16) + 16 + 24 + 32 + 4), R * 20, f"N={N}, + depth"
+
+        def per_point(read, write):
+            return lambda a, k, out: (a[0].shape[0] * a[0].shape[1] * (read + write),
+                                      a[0].shape[0] * a[0].shape[1] * write, "")
 
         self._wrap("rays_sample_coarse", "rays_coarse_kernel", rays_coarse_bytes)
         self._wrap("composite_depth", "composite_fwd_kernel", composite_depth_bytes)
-        self._wrap("world_rays", "world_rays_kernel", lambda a, k, out: (a[0].shape[0] * a[0].shape[1] * 32, ""))
-        self._wrap("sample_coarse", "sample_coarse_kernel", lambda a, k, out: (out.numel() * 4, f"N={out.shape[1]}"))
+        self._wrap("world_rays", "world_rays_kernel", per_point(8, 24))
+        self._wrap("sample_coarse", "sample_coarse_kernel",
+                   lambda a, k, out: (out.numel() * 4, out.numel() * 4, f"N={out.shape[1]}"))
         self._wrap("composite_fwd", "composite_fwd_kernel", composite_bytes)
         self._wrap("sample_fine", "sample_fine_kernel", sample_fine_bytes)
-        self._wrap("depth_from_world_fwd", "depth_kernel", lambda a, k, out: (a[0].shape[0] * a[0].shape[1] * 32, ""))
+        self._wrap("depth_from_world_fwd", "depth_kernel", per_point(28, 4))
 
     @staticmethod
     def _input_sets(a, k, min_bytes, max_sets):
@@ -224,42 +233,59 @@ class HbmKernelTimer:
         return us, n_sets, in_b
 
     def report(self, reps=20, achievable=None, min_bytes=1 << 30):
+        """achievable: (copy GB/s, fill GB/s) on this box. A kernel's achievable time is its read bytes at
+        the copy's read rate plus its written bytes at the fill's write rate (the copy's time split by the
+        fill's: a copy of N bytes takes N/read + N/write), frac_of_achievable = that time / measured."""
         res = []
-        for label, (fn, a, k, nb) in self.calls.items():
+        for label, (fn, a, k, (nb, nw)) in self.calls.items():
             us, n_sets, in_b = self._replay_us(fn, a, k, reps, min_bytes)
             gbs = nb / (us * 1e-6) / 1e9
             res.append({"kernel": label, "avg_us": round(us, 2), "bytes_per_launch": int(nb),
+                        "written_bytes_per_launch": int(nw),
                         "achieved_GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
                         "input_sets": n_sets, "input_bytes_rotated": int(n_sets * in_b)})
             if achievable:
-                res[-1]["frac_of_achievable"] = round(gbs / achievable, 4)
+                copy_gbs, fill_gbs = achievable
+                sec_per_read_byte = max(2.0 / copy_gbs - 1.0 / fill_gbs, 1.0 / HBM_PEAK_GBS) / 1e9
+                floor_us = ((nb - nw) * sec_per_read_byte + nw / fill_gbs / 1e9) * 1e6
+                res[-1]["achievable_us"] = round(floor_us, 2)
+                res[-1]["frac_of_achievable"] = round(floor_us / us, 4)
         return res
 
 
 def achievable_hbm_gbs(device, nbytes=1 << 31, reps=5):
-    """the HBM bandwidth a streaming copy reaches on this box --
-    avr_stream_copy (16 B per lane, 4 loads in flight per lane; the kind of
-    float4 copy MI355X_MICROARCH.md measures at 6.29 TB/s) over 2 GiB buffers
-    (8x the Infinity Cache), read + write bytes / time, best of `reps` launches
-    timed one by one with HIP events."""
+    """the HBM bandwidth streaming kernels reach on this box, over
+    2 GiB buffers (8x the Infinity Cache), best of `reps` launches timed one by
+    one with HIP events: avr_stream_copy (16 B per lane, 4 loads in flight per
+    lane; the kind of float4 copy MI355X_MICROARCH.md measures at 6.29 TB/s),
+    read + write bytes / time, and avr_stream_fill (the same stores, no loads),
+    written bytes / time -- the ceiling of store-dominated kernels.
+    Returns (copy GB/s, fill GB/s)."""
     import avr
     src = torch.empty(nbytes // 4, device=device, dtype=torch.float32).fill_(1.0)
     dst = torch.empty_like(src)
-    avr.ops.stream_copy(src, dst)
-    torch.cuda.synchronize()
-    best = None
-    for _ in range(reps):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        avr.ops.stream_copy(src, dst)
-        e.record()
-        e.synchronize()
-        ms = s.elapsed_time(e)
-        best = ms if best is None else min(best, ms)
+
+    def best_ms(fn):
+        fn()
+        torch.cuda.synchronize()
+        best = None
+        for _ in range(reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            e.record()
+            e.synchronize()
+            ms = s.elapsed_time(e)
+            best = ms if best is None else min(best, ms)
+        return best
+
+    copy_ms = best_ms(lambda: avr.ops.stream_copy(src, dst))
     assert bool((dst[:: 1 << 20] == 1.0).all())
+    fill_ms = best_ms(lambda: avr.ops.stream_fill(dst, 0x40000000))   # 2.0f
+    assert bool((dst[:: 1 << 20] == 2.0).all())
     del src, dst
     torch.cuda.empty_cache()
-    return 2 * nbytes / (best * 1e-3) / 1e9
+    return 2 * nbytes / (copy_ms * 1e-3) / 1e9, nbytes / (fill_ms * 1e-3) / 1e9
 
 
 def cpu_share():
@@ -1007,7 +1033,8 @@ def main():
     # the renderer's HBM-bound kernels (the metric's "achieved HBM GB/s vs roofline"), HIP events per launch,
     # against the 8 TB/s peak and against what a streaming copy reaches on this box
     ach = achievable_hbm_gbs(device)
-    line["hbm_achievable_GBs"] = round(ach, 1)
+    line["hbm_achievable_GBs"] = round(ach[0], 1)
+    line["hbm_write_achievable_GBs"] = round(ach[1], 1)
     line["hbm_kernels"] = hbm.report(achievable=ach)
     if config == 4:
         line["config"]["fine_samples_evaluated_fraction"] = round(

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 9
+#define AVR_ABI_VERSION 10
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -376,6 +376,12 @@ int avr_raymarch(const avr_view_desc* view, const float* gate_table, const float
  * n_bytes a multiple of 16): the achievable-HBM yardstick bench.py reports
  * every renderer kernel against. Not on the rendering path.      */
 int avr_stream_copy(const void* src, void* dst, int64_t n_bytes, void* stream);
+
+/* Streaming device fill: every 32-bit word of dst[0, n_bytes) = word (16-B
+ * aligned, n_bytes a multiple of 16): the write-only yardstick (the ceiling
+ * of store-dominated kernels such as the stratified sampler). Not on the
+ * rendering path (ABI 10).                                                    */
+int avr_stream_fill(void* dst, int64_t n_bytes, uint32_t word, void* stream);
 
 #ifdef __cplusplus
 }

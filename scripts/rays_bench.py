@@ -1,6 +1,6 @@
 """Isolated timing of avr_rays_sample_coarse at the C3 shape (65536 rays x 128,
 one pose expanded per ray as in the bench): with and without the fp64 depth
-rows, and avr_sample_coarse alone (z only). Diagnostic only."""
+rows, and avr_sample_coarse alone (z only), and a plain fill of the z bytes (the store floor). Diagnostic only."""
 import os
 import sys
 
@@ -35,6 +35,9 @@ def main():
         print(f"rays_sample_coarse depth_row={drow}: {us:.2f} us", flush=True)
     us = timed(lambda: ops.sample_coarse(0.8, 1.8, R, N, dev, seed=3), reps)
     print(f"sample_coarse (z only): {us:.2f} us", flush=True)
+    zbuf = torch.empty(R * N, device=dev)
+    us = timed(lambda: ops.stream_fill(zbuf, 0), reps)
+    print(f"stream_fill of the z bytes: {us:.2f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -184,6 +184,9 @@ int main(void) {
   expect("copy odd size", avr_stream_copy(buf, buf + 8, 15, NULL), AVR_E_INVALID);
   expect("copy null", avr_stream_copy(NULL, buf, 16, NULL), AVR_E_INVALID);
   expect("copy empty", avr_stream_copy(NULL, NULL, 0, NULL), AVR_OK);
+  expect("fill odd size", avr_stream_fill(buf, 15, 0u, NULL), AVR_E_INVALID);
+  expect("fill null", avr_stream_fill(NULL, 16, 0u, NULL), AVR_E_INVALID);
+  expect("fill empty", avr_stream_fill(NULL, 0, 0u, NULL), AVR_OK);
 
   printf("abi_check: %d failure(s)\n", failures);
   return failures;
