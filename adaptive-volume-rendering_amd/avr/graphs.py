@@ -11,6 +11,13 @@ Noise: with `renderer.seed = None` the reference's draws (torch.rand / randn, re
 are captured too and advance on every replay like eager calls. With an integer seed the in-kernel Philox draws
 are keyed by the offset the renderer held at capture time, so every replay draws the same noise (eager calls
 advance the offset per call).
+
+State: the captured launches read the packed weights, lin_z tables and source-view descriptors the renderer
+built from the net at capture time. Every call checks the tensors those come from for an in-place update (the
+MLPs' parameters and buffers: an optimizer step, load_state_dict) or a new tensor (the encoder's latent, the
+source poses / focal / principal point: net.encode() of new images) and captures the chain again when one
+changed, so a replay never renders with stale weights or views (a few microseconds per call). Replacing a
+Parameter object itself is not seen: call refresh() after that.
 """
 import torch
 
@@ -28,9 +35,41 @@ class GraphedRenderer:
         if renderer.t_stop is not None:
             raise ValueError("GraphedRenderer: early termination sizes its launches on the host (t_stop must be None)")
         self.renderer, self.net = renderer, net
+        self.warmup = warmup
         self.c2w = cam2world.detach().clone().contiguous()
         self.K = intrinsics.detach().clone().contiguous()
         self.x_pix = x_pix.detach().clone().contiguous()
+        self.captures = 0
+        self._capture()
+
+    def _params(self):
+        """The MLPs' parameters and buffers: updated in place (optimizer steps, load_state_dict), so their
+        versions are compared; the Parameter objects are collected once per capture."""
+        ts = []
+        for mlp in (getattr(self.net, "mlp_coarse", None), getattr(self.net, "mlp_fine", None)):
+            if mlp is not None:
+                ts += list(mlp.parameters()) + list(mlp.buffers())
+        return ts
+
+    def _views(self):
+        """The source-view state net.encode() replaces: latent, latent scaling, poses, focal, principal point."""
+        enc = getattr(self.net, "encoder", None)
+        return [getattr(enc, "latent", None), getattr(enc, "latent_scaling", None)] + \
+               [getattr(self.net, a, None) for a in ("poses", "focal", "c", "image_shape")]
+
+    def _stale(self):
+        # held references: no address is reused while compared
+        return any(t._version != v for t, v in self._held) or \
+            any(a is not b for a, b in zip(self._views(), self._held_views))
+
+    def refresh(self):
+        """Capture again (after replacing a Parameter object of the net, which the per-call check does not see)."""
+        self._capture()
+
+    def _capture(self):
+        renderer, net = self.renderer, self.net
+        warmup = self.warmup
+        self.graph = self.out = None
         stream = torch.cuda.Stream(device=self.x_pix.device)
         stream.wait_stream(torch.cuda.current_stream())
         with torch.no_grad(), torch.cuda.stream(stream):
@@ -46,6 +85,10 @@ class GraphedRenderer:
         with torch.no_grad(), torch.cuda.graph(self.graph):
             self.out = renderer(self.c2w, self.K, self.x_pix, net)
         renderer._offset = self.offset   # the captured launches keep the offset they were recorded with
+        views = self._views()
+        self._held_views = views
+        self._held = [(t, t._version) for t in self._params() + views if isinstance(t, torch.Tensor)]
+        self.captures += 1
 
     def __call__(self, cam2world=None, intrinsics=None, x_pix=None):
         if cam2world is not None:
@@ -54,5 +97,7 @@ class GraphedRenderer:
             self.K.copy_(intrinsics)
         if x_pix is not None:
             self.x_pix.copy_(x_pix)
+        if self._stale():
+            self._capture()
         self.graph.replay()
         return self.out

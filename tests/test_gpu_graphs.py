@@ -47,3 +47,35 @@ def test_graph_replay_torch_draws_advance():
     assert all(bool(torch.isfinite(t).all()) for t in a + b)
     assert not torch.equal(a[1], b[1])          # new draws on every replay, as eager calls
     assert float((a[0] - b[0]).abs().mean()) < 0.05   # same scene: the coarse rgb moves by sampling noise only
+
+
+def test_graph_recaptures_after_state_change():
+    """An in-place weight update (an optimizer step) or a new latent (net.encode of new images) makes the next
+    call capture the chain again, so the replay matches the eager renderer on the new state bit for bit."""
+    from avr.graphs import GraphedRenderer
+    net, rend, c2w, K, x_pix = _scene(300, 5)
+    rend.seed = 11
+    gr = GraphedRenderer(rend, net, c2w, K, x_pix)
+    gr()
+    gr()
+    assert gr.captures == 1
+
+    def check():
+        got = [t.clone() for t in gr()]
+        rend._offset = gr.offset
+        with torch.no_grad():
+            want = rend(c2w, K, x_pix, net)
+        for a, b in zip(got, want):
+            assert torch.equal(a, b)
+        return got
+
+    before = [t.clone() for t in gr()]
+    with torch.no_grad():
+        net.mlp_fine.lin_out.bias.add_(0.25)
+    after = check()
+    assert gr.captures == 2 and not torch.equal(before[1], after[1])
+    net.encoder.set_latent(net.encoder.latent * 1.5)
+    check()
+    assert gr.captures == 3
+    gr()
+    assert gr.captures == 3

@@ -1,0 +1,45 @@
+"""GraphedRenderer's state check (host logic, no GPU): in-place parameter updates and a new latent / source
+view mark the captured graph stale; an unchanged net does not."""
+import warnings
+
+import torch
+
+
+def _graphed_state():
+    from avr.conf import default_conf
+    from avr.graphs import GraphedRenderer
+    from avr.models import NewPixelNeRFNet
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")   # random-init encoder (no pretrained weights offline)
+        net = NewPixelNeRFNet(default_conf()["model"]).eval()
+    net.encoder.set_latent(torch.randn(1, net.d_latent, 8, 8))
+    net.poses, net.focal = torch.zeros(1, 3, 4), torch.ones(1, 2)
+    net.c, net.image_shape = torch.ones(1, 2), torch.ones(2)
+    g = GraphedRenderer.__new__(GraphedRenderer)   # the check alone: no capture
+    g.net = net
+
+    def hold():
+        views = g._views()
+        g._held_views = views
+        g._held = [(t, t._version) for t in g._params() + views if isinstance(t, torch.Tensor)]
+    hold()
+    return g, net, hold
+
+
+def test_state_check_sees_updates():
+    g, net, hold = _graphed_state()
+    assert not g._stale()
+    with torch.no_grad():
+        net.mlp_fine.lin_out.bias.add_(1.0)        # optimizer-style in-place step
+    assert g._stale()
+    hold()
+    net.load_state_dict(net.state_dict())           # copies in place
+    assert g._stale()
+    hold()
+    net.encoder.set_latent(net.encoder.latent * 2)  # net.encode() of new images
+    assert g._stale()
+    hold()
+    net.poses = net.poses.clone()
+    assert g._stale()
+    hold()
+    assert not g._stale()
