@@ -21,6 +21,8 @@ Parameter object itself is not seen: call refresh() after that.
 """
 import torch
 
+from . import anomaly
+
 __all__ = ["GraphedRenderer"]
 
 
@@ -100,4 +102,6 @@ class GraphedRenderer:
         if self._stale():
             self._capture()
         self.graph.replay()
+        if anomaly.is_enabled():   # the captured launches were not checked at capture time (avr/anomaly.py)
+            anomaly.check_outputs("GraphedRenderer replay", self.out)
         return self.out

@@ -79,3 +79,20 @@ def test_graph_recaptures_after_state_change():
     assert gr.captures == 3
     gr()
     assert gr.captures == 3
+
+
+def test_graph_capture_and_replay_under_anomaly_mode():
+    """torch anomaly mode (train.py --anomaly_detection) on: the warm-up calls are checked op by op, the capture
+    skips the checks (a capture cannot synchronise), every replay checks its outputs; a clean scene raises
+    nothing and the replay still equals the eager call."""
+    from avr.graphs import GraphedRenderer
+    net, rend, c2w, K, x_pix = _scene(300, 6)
+    rend.seed = 5
+    with torch.autograd.set_detect_anomaly(True):
+        gr = GraphedRenderer(rend, net, c2w, K, x_pix)
+        got = [t.clone() for t in gr()]
+        rend._offset = gr.offset
+        with torch.no_grad():
+            want = rend(c2w, K, x_pix, net)
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
