@@ -78,7 +78,10 @@ def fused_eligible(net, multiview=False):
         if multiview:
             mlps = [net.mlp_coarse] + ([net.mlp_fine] if net.mlp_fine is not None else [])
             if not (ns > 1 and getattr(net, "field_precision", "x3") == "x3"
-                    and all(m.combine_layer < m.n_blocks and m.combine_type in ("average", "max") for m in mlps)):
+                    and all(1 <= m.combine_layer < m.n_blocks and m.combine_type in ("average", "max")
+                            for m in mlps)):
+                # combine_layer 0 (views combined right after lin_in, no lin_z): module path -- the split
+                # launch's first half needs at least one block (avr_field_fwd_points_split, b_end > 0)
                 return False
         elif ns != 1:
             return False
@@ -154,6 +157,28 @@ class FusedField:
         self._packed = {}     # coarse(bool) -> (key, _Packed)
         self._view_cache = {}
         self._latent_cache = {}   # per latent version: channels-last copies, max |latent| (both MLPs share them)
+
+    def invalidate(self):
+        """Drop every cached blob, table and view descriptor (avr.parallel.broadcast_scene calls it after
+        writing a scene into the net; the (data_ptr, _version) keys would catch that too)."""
+        self._packed.clear()
+        self._view_cache.clear()
+        self._latent_cache.clear()
+
+    def cache_tensors(self):
+        """Every device buffer the caches hold (packed blobs, backward blobs, lin_z tables, batched tables):
+        what a captured HIP graph reads (avr.graphs.GraphedRenderer keeps references to them, so an eager call
+        that replaces a cache entry cannot free memory a replay still reads)."""
+        out = []
+        for _, entry in self._packed.values():
+            if entry is None:
+                continue
+            out.append(entry.packed)
+            if getattr(entry, "bwd", None) is not None:
+                out.append(entry.bwd)
+            out += [hit[1] for hit in entry.tables.values()]
+            out += [hit[1] for hit in entry.__dict__.get("batch_tables", {}).values()]
+        return out
 
     def _latent_cached(self, what, latent, make):
         key = (latent.data_ptr(), latent._version, tuple(latent.shape))
@@ -385,23 +410,28 @@ class FusedField:
         tables = self.tables_batch(coarse, K)
         h = torch.empty(K * B, H, device=dev, dtype=F32)
         out = torch.empty(SB, B, 4, device=dev, dtype=F32)
-        entry.dims.precision = _lib.FIELD_X3
-        for g0 in range(0, K, _lib.AVR_MAX_SCENES):
-            n = min(_lib.AVR_MAX_SCENES, K - g0)
-            views = (ViewDesc * n)(*[self.view(k, NS) for k in range(g0, g0 + n)])
-            call("avr_field_fwd_points_split", ctypes.byref(entry.dims), views, n, ptr(entry.packed), ptr(tables[g0]),
-                 ptr(p[g0]), ptr(v[g0]), B, 0, cl, None, ptr(h[g0 * B]), None, stream_of(p))
-        hc = combine_interleaved(h, (NS, B), mlp.combine_type).reshape(SB * B, H).contiguous()
-        for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
-            n = min(_lib.AVR_MAX_SCENES, SB - g0)
-            views = (ViewDesc * n)(*[self.view(s * NS, NS) for s in range(g0, g0 + n)])
-            call("avr_field_fwd_points_split", ctypes.byref(entry.dims), views, n, ptr(entry.packed), ptr(tables[0]),
-                 None, None, B, cl, nb, ptr(hc[g0 * B]), None, ptr(out[g0]), stream_of(p))
+        with _precision(dims, _lib.FIELD_X3):
+            for g0 in range(0, K, _lib.AVR_MAX_SCENES):
+                n = min(_lib.AVR_MAX_SCENES, K - g0)
+                views = (ViewDesc * n)(*[self.view(k, NS) for k in range(g0, g0 + n)])
+                call("avr_field_fwd_points_split", ctypes.byref(entry.dims), views, n, ptr(entry.packed),
+                     ptr(tables[g0]), ptr(p[g0]), ptr(v[g0]), B, 0, cl, None, ptr(h[g0 * B]), None, stream_of(p))
+            hc = combine_interleaved(h, (NS, B), mlp.combine_type).reshape(SB * B, H).contiguous()
+            for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
+                n = min(_lib.AVR_MAX_SCENES, SB - g0)
+                views = (ViewDesc * n)(*[self.view(s * NS, NS) for s in range(g0, g0 + n)])
+                call("avr_field_fwd_points_split", ctypes.byref(entry.dims), views, n, ptr(entry.packed),
+                     ptr(tables[0]), None, None, B, cl, nb, ptr(hc[g0 * B]), None, ptr(out[g0]), stream_of(p))
         return out
 
     def forward_points(self, xyz, viewdirs, coarse):
         """The rf(xyz (SB,B,3), viewdirs, coarse) protocol -> (SB, B, 4)."""
         if getattr(self.net, "num_views_per_obj", 1) > 1:
+            # NS > 1 runs on the x3 split launches only: another precision or an ineligible combine must not be
+            # served silently at x3
+            if self.precision != "x3" or not fused_eligible(self.net, multiview=True):
+                raise _lib.AVRError("FusedField.forward_points: NS > 1 source views need precision 'x3' and an "
+                                    "eligible combine (1 <= combine_layer < n_blocks); use the module path")
             return self.forward_points_multiview(xyz, viewdirs, coarse)
         SB, B, _ = xyz.shape
         out = torch.empty(SB, B, 4, device=xyz.device, dtype=F32)

@@ -16,8 +16,11 @@ State: the captured launches read the packed weights, lin_z tables and source-vi
 built from the net at capture time. Every call checks the tensors those come from for an in-place update (the
 MLPs' parameters and buffers: an optimizer step, load_state_dict) or a new tensor (the encoder's latent, the
 source poses / focal / principal point: net.encode() of new images) and captures the chain again when one
-changed, so a replay never renders with stale weights or views (a few microseconds per call). Replacing a
-Parameter object itself is not seen: call refresh() after that.
+changed, so a replay never renders with stale weights or views (a few microseconds per call). A change of
+net.field_precision captures again too. The packed weights and lin_z tables the captured launches read are
+referenced by the GraphedRenderer, so an eager call that replaces those cache entries (another scene count or
+precision) cannot free memory a replay reads. Replacing a Parameter object itself is not seen: call refresh()
+after that. Warm-ups and re-captures leave the renderer's Philox offset where it was.
 """
 import torch
 
@@ -62,7 +65,8 @@ class GraphedRenderer:
     def _stale(self):
         # held references: no address is reused while compared
         return any(t._version != v for t, v in self._held) or \
-            any(a is not b for a, b in zip(self._views(), self._held_views))
+            any(a is not b for a, b in zip(self._views(), self._held_views)) or \
+            getattr(self.net, "field_precision", None) != self._held_precision
 
     def refresh(self):
         """Capture again (after replacing a Parameter object of the net, which the per-call check does not see)."""
@@ -72,6 +76,7 @@ class GraphedRenderer:
         renderer, net = self.renderer, self.net
         warmup = self.warmup
         self.graph = self.out = None
+        offset0 = renderer._offset    # warm-ups and re-captures leave the eager calls' Philox offset as it was
         stream = torch.cuda.Stream(device=self.x_pix.device)
         stream.wait_stream(torch.cuda.current_stream())
         with torch.no_grad(), torch.cuda.stream(stream):
@@ -82,11 +87,16 @@ class GraphedRenderer:
             if renderer.last_path != "fused":
                 raise ValueError("GraphedRenderer: the net must take the fused field path (net.can_fuse)")
         torch.cuda.current_stream().wait_stream(stream)
-        self.offset = renderer._offset
+        renderer._offset = self.offset = offset0
         self.graph = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(self.graph):
             self.out = renderer(self.c2w, self.K, self.x_pix, net)
-        renderer._offset = self.offset   # the captured launches keep the offset they were recorded with
+        renderer._offset = offset0   # the captured launches keep the offset they were recorded with
+        # the packed weights, lin_z tables and batched tables the captured kernels read: referenced here, so an
+        # eager call that replaces a cache entry (another scene count, another precision) cannot free them
+        fused = getattr(net, "_fused", None)
+        self._held_buffers = fused.cache_tensors() if fused is not None else []
+        self._held_precision = getattr(net, "field_precision", None)
         views = self._views()
         self._held_views = views
         self._held = [(t, t._version) for t in self._params() + views if isinstance(t, torch.Tensor)]

@@ -30,11 +30,90 @@ def max_local_rays(n_rays, world, tile=64):
     return ((n_tiles + world - 1) // world) * tile
 
 
+_DTYPES = [torch.float32, torch.float64, torch.float16, torch.bfloat16, torch.int64, torch.int32, torch.uint8,
+           torch.bool]
+_MAX_DIMS = 6
+
+
+def _scene_tensors(net):
+    """(owner module, attribute name, tensor, qualified name) of every parameter and buffer of `net`, in
+    module order (the same on every rank for one architecture)."""
+    out = []
+    for mname, mod in net.named_modules():
+        for name, t in list(mod.named_parameters(recurse=False)) + list(mod.named_buffers(recurse=False)):
+            if t is not None:
+                out.append((mod, name, t, f"{mname}.{name}" if mname else name))
+    return out
+
+
 def broadcast_scene(net, src=0, group=None):
-    """Send the field weights and the latent map from `src` to every rank (once per scene)."""
-    for t in list(net.parameters()) + [net.encoder.latent, net.poses, net.focal, net.c, net.image_shape,
-                                       net.encoder.latent_scaling]:
-        dist.broadcast(t.data, src, group=group)
+    """Make every rank's `net` equal to rank `src`'s: all parameters and buffers -- the field weights, the
+    latent map (encoder.latent, latent_scaling) and the source view (poses, focal, c, image_shape) -- in one
+    collective per dtype (once per scene, ~27 MB at default.conf; the reference is single-process,
+    train.py:238-240, so this replaces nothing there).
+
+    Receiving ranks copy the values in with in-place `copy_` under no_grad, so every tensor's version counter
+    advances: the caches keyed by (data_ptr, _version) -- FusedField's packed weights, lin_z tables and view
+    descriptors, GraphedRenderer's capture check -- rebuild on the next render instead of serving the weights
+    the rank had before (a c10d collective writing into the tensors does not advance it). A buffer whose shape
+    differs from src's (another latent resolution, more source views) is replaced by a tensor of src's shape;
+    a parameter shape mismatch (another architecture) raises on every rank. The net's FusedField, if any, is
+    also invalidated explicitly. Returns the number of bytes broadcast."""
+    is_src = dist.get_rank() == src            # src is a global rank, as in dist.broadcast
+    entries = _scene_tensors(net)
+    dev = entries[0][2].device
+    comm_dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else dev
+
+    def any_rank(flag):      # every rank takes the same branch (no rank left waiting in a collective)
+        f = torch.tensor([int(flag)], dtype=torch.int64, device=comm_dev)
+        dist.all_reduce(f, group=group)
+        return bool(f.item())
+
+    # header: per tensor [dtype, ndim, shape...]: the receivers check the architecture and resize buffers
+    head = torch.zeros(len(entries), 2 + _MAX_DIMS, dtype=torch.int64)
+    for i, (_, _, t, full) in enumerate(entries):
+        if t.dim() > _MAX_DIMS or t.dtype not in _DTYPES:
+            raise ValueError(f"broadcast_scene: unsupported tensor {full} {t.dtype} {tuple(t.shape)}")
+        head[i, 0], head[i, 1] = _DTYPES.index(t.dtype), t.dim()
+        head[i, 2:2 + t.dim()] = torch.tensor(t.shape, dtype=torch.int64)
+    n = torch.tensor([len(entries)], dtype=torch.int64, device=comm_dev)
+    dist.broadcast(n, src, group=group)
+    if any_rank(int(n.item()) != len(entries)):
+        raise ValueError("broadcast_scene: the ranks' nets hold different numbers of parameters / buffers")
+    src_head = head.to(comm_dev)
+    dist.broadcast(src_head, src, group=group)
+    src_head = src_head.cpu()
+    mismatch = any(not torch.equal(src_head[i], head[i]) and (isinstance(t, torch.nn.Parameter)
+                                                             or int(src_head[i, 0]) != int(head[i, 0]))
+                   for i, (_, _, t, _) in enumerate(entries))
+    if any_rank(mismatch):
+        raise ValueError("broadcast_scene: the ranks' nets differ in architecture (a parameter's shape or a dtype)")
+    if not is_src:
+        for i, (mod, name, t, full) in enumerate(entries):
+            shape = tuple(int(s) for s in src_head[i, 2:2 + int(src_head[i, 1])])
+            if tuple(t.shape) != shape:     # a buffer of another shape: replaced by one of src's
+                t = torch.empty(shape, dtype=t.dtype, device=dev)
+                setattr(mod, name, t)
+                entries[i] = (mod, name, t, full)
+    total = 0
+    with torch.no_grad():
+        for dtype in _DTYPES:
+            group_ts = [t for _, _, t, _ in entries if t.dtype == dtype]
+            if not group_ts:
+                continue
+            flat = torch.cat([t.detach().reshape(-1) for t in group_ts]).to(comm_dev) if is_src else \
+                torch.empty(sum(t.numel() for t in group_ts), dtype=dtype, device=comm_dev)
+            dist.broadcast(flat, src, group=group)
+            total += flat.numel() * flat.element_size()
+            if not is_src:
+                off = 0
+                for t in group_ts:
+                    t.copy_(flat[off:off + t.numel()].view(t.shape))   # in place: advances t._version
+                    off += t.numel()
+    fused = getattr(net, "_fused", None)
+    if fused is not None and not is_src:
+        fused.invalidate()
+    return total
 
 
 def _takes_ray_ids(fn):

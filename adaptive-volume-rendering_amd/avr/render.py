@@ -10,7 +10,8 @@ of the synthetic scene (avr.scene) or of a NewPixelNeRFNet state_dict
 .npy (1, 512, H, W)). Prints one JSON line with rays/s and the fine samples
 evaluated; `--out` writes PPM frames. Multi-GPU: every rank renders its
 64-ray tiles of each frame and one RCCL all_gather assembles the frame
-(avr.parallel.render_sharded)."""
+(avr.parallel.render_sharded); the scene (weights, latent, source view) is
+broadcast from rank 0 once before the first frame (avr.parallel.broadcast_scene)."""
 import argparse
 import json
 import os
@@ -77,6 +78,11 @@ def main(argv=None):
     from .video import get_opencv_pixel_coordinates, orbit_cam2world, to_uint8, write_ppm
     load_library()
     net = build_net(args, device)
+    if dist is not None:
+        # every rank renders rank 0's scene: weights, latent map and source view from rank 0 (one collective per
+        # dtype; the receivers' packed-weight / table caches are invalidated)
+        from .parallel import broadcast_scene
+        broadcast_scene(net, src=0)
     if args.renderer == "adaptive":
         torch.manual_seed(args.seed + 2)
         rend = AdaptiveVolumeRenderer(net.d_latent, args.raymarch_steps, args.epsilon, args.n_coarse, True).to(device)

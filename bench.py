@@ -504,6 +504,33 @@ def standin_render(c2w, K, x_pix, ray_ids=None, n_rays_total=None):
     return rgb_c, rgb_f, depth, depth
 
 
+def share_scene(net, device, use_dist):
+    """N > 1: every rank renders rank 0's scene. avr.parallel.broadcast_scene sends its weights, latent map and
+    source view (one collective per dtype) and invalidates the receivers' packed-weight / table / view caches;
+    timed between barriers, max over ranks (once per scene, not per step)."""
+    if not use_dist:
+        return None
+    from avr.parallel import broadcast_scene
+    dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    nbytes = broadcast_scene(net, src=0)
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                     device=device if dist.get_backend() != "gloo" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"ms": round(float(t[0]) * 1e3, 3), "bytes": int(nbytes), "src": 0,
+            "what": "field weights + latent map + source view (avr.parallel.broadcast_scene), before the timed steps"}
+
+
+def scene_checksum(net):
+    """Sum of a few scene tensors in fp64: equal on every rank after share_scene."""
+    ts = [net.mlp_coarse.lin_in.weight, net.mlp_fine.lin_out.weight, net.encoder.latent, net.poses]
+    return round(float(sum(t.detach().double().sum().cpu() for t in ts)), 6)
+
+
 def run_standin(args, config, world, rank):
     from avr.parallel import render_sharded
     from avr.video import get_opencv_pixel_coordinates
@@ -513,6 +540,9 @@ def run_standin(args, config, world, rank):
     c2w = torch.stack([orbit_c2w(2 * np.pi * v / n_views) for v in range(n_views)])
     c2w = c2w.repeat_interleave(R // n_views, 0).reshape(1, R, 4, 4)
     K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]])
+    # the scene distribution of the GPU path: ranks > 0 start from another scene and receive rank 0's
+    net = build_scene(torch.device("cpu"), seed=0 if rank == 0 else 1000 + rank)
+    shared = share_scene(net, torch.device("cpu"), world > 1)
 
     def step():
         if world > 1:
@@ -541,7 +571,10 @@ def run_standin(args, config, world, rank):
                 "data": "STAND-IN renderer on the CPU (--device cpu): launcher / sharding test, not a measurement",
                 "config": {"workload": f"stand-in, {n_views} views x {args.frame}x{args.frame}", "rays_per_step": R,
                            "parallelism": f"ray-shard x{world} + gloo gather"},
-                "checksum": [round(float(o.double().sum()), 6) for o in out[:3]]}
+                "checksum": [round(float(o.double().sum()), 6) for o in out[:3]],
+                "scene_checksum": scene_checksum(net)}
+        if shared is not None:
+            line["scene_broadcast"] = shared
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -858,9 +891,11 @@ def main():
     if args.mode == "train":
         return run_train(args, device)
 
-    net = build_scene(device, sigma_bias=args.sigma_bias)
+    # N > 1: ranks > 0 build a scene of the same architecture and receive rank 0's (broadcast_scene)
+    net = build_scene(device, seed=0 if rank == 0 else 1000 + rank, sigma_bias=args.sigma_bias)
     net.field_precision = args.precision
     fused = net.fused()
+    shared = share_scene(net, device, use_dist)
     timer = FieldTimer()
     timer.wrap(fused)
     hbm = HbmKernelTimer(avr.ops)
@@ -1036,6 +1071,9 @@ def main():
     line["hbm_achievable_GBs"] = round(ach[0], 1)
     line["hbm_write_achievable_GBs"] = round(ach[1], 1)
     line["hbm_kernels"] = hbm.report(achievable=ach)
+    if shared is not None:
+        line["scene_broadcast"] = shared
+        line["scene_checksum"] = scene_checksum(net)
     if config == 4:
         line["config"]["fine_samples_evaluated_fraction"] = round(
             fine_evaluated[0] / (args.steps * R * (args.n_coarse + args.n_fine)), 4)

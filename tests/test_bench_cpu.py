@@ -35,6 +35,9 @@ def test_bench_gpus_n_spawns_n_ranks(n):
     # N > 1 defaults to BASELINE config 5 (fixed 4 views per step: strong scaling)
     assert many["scaling"] == "strong" and many["config"]["rays_per_step"] == 4 * 48 * 48
     assert many["checksum"] == one["checksum"]
+    # ranks > 0 start from another scene; broadcast_scene hands them rank 0's
+    assert many["scene_checksum"] == one["scene_checksum"]
+    assert many["scene_broadcast"]["bytes"] > 27e6 and "scene_broadcast" not in one
 
 
 def test_bench_default_is_config3_weak():

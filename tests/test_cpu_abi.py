@@ -98,6 +98,12 @@ def test_model_state_dict_keys_match_reference_layout():
     mv = NewPixelNeRFNet(default_conf(multiview=True)["model"])
     mv.encoder.set_latent(torch.zeros(1, 512, 4, 4))
     assert fused_eligible(mv) and len(mv.mlp_coarse.lin_z) == 3 and mv.mlp_coarse.n_blocks == 5
+    # NS > 1 source views (the split launches): combine_layer must leave at least one block before the combine
+    mv.num_views_per_obj = 2
+    assert fused_eligible(mv, multiview=True) and not fused_eligible(mv)
+    for mlp in (mv.mlp_coarse, mv.mlp_fine):
+        mlp.combine_layer = 0
+    assert not fused_eligible(mv, multiview=True)
 
 
 def test_graft_entry_build():

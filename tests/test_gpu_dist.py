@@ -86,3 +86,96 @@ def test_bench_dist_path_at_one_rank():
     assert line["n_gpus"] == 1 and line["scaling"] == "strong"
     assert "RCCL gather" in line["config"]["parallelism"]
     assert line["config"]["rays_per_gpu"] == 4 * 160 * 160 and line["value"] > 0
+
+
+def test_broadcast_scene_over_rccl_world1(nccl_world1):
+    """broadcast_scene on the RCCL group (device tensors, one collective per dtype): at src the net is left
+    as it was (no version bump, caches kept) and the render after it equals the render before it."""
+    from avr.parallel import broadcast_scene
+    from avr.renderers import VolumeRenderer
+    from avr.scene import INTRINSICS, synthetic_scene
+    net = synthetic_scene(DEV)
+    R = 512
+    g = torch.Generator().manual_seed(5)
+    x_pix = torch.rand(1, R, 2, generator=g).to(DEV)
+    from bench import orbit_c2w
+    c2w = orbit_c2w(0.3).to(DEV).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
+    K = torch.tensor([INTRINSICS], device=DEV)
+    rend = VolumeRenderer(0.8, 1.8, 64, 32, 0, 0.01, True)
+    with torch.no_grad():
+        rend.seed, rend._offset = 9, 0
+        before = rend(c2w, K, x_pix, net)
+        key = net.fused()._packed[True][0]
+        nbytes = broadcast_scene(net, src=0)
+        rend.seed, rend._offset = 9, 0
+        after = rend(c2w, K, x_pix, net)
+    torch.cuda.synchronize()
+    assert nbytes > 27e6 and rend.last_path == "fused"
+    assert net.fused()._packed[True][0] == key        # src: nothing rewritten, nothing repacked
+    for a, b in zip(before[:3], after[:3]):
+        assert torch.equal(a, b)
+
+
+def _bcast_gpu_worker(rank, port, q):
+    import torch.distributed as dist
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        sys.path[:0] = [REPO, os.path.join(REPO, "adaptive-volume-rendering_amd")]
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        # two ranks on the one GPU of the box: RCCL needs one GPU per rank, so the group is gloo (broadcast_scene
+        # stages the device tensors through the host) -- what is tested is the receivers' cache invalidation
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        import avr
+        from avr.parallel import broadcast_scene
+        from avr.renderers import VolumeRenderer
+        from avr.scene import INTRINSICS, synthetic_scene
+        from bench import orbit_c2w
+        avr.load_library()
+        net = synthetic_scene(dev, 0 if rank == 0 else 7, latent_hw=(64, 64) if rank == 0 else (32, 32))
+        R = 640
+        g = torch.Generator().manual_seed(5)
+        x_pix = torch.rand(1, R, 2, generator=g).to(dev)
+        c2w = orbit_c2w(0.3).to(dev).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
+        K = torch.tensor([INTRINSICS], device=dev)
+        rend = VolumeRenderer(0.8, 1.8, 64, 32, 0, 0.01, True)
+        with torch.no_grad():
+            rend.seed, rend._offset = 9, 0
+            own = rend(c2w, K, x_pix, net)          # rank 1 renders its own scene first: caches built
+            fused = net.fused()
+            key0 = fused._packed[True][0]
+            broadcast_scene(net, src=0)
+            rend.seed, rend._offset = 9, 0
+            shared = rend(c2w, K, x_pix, net)
+            key1 = fused._packed[True][0]
+        torch.cuda.synchronize()
+        res = torch.cat([t.reshape(-1) for t in shared[:3]]).cpu()
+        outs = [torch.empty_like(res) for _ in range(2)]
+        dist.all_gather(outs, res)
+        own_flat = torch.cat([t.reshape(-1) for t in own[:3]]).cpu()
+        checks = {"fused": rend.last_path == "fused", "equal_to_rank0": torch.equal(outs[0], outs[1]),
+                  "repacked": (key1 != key0) if rank == 1 else (key1 == key0),
+                  "changed": (not torch.equal(own_flat, res)) if rank == 1 else torch.equal(own_flat, res)}
+        q.put((rank, all(checks.values()), str(checks)))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 -- report instead of hanging the peer
+        q.put((rank, False, repr(e)))
+
+
+def test_broadcast_scene_two_ranks_repack():
+    """SURVEY §8e on the GPU: rank 1 renders its own scene (other weights, a 32x32 latent), receives rank 0's
+    with broadcast_scene, repacks its weights / rebuilds its tables on the next render, and renders rank 0's
+    frame bit for bit; rank 0 keeps its caches."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_gpu_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert all(ok for _, ok, _ in res), res

@@ -96,3 +96,50 @@ def test_graph_capture_and_replay_under_anomaly_mode():
             want = rend(c2w, K, x_pix, net)
     for a, b in zip(got, want):
         assert torch.equal(a, b)
+
+
+def _scenes(SB, R, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x_pix = torch.rand(SB, R, 2, generator=g).to(DEV)
+    c2w = torch.eye(4).reshape(1, 1, 4, 4).repeat(SB, R, 1, 1)
+    c2w[..., 2, 3] = -1.3 - 0.2 * torch.rand(SB, R, generator=g)
+    return c2w.to(DEV), x_pix
+
+
+def test_graph_survives_eager_calls_that_replace_caches():
+    """the captured launches read FusedField's batched lin_z tables and packed blob. An eager call
+    with another scene count replaces the batched-table cache entry, one at the other precision the packed
+    entry; the graph keeps references to what it reads (and re-captures after a precision change), so the
+    replay still equals the eager call. Capture and re-capture leave the renderer's Philox offset alone."""
+    from avr.graphs import GraphedRenderer
+    from avr.scene import INTRINSICS
+    net, rend, _, _, _ = _scene(8, 1)
+    net.encoder.set_latent(net.encoder.latent.expand(3, -1, -1, -1).contiguous() *
+                           torch.tensor([1.0, 0.5, -1.0], device=DEV).reshape(3, 1, 1, 1))
+    net.poses = net.poses.expand(3, 3, 4).contiguous()
+    K = torch.tensor([INTRINSICS], device=DEV).expand(3, 3, 3).contiguous()
+    rend.seed = 21
+    c2w2, x2 = _scenes(2, 256, 7)
+    gr = GraphedRenderer(rend, net, c2w2, K[:2], x2)
+    assert rend._offset == 0 and gr.offset == 0
+    c2w3, x3 = _scenes(3, 256, 8)
+    with torch.no_grad():
+        rend(c2w3, K, x3, net)                  # SB = 3: a new batched-table entry replaces the SB = 2 one
+        net.field_precision = "fp32"
+        rend(c2w2, K[:2], x2, net)              # the fp32 blob replaces the x3 one
+        net.field_precision = "x3"
+        torch.cuda.empty_cache()
+        junk = torch.full((64 << 20,), float("nan"), device=DEV)   # reuse any freed block
+    captures = gr.captures
+    got = [t.clone() for t in gr()]
+    assert gr.captures == captures              # back at x3: the capture's precision, no re-capture needed
+    rend._offset = gr.offset
+    with torch.no_grad():
+        want = rend(c2w2, K[:2], x2, net)
+    del junk
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
+    net.field_precision = "fp32"
+    gr()
+    assert gr.captures == captures + 1          # a precision change re-captures
+    net.field_precision = "x3"

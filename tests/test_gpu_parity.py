@@ -345,6 +345,31 @@ def test_field_multiview_golden(golden, tag):
     np.testing.assert_allclose(to_np(tc), g["out_coarse"], atol=5e-5, rtol=1e-4)
 
 
+def test_field_multiview_combine_layer0_module_path(golden):
+    """combine_layer 0 (the views combined right after lin_in) is a valid ResnetFC config the split
+    launches do not run: the net routes it to the module path (no AVRError), and a direct FusedField call
+    raises instead of serving it at x3; at fp32 precision the NS > 1 redirect raises as well."""
+    from avr import _lib
+    g = golden("g4_field_ns2_small.npz")
+    net = build_net(g, DEV, "x3")
+    xyz, vd = T(g["xyz"]), T(g["viewdirs"])
+    with torch.no_grad():
+        ref = net.forward_torch(xyz, coarse=True, viewdirs=vd)
+        for mlp in (net.mlp_coarse, net.mlp_fine):
+            mlp.combine_layer = 0
+        assert not net.can_fuse(xyz) and not net.can_fuse_multiview(xyz)
+        out = net(xyz, coarse=True, viewdirs=vd)
+        np.testing.assert_array_equal(to_np(out), to_np(net.forward_torch(xyz, coarse=True, viewdirs=vd)))
+        assert not np.array_equal(to_np(out), to_np(ref))      # the combine really moved
+        with pytest.raises(_lib.AVRError):
+            net.fused().forward_points(xyz, vd, True)
+        for mlp in (net.mlp_coarse, net.mlp_fine):
+            mlp.combine_layer = int(g["combine_layer"])
+        net.field_precision = "fp32"
+        with pytest.raises(_lib.AVRError):
+            net.fused().forward_points(xyz, vd, True)
+
+
 def test_field_multiview_objects_and_renderer(golden):
     """SB = 2 objects x NS = 2 views (more scenes than points per object would need: 4
     (object, view) pairs in the first launch, 2 objects in the second), equal to each object

@@ -22,6 +22,7 @@ def _graphed_state():
         views = g._views()
         g._held_views = views
         g._held = [(t, t._version) for t in g._params() + views if isinstance(t, torch.Tensor)]
+        g._held_precision = net.field_precision
     hold()
     return g, net, hold
 
@@ -40,6 +41,10 @@ def test_state_check_sees_updates():
     assert g._stale()
     hold()
     net.poses = net.poses.clone()
+    assert g._stale()
+    hold()
+    assert not g._stale()
+    net.field_precision = "fp32"                    # the captured kernels are the x3 ones
     assert g._stale()
     hold()
     assert not g._stale()

@@ -67,3 +67,72 @@ def test_ray_tiles_partition():
         allidx = torch.cat(parts).sort()[0]
         assert torch.equal(allidx, torch.arange(R))
         assert max(p.numel() for p in parts) <= max_local_rays(R, world)
+
+
+def _bcast_worker(rank, world, port, q, mismatch):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from avr.conf import default_conf
+        from avr.parallel import broadcast_scene
+        from avr.scene import synthetic_scene
+        cpu = torch.device("cpu")
+        if mismatch and rank == 1:    # another architecture (default_mv: 5 blocks) must raise on every rank
+            net = synthetic_scene(cpu, 7, default_conf(multiview=True)["model"])
+        else:
+            # rank 1: other weights, another latent (other resolution) and another source pose than rank 0
+            net = synthetic_scene(cpu, 0 if rank == 0 else 7, latent_hw=(64, 64) if rank == 0 else (32, 48))
+            if rank == 1:
+                net.poses[0, 2, 3] = 2.0
+        fused = net.fused()
+        view_before = fused.view(0)            # rank 1 caches its own scene's view descriptor first
+        params = list(net.mlp_coarse.parameters())
+        key_before = [(p.data_ptr(), p._version) for p in params]
+        fused._packed[True] = (("stale",), None)   # stands in for a packed blob of rank 1's weights
+        try:
+            nbytes = broadcast_scene(net, src=0)
+        except ValueError as e:
+            q.put((rank, mismatch and "architecture" in str(e) or "numbers" in str(e), repr(e)))
+            dist.destroy_process_group()
+            return
+        key_after = [(p.data_ptr(), p._version) for p in params]
+        checks = {"bytes": nbytes > 27e6}
+        if rank == 1:
+            checks["versions_advanced"] = all(a[1] > b[1] for a, b in zip(key_after, key_before))
+            checks["caches_dropped"] = not fused._packed and fused.view(0) is not view_before
+        else:
+            checks["src_untouched"] = key_after == key_before and bool(fused._packed)
+        checks["latent_shape"] = tuple(net.encoder.latent.shape) == (1, 512, 64, 64)
+        checks["pose"] = abs(float(fused.view(0).poses[11]) - 1.3) < 1e-6
+        # the field itself (module path on the CPU) gives rank 0's outputs on every rank
+        g = torch.Generator().manual_seed(3)
+        xyz = torch.rand(1, 64, 3, generator=g) * 0.6 - 0.3
+        vd = torch.nn.functional.normalize(torch.rand(1, 64, 3, generator=g) - 0.5, dim=-1)
+        with torch.no_grad():
+            out = torch.cat([net(xyz, coarse=c, viewdirs=vd).reshape(-1) for c in (True, False)])
+        outs = [torch.empty_like(out) for _ in range(world)]
+        dist.all_gather(outs, out)
+        checks["same_field"] = all(torch.equal(o, outs[0]) for o in outs)
+        q.put((rank, all(checks.values()), str(checks)))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 -- report instead of hanging the peer
+        q.put((rank, False, repr(e)))
+
+
+@pytest.mark.parametrize("mismatch", [False, True])
+def test_broadcast_scene_gloo(mismatch):
+    """rank 1 starts from another scene (weights, latent of another size, source pose) and has
+    cached its view descriptor and a packed blob; after broadcast_scene every tensor's version advanced, the
+    caches are gone, and the field gives rank 0's outputs bit for bit. Another architecture raises on both."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q, mismatch)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert all(ok for _, ok, _ in res), res
