@@ -80,22 +80,14 @@ __device__ __forceinline__ float mask_select(uint64_t m, float clear, float set)
 
 // ------------------------------------------------------------------ Philox4x32-10
 // Counter-based RNG for in-kernel noise (no noise bytes read from HBM).
-#ifndef AVR_DIAG_PHILOX_ROUNDS
-#define AVR_DIAG_PHILOX_ROUNDS 10   // timing diagnostics only (any other count gives wrong noise)
-#endif
 __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
 #pragma unroll
-  for (int i = 0; i < AVR_DIAG_PHILOX_ROUNDS; ++i) {
-#ifdef AVR_DIAG_PHILOX_MULHI
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-#else
+  for (int i = 0; i < 10; ++i) {
     // one v_mad_u64_u32 per product gives both halves (32-bit integer multiplies are
     // the slow part of the generator; separate mul_lo / mul_hi would double them)
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
     const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-#endif
     c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
     k.x += 0x9E3779B9u;
     k.y += 0xBB67AE85u;

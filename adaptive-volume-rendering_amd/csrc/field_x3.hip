@@ -191,9 +191,7 @@ struct LdsPlan {
   static_assert(CAP * (4 * HID >= 1024 ? HID / 256 : 1) <= 4 * 64, "stage_rows: one lane per piece");
 };
 
-#if defined(AVR_DIAG_ONE_LAYER)   // timing-only diagnostic: every block reads block 0's weights (L2-resident)
-#define DBG_B(b) 0
-#elif defined(AVR_STAMPS)
+#if defined(AVR_STAMPS)
 #define DBG_B(b) ((a.debug & 1) ? 0 : (b))
 #else
 #define DBG_B(b) (b)
@@ -221,18 +219,14 @@ __device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const 
     for (int sg = 0; sg < 4; ++sg) {
       const floatx4 x = v[ft][sg];
       const int64_t m = base + 16 * sg + j;
-#ifndef AVR_DIAG_NO_ACT_STORE   // timing-only diagnostic: the act rows are not written
       if (m < a.M) __builtin_nontemporal_store(x, reinterpret_cast<floatx4*>(act + m * HID + 16 * (FT * wid + ft) + 4 * g));
-#endif
       const int idx = (ft * 4 + sg) * 4;
       const unsigned nib = (x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) | (x.w > 0.f ? 8u : 0u);
       bits[idx >> 5] |= nib << (idx & 31);
     }
   unsigned* mk = a.mask + (((int64_t)layer * gridDim.x + blockIdx.x) * NW + wid) * MW * 64 + lane;
-#ifndef AVR_DIAG_NO_MASK_STORE   // timing-only diagnostic: the mask words are not written
 #pragma unroll
   for (int q = 0; q < MW; ++q) mk[q * 64] = bits[q];
-#endif
 }
 
 // Work split: NW waves (4: one per SIMD; 8: two per SIMD, which doubles the
@@ -480,11 +474,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       __syncthreads();
       AVR_STAMP(30);
       mx = 0.f;
-#ifndef AVR_DIAG_NO_BLEND   // timing-only diagnostic: the lin_z blend skipped (wrong results)
       blend_stage<FT, true, !TWO, ACT>(h, v, mx, stage, tail, 0, D, P::RS, S_h, 1.0f / S_h, wid, g, j, beta);
-#else
-      mx = max_relu_affine<FT, false>(h, 1.0f / S_h, bz);
-#endif
       mx = wave_max(mx);
     } else {
       for (int lo = 0; b < a.n_lin_z && lo < D; lo += P::CAP) {   // more distinct texels than the stage holds

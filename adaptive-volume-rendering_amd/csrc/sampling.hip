@@ -212,9 +212,6 @@ __global__ void __launch_bounds__(kRaysThreads) rays_coarse_kernel(
     __syncthreads();   // base_tab
   }
   if (threadIdx.x < 64) {   // wave 0: the rays' geometry, one lane per ray
-#ifdef AVR_DIAG_NO_GEOM
-    return;
-#endif
     if (threadIdx.x >= kRaysPerBlock || r0 + threadIdx.x >= total) return;
     const int64_t i = r0 + threadIdx.x;
     const int64_t sb = i / n_rays, r = i - sb * n_rays;

@@ -134,13 +134,8 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
     const int64_t row0 = k0 + (int64_t)kDwK * c;
     const int last = chunk_last(c);
     const int r = rb + NW * u < last ? rb + NW * u : last;
-#ifndef AVR_WGRAD_NO_LOAD   // diagnostic build: no global loads (constant operands)
     gn[u] = *reinterpret_cast<const floatx4*>(D.g + row0 * D.ldg + (r * ldg + gcol));
     xn[u] = *reinterpret_cast<const floatx4*>(D.x + row0 * D.ldx + (r * ldx + xcol));
-#else
-    gn[u] = floatx4{1.f, 2.f, 3.f, (float)r};
-    xn[u] = floatx4{(float)row0, 2.f, 1.f, 0.5f};
-#endif
   };
 
   const int wo = wid / WI, wi = wid % WI;
@@ -192,17 +187,12 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
         ahn = tr_frag(st, 128 * wo + 16 * (t + 1), trb);
         aln = tr_frag(st + kDwImg, 128 * wo + 16 * (t + 1), trb);
       }
-#ifndef AVR_WGRAD_NO_MFMA   // diagnostic build: the staging pipeline alone
 #pragma unroll
       for (int u = 0; u < TI; ++u) {
         acc[t][u] = mfma32h(ah, bh[u], acc[t][u]);
         acc[t][u] = mfma32h(ah, bl[u], acc[t][u]);
         acc[t][u] = mfma32h(al, bh[u], acc[t][u]);
       }
-#else
-      acc[t][0][0] += __builtin_bit_cast(floatx4, ah)[0] + __builtin_bit_cast(floatx4, al)[1] +
-                      __builtin_bit_cast(floatx4, bh[t % TI])[2] + __builtin_bit_cast(floatx4, bl[t % TI])[3];
-#endif
       __builtin_amdgcn_sched_barrier(0);
       ah = ahn;
       al = aln;
@@ -234,17 +224,12 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
         ahn = tr_frag(st, 128 * wo + 16 * (t + 1), trb);
         aln = tr_frag(st + kDwImg, 128 * wo + 16 * (t + 1), trb);
       }
-#ifndef AVR_WGRAD_NO_MFMA
 #pragma unroll
       for (int u = 0; u < TI; ++u) {
         acc[t][u] = mfma32h(ah, bh[u], acc[t][u]);
         acc[t][u] = mfma32h(ah, bl[u], acc[t][u]);
         acc[t][u] = mfma32h(al, bh[u], acc[t][u]);
       }
-#else
-      acc[t][0][0] += __builtin_bit_cast(floatx4, ah)[0] + __builtin_bit_cast(floatx4, al)[1] +
-                      __builtin_bit_cast(floatx4, bh[t % TI])[2] + __builtin_bit_cast(floatx4, bl[t % TI])[3];
-#endif
       constexpr int TPU = TO / NU;
       if (t % TPU == 0) {
         put(c + 1, t / TPU);

@@ -10,10 +10,6 @@
 // scaling); the geometry helpers use __f*_rn intrinsics, which never contract.
 #pragma clang fp contract(fast)
 
-#ifndef AVR_X3_ORDER
-#define AVR_X3_ORDER 0   // MFMA order of the 8-wave K loop (diagnostic A/B switch; 0 = shipped)
-#endif
-
 namespace avr {
 
 struct FragX3 {
@@ -224,42 +220,13 @@ __device__ __forceinline__ void chunk_step_sg(floatx4 (&acc)[FT][4], const FragX
 #pragma unroll
   for (int sg = 0; sg < 4; ++sg) {
     const BPair Bn = sg < 3 ? read_b(X16, c, sg + 1, g, j) : read_b(X16, cn, 0, g, j);
-#ifndef AVR_W_BUF_AUX
     An[sg] = load_frag(wn + (lo + 2 * 64 * sg));   // wave-uniform base + 32-bit lane offset
-#else
-    {  // diagnostic A/B: the same fragment by raw buffer loads with cache-policy bits AVR_W_BUF_AUX
-      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)wn, 0, 0x7fffffff, 0x00020000);
-      const int off = 16 * (int)(lo + 2 * 64 * sg);
-      An[sg].hi = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AVR_W_BUF_AUX));
-      An[sg].lo = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 1024, 0, AVR_W_BUF_AUX));
-    }
-#endif
-#if AVR_X3_ORDER == 1
-    // small terms first, then hi.hi: the two corrections meet before the large product
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft) {
-      acc[ft][sg] = mfma32h(A[ft].lo, B.hi, ZERO ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[ft][sg]);
-      acc[ft][sg] = mfma32h(A[ft].hi, B.lo, acc[ft][sg]);
-      acc[ft][sg] = mfma32h(A[ft].hi, B.hi, acc[ft][sg]);
-    }
-#elif AVR_X3_ORDER == 2
-    // term-major: one B operand half feeds four consecutive MFMAs (four independent chains interleaved)
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft)
-      acc[ft][sg] = mfma32h(A[ft].hi, B.hi, ZERO ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[ft][sg]);
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft) acc[ft][sg] = mfma32h(A[ft].lo, B.hi, acc[ft][sg]);
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft) acc[ft][sg] = mfma32h(A[ft].hi, B.lo, acc[ft][sg]);
-#else
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft) {
       acc[ft][sg] = mfma32h(A[ft].hi, B.hi, ZERO ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[ft][sg]);
       acc[ft][sg] = mfma32h(A[ft].hi, B.lo, acc[ft][sg]);
       acc[ft][sg] = mfma32h(A[ft].lo, B.hi, acc[ft][sg]);
     }
-#endif
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);

@@ -11,6 +11,7 @@ start/end timestamps), mean of every counter per dispatch, and derived values:
   hbm_GBs     = hbm_bytes / duration
   mfma_busy   = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)
   l2_hit_rate = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
+  clock_GHz   = GRBM_GUI_ACTIVE / 8 XCDs / duration
 """
 import collections
 import csv
@@ -47,6 +48,8 @@ def main():
             e["hbm_GBs"] = e["hbm_bytes"] / e["mean_ns"] if e["mean_ns"] else None
         if "SQ_VALU_MFMA_BUSY_CYCLES" in e and e.get("GRBM_GUI_ACTIVE"):
             e["mfma_busy"] = e["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * e["GRBM_GUI_ACTIVE"] / 8)
+        if e.get("GRBM_GUI_ACTIVE") and e["mean_ns"]:
+            e["clock_GHz"] = e["GRBM_GUI_ACTIVE"] / 8 / e["mean_ns"]
         if "TCC_HIT_sum" in e and "TCC_MISS_sum" in e and e["TCC_HIT_sum"] + e["TCC_MISS_sum"] > 0:
             e["l2_hit_rate"] = e["TCC_HIT_sum"] / (e["TCC_HIT_sum"] + e["TCC_MISS_sum"])
         res[k] = e
@@ -54,7 +57,7 @@ def main():
     json.dump({"source": dirs, "kernels": res}, open(out, "w"), indent=1)
     for k, e in list(res.items())[:8]:
         extra = {x: round(e[x], 3) if isinstance(e.get(x), float) else e.get(x)
-                 for x in ("hbm_GBs", "mfma_busy", "l2_hit_rate") if x in e}
+                 for x in ("hbm_GBs", "mfma_busy", "l2_hit_rate", "clock_GHz") if x in e}
         print(f"{k[:48]:48s} n={e['dispatches']:3d} {e['mean_ns'] / 1e3:10.1f} us {extra}")
 
 

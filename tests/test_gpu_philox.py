@@ -135,11 +135,35 @@ def _c3_philox_oracle():
     return cat(0), cat(1), cat(2), aux, ns
 
 
-def test_c3_philox_bench_path_vs_oracle():
+def _record(entry):
+    """Append one JSON line to $AVR_TEST_REPORT (default gpurun_out/philox_c3_flip_rates.jsonl): the measured
+    flip rates of the benchmarked path, kept under profiles/ per round."""
+    import json
+    import os
+    path = os.environ.get("AVR_TEST_REPORT", os.path.join("gpurun_out", "philox_c3_flip_rates.jsonl"))
+    d = os.path.dirname(path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    with open(path, "a") as f:
+        f.write(json.dumps(entry) + "\n")
+
+
+@pytest.mark.parametrize("precision", ["x3", "fp32"])
+def test_c3_philox_bench_path_vs_oracle(precision):
+    """BASELINE config 3 exactly as bench.py runs it, at both field precisions: the bin-flip rate of the fog
+    scene against the oracle is written to $AVR_TEST_REPORT for profiles/."""
+    net, x_pix_np = _bench_scene()
+    net.field_precision = precision
+    try:
+        _c3_philox_check(net, x_pix_np, precision)
+    finally:
+        net.field_precision = "x3"
+
+
+def _c3_philox_check(net, x_pix_np, precision):
     from avr import ops
     from avr.renderers import VolumeRenderer
     from bench import orbit_c2w
-    net, x_pix_np = _bench_scene()
     x_pix = T(x_pix_np)
     K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]], device=DEV)
     c2w = orbit_c2w(0.7).to(DEV).reshape(1, 1, 4, 4).expand(1, R3, 4, 4)
@@ -181,7 +205,8 @@ def test_c3_philox_bench_path_vs_oracle():
     # rays take other fine bins than the oracle's own weights give; the oracle's fine pass on the HIP-chosen
     # samples (bins bit-exact above) must then match them like every other ray
     flips = np.flatnonzero(~same)
-    print(f"philox C3: rays with the oracle's bins {same.mean():.5f} ({flips.size} bin flips)")
+    sample_same = float((to_np(idx[S]) == aux["idx"][0]).mean())
+    print(f"philox C3 {precision}: rays with the oracle's bins {same.mean():.5f} ({flips.size} bin flips)")
     assert same.mean() >= 0.99, same.mean()
     np.testing.assert_allclose(to_np(ff[S])[same], aux["field_fine"][0][same], atol=5e-5, rtol=1e-4)
     rgb_ref, depth_ref = o_f[0].copy(), o_d[0].copy()
@@ -201,7 +226,13 @@ def test_c3_philox_bench_path_vs_oracle():
     assert staged.all(), staged.mean()
     # end to end against the pure oracle: an outlier only where the bins flipped
     ok = (np.abs(to_np(r_f[0, S]) - o_f[0]).max(-1) <= 1e-4) & (np.abs(to_np(r_d[0, S]) - o_d[0]) <= 1e-4)
-    print(f"philox C3: end-to-end within 1e-4 on {ok.mean():.5f} of rays")
+    print(f"philox C3 {precision}: end-to-end within 1e-4 on {ok.mean():.5f} of rays")
+    _record({"test": "test_c3_philox_bench_path_vs_oracle", "precision": precision, "rays": int(same.size),
+             "rays_with_oracle_bins": float(same.mean()), "bin_flip_rays": int(flips.size),
+             "fine_samples_with_oracle_bin": sample_same, "end_to_end_within_1e-4": float(ok.mean()),
+             "outliers": int((~ok).sum()), "outliers_not_bin_flips": int((~ok & same).sum()),
+             "max_coarse_field_err": float(np.abs(to_np(fc[S]) - aux["field_coarse"][0]).max()),
+             "max_coarse_rgb_err": float(np.abs(to_np(rgb_c[S]) - o_c[0]).max())})
     assert ok.mean() >= 0.99, ok.mean()
     assert not (~ok & same).any(), "a ray with the oracle's bins must match it"
     assert np.abs(to_np(r_c[0, S]) - o_c[0]).max() <= 1e-4
