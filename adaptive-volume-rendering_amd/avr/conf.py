@@ -42,7 +42,7 @@ class Conf(dict):
         return Conf(v) if isinstance(v, dict) and not isinstance(v, Conf) else v
 
 
-# conf/default.conf (model{} and normal_renderer{}) restated as data.
+# conf/default.conf (model{}, normal_renderer{}, raymarcher{}, adaptive_renderer{}) restated as data.
 DEFAULT_MODEL = {
     "use_encoder": True, "use_global_encoder": False, "use_xyz": True, "canon_xyz": False, "use_code": True,
     "code": {"num_freqs": 6, "freq_factor": 1.5, "include_input": True},
@@ -53,6 +53,9 @@ DEFAULT_MODEL = {
 }
 DEFAULT_NORMAL_RENDERER = {"near": 0.8, "far": 1.8, "n_coarse": 64, "n_fine": 32, "n_fine_depth": 16,
                            "depth_std": 0.01, "white_back": True}
+DEFAULT_RAYMARCHER = {"num_feature_channels": 512, "raymarch_steps": 10}
+DEFAULT_ADAPTIVE_RENDERER = {"num_feature_channels": 512, "raymarch_steps": 10, "epsilon": 0.15, "n_coarse": 20,
+                             "white_back": True}
 # conf/default_mv.conf overrides (5 blocks, combine after the 3rd)
 DEFAULT_MV_MLP = {"type": "resnet", "n_blocks": 5, "d_hidden": 512, "combine_layer": 3, "combine_type": "average"}
 
@@ -63,4 +66,5 @@ def default_conf(multiview=False):
     if multiview:
         model["mlp_coarse"] = dict(DEFAULT_MV_MLP)
         model["mlp_fine"] = dict(DEFAULT_MV_MLP)
-    return Conf({"model": model, "normal_renderer": dict(DEFAULT_NORMAL_RENDERER)})
+    return Conf({"model": model, "normal_renderer": dict(DEFAULT_NORMAL_RENDERER),
+                 "raymarcher": dict(DEFAULT_RAYMARCHER), "adaptive_renderer": dict(DEFAULT_ADAPTIVE_RENDERER)})

@@ -415,7 +415,7 @@ def run_train(args, device):
     backward chain + the x3 weight-gradient kernel) and PyTorch autograd of
     the same module (forward_torch; the rest of the step is identical)."""
     from avr.conf import default_conf
-    from avr.renderers import VolumeRenderer
+    from avr.renderers import AdaptiveVolumeRenderer, VolumeRenderer
     SB, R = 4, 512
     net = build_scene(device, conf=args.conf)
     g = torch.Generator(device="cpu").manual_seed(7)
@@ -427,14 +427,23 @@ def run_train(args, device):
     net.train()
     for p in net.parameters():
         p.requires_grad_(True)
-    rend = VolumeRenderer.from_conf(default_conf()["normal_renderer"]).to(device)
-    rend.seed = 99
+    if args.renderer == "adaptive":
+        # train.py:272-273 (any run name not starting with "VR" / naming "Raymarcher"):
+        # AdaptiveVolumeRenderer.from_conf(conf["adaptive_renderer"]); its LSTM / out_layer train with the net
+        # (rf_and_renderer.parameters(), train.py:300)
+        torch.manual_seed(11)
+        rend = AdaptiveVolumeRenderer.from_conf(default_conf()["adaptive_renderer"]).to(device)
+        params = list(net.parameters()) + list(rend.parameters())
+    else:
+        rend = VolumeRenderer.from_conf(default_conf()["normal_renderer"]).to(device)
+        rend.seed = 99
+        params = list(net.parameters())
     x_pix = torch.rand(SB, R, 2, generator=g).to(device)
     c2w = torch.stack([orbit_c2w(0.3 + 0.9 * b) for b in range(SB)]).to(device)
     c2w = c2w.reshape(SB, 1, 4, 4).expand(SB, R, 4, 4)
     K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]] * SB, device=device)
     gt = torch.rand(SB, R, 3, generator=g).to(device)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    opt = torch.optim.Adam(params, lr=1e-4)
 
     def step():
         rgb_c, rgb_f, _, _ = rend(c2w, K, x_pix, net)
@@ -456,17 +465,24 @@ def run_train(args, device):
         torch.cuda.synchronize()
         res[mode] = (time.perf_counter() - t0) / args.steps
         assert bool(torch.isfinite(loss))
-    spr = rend.n_coarse + rend.n_coarse + rend.n_fine
+    if args.renderer == "adaptive":
+        spr = 1 + rend.n_coarse      # the marched point (coarse MLP) + the band (fine MLP); + steps latent lookups
+        wl = (f"train.py defaults: {SB} scenes x {R} rays, AdaptiveVolumeRenderer (conf adaptive_renderer: "
+              f"{rend.steps} LSTM march steps on 512-channel latent lookups, band of {rend.n_coarse} samples, "
+              f"epsilon {rend.epsilon}), Adam lr 1e-4 over net + LSTM / out_layer")
+    else:
+        spr = rend.n_coarse + rend.n_coarse + rend.n_fine
+        wl = (f"train.py defaults: {SB} scenes x {R} rays, {rend.n_coarse} coarse + {rend.n_fine} fine "
+              f"({rend.n_fine_depth} depth) samples, Adam lr 1e-4")
     line = {
-        "metric": "training rays/s (train.py step: forward + loss.backward() + Adam through VolumeRenderer)",
+        "metric": "training rays/s (train.py step: forward + loss.backward() + Adam through "
+                  + ("AdaptiveVolumeRenderer)" if args.renderer == "adaptive" else "VolumeRenderer)"),
         "value": round(SB * R / res["hip"], 1), "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(res["hip"] * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (field products as 3 fp16 MFMA terms)",
         "data": f"synthetic: random-init {args.conf}.conf field, 4 random 512x64x64 latents, random pixels/targets",
-        "config": {"workload": f"train.py defaults: {SB} scenes x {R} rays, {rend.n_coarse} coarse + "
-                               f"{rend.n_fine} fine ({rend.n_fine_depth} depth) samples, Adam lr 1e-4, field of "
-                               f"conf/{args.conf}.conf ({net.mlp_coarse.n_blocks} x {net.mlp_coarse.d_hidden} "
-                               f"ResnetFC, combine_layer {net.mlp_coarse.combine_layer})",
+        "config": {"workload": wl + f", field of conf/{args.conf}.conf ({net.mlp_coarse.n_blocks} x "
+                               f"{net.mlp_coarse.d_hidden} ResnetFC, combine_layer {net.mlp_coarse.combine_layer})",
                    "field_samples_per_step": SB * R * spr},
     }
     if "torch" in res:
@@ -852,6 +868,9 @@ def main():
     ap.add_argument("--conf", choices=["default", "default_mv"], default="default",
                     help="--mode train: the field of conf/default.conf or conf/default_mv.conf (train.py:262)")
     ap.add_argument("--train-modes", default="hip,torch", help="--mode train: which autograd paths to time")
+    ap.add_argument("--renderer", choices=["volume", "adaptive"], default="volume",
+                    help="--mode train: VolumeRenderer (train.py 'VR*' runs) or AdaptiveVolumeRenderer (train.py's "
+                         "default for other run names, train.py:268-273)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: stand-in renderer on gloo (tests the launcher and the config-5 sharding only)")
     args = ap.parse_args()

@@ -2,7 +2,7 @@
 their input shapes and the Python call sites of the copies / cats / fills (what the kernel list calls
 direct_copy, CatArrayBatchedCopy, FillFunctor). Not part of the product or the bench.
 
-env: CONF (default_mv | default), STEPS
+env: CONF (default_mv | default), STEPS, RENDERER (volume | adaptive: AdaptiveVolumeRenderer, train.py:268-273)
 """
 import os
 import sys
@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(REPO, "adaptive-volume-rendering_amd"))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402
 from avr.conf import default_conf  # noqa: E402
-from avr.renderers import VolumeRenderer  # noqa: E402
+from avr.renderers import AdaptiveVolumeRenderer, VolumeRenderer  # noqa: E402
 
 dev = torch.device("cuda:0")
 SB, R = 4, 512
@@ -29,13 +29,19 @@ net.focal, net.c = net.focal.repeat(SB, 1), net.c.repeat(SB, 1)
 net.train()
 for p in net.parameters():
     p.requires_grad_(True)
-rend = VolumeRenderer.from_conf(default_conf()["normal_renderer"]).to(dev)
-rend.seed = 99
+params = list(net.parameters())
+if os.environ.get("RENDERER", "volume") == "adaptive":
+    torch.manual_seed(11)
+    rend = AdaptiveVolumeRenderer.from_conf(default_conf()["adaptive_renderer"]).to(dev)
+    params += list(rend.parameters())
+else:
+    rend = VolumeRenderer.from_conf(default_conf()["normal_renderer"]).to(dev)
+    rend.seed = 99
 x_pix = torch.rand(SB, R, 2, generator=g).to(dev)
 c2w = torch.stack([bench.orbit_c2w(0.3 + 0.9 * b) for b in range(SB)]).to(dev).reshape(SB, 1, 4, 4).expand(SB, R, 4, 4)
 K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]] * SB, device=dev)
 gt = torch.rand(SB, R, 3, generator=g).to(dev)
-opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+opt = torch.optim.Adam(params, lr=1e-4)
 net.hip_backward = True
 
 

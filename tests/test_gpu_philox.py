@@ -207,7 +207,7 @@ def _c3_philox_check(net, x_pix_np, precision):
     flips = np.flatnonzero(~same)
     sample_same = float((to_np(idx[S]) == aux["idx"][0]).mean())
     print(f"philox C3 {precision}: rays with the oracle's bins {same.mean():.5f} ({flips.size} bin flips)")
-    assert same.mean() >= 0.99, same.mean()
+    assert same.mean() >= 0.985, same.mean()   # r04b: 0.9915 (x3) / 0.9917 (fp32) of rays keep all 64 bins
     np.testing.assert_allclose(to_np(ff[S])[same], aux["field_fine"][0][same], atol=5e-5, rtol=1e-4)
     rgb_ref, depth_ref = o_f[0].copy(), o_d[0].copy()
     if flips.size:
@@ -233,6 +233,11 @@ def _c3_philox_check(net, x_pix_np, precision):
              "outliers": int((~ok).sum()), "outliers_not_bin_flips": int((~ok & same).sum()),
              "max_coarse_field_err": float(np.abs(to_np(fc[S]) - aux["field_coarse"][0]).max()),
              "max_coarse_rgb_err": float(np.abs(to_np(rgb_c[S]) - o_c[0]).max())})
-    assert ok.mean() >= 0.99, ok.mean()
+    # bar: the survey's >= 99.9 % is out of reach for ANY fp32 field on this random-init fog scene -- the strict
+    # fp32 kernel flips as many rays as x3 (r04b: fp32 34 / 4096 bin-flip rays, 6 outliers = 0.99854; x3 35 and 8
+    # = 0.99805; profiles/r04b_philox_c3_flip_rates.jsonl): the flips are fp32 noise of the coarse weights against
+    # the numpy oracle's own fp32 field at cdf steps (quirk Q3), not a cost of the split-fp16 products. Both
+    # precisions are held to 0.997 with every outlier a bin flip.
+    assert ok.mean() >= 0.997, ok.mean()
     assert not (~ok & same).any(), "a ray with the oracle's bins must match it"
     assert np.abs(to_np(r_c[0, S]) - o_c[0]).max() <= 1e-4
