@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -58,6 +58,23 @@ class WGradLayer(ctypes.Structure):
                 ("partial", c_void_p), ("bias_partial", c_void_p)]
 
 
+BN_FWD, BN_BWD = 0, 1
+BN_PLAIN, BN_RELU, BN_GRAD = 0, 1, 2
+
+
+class BnLayer(ctypes.Structure):
+    """avr_bn_layer (ABI 11): one layer GEMM of the training-mode BatchNorm path (see include/avr.h)."""
+    _fields_ = [("n_rows", i64), ("mode", c_int), ("prologue", c_int), ("in_dim", c_int), ("in_valid", c_int),
+                ("src", c_void_p), ("ld_src", i64), ("src_pre", c_void_p), ("src_res", c_void_p),
+                ("in_mu", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p),
+                ("in_m1", c_void_p), ("in_m2", c_void_p), ("in_invstd", c_void_p),
+                ("operand_out", c_void_p), ("operand_max", c_void_p),
+                ("blob", c_void_p), ("layer", c_int),
+                ("bias", c_void_p), ("add1", c_void_p), ("add2", c_void_p), ("out", c_void_p),
+                ("mask_rows", c_void_p), ("pre_rows", c_void_p), ("out_mu", c_void_p), ("out_invstd", c_void_p),
+                ("partial", c_void_p)]
+
+
 # name -> argtypes (all return int status)
 _SIGS = {
     "avr_world_rays": [c_void_p, c_void_p, c_void_p, i64, i64, i64, i64, c_void_p, c_void_p, c_void_p],
@@ -76,6 +93,10 @@ _SIGS = {
     "avr_sample_coarse_rays": [c_void_p, c_void_p, i64, c_int, c_void_p, u64, u64, c_void_p, c_void_p],
     "avr_raymarch": [ctypes.POINTER(ViewDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "avr_raymarch_train": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "avr_raymarch_bwd": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, i64, c_int, c_void_p, c_void_p, c_void_p],
     "avr_march_state_bytes": [i64, ctypes.POINTER(i64)],
     "avr_march_init": [i64, c_void_p, c_void_p, c_void_p],
     "avr_march_gather": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_int, c_int, c_int, c_void_p, c_void_p,
@@ -111,6 +132,13 @@ _SIGS = {
                                 ctypes.POINTER(c_void_p), c_void_p],
     "avr_latent_features": [ctypes.POINTER(ViewDesc), c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
     "avr_latent_features_batch": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
+    "avr_bn_layer_run": [ctypes.POINTER(FieldDims), ctypes.POINTER(BnLayer), c_void_p],
+    "avr_bn_stats": [c_void_p, i64, c_int, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_void_p],
+    "avr_bn_grad_stats": [c_void_p, i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p],
+    "avr_bn_grad_rows": [i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p],
     "avr_stream_copy": [c_void_p, c_void_p, i64, c_void_p],
     "avr_stream_fill": [c_void_p, i64, c_uint32, c_void_p],
 }

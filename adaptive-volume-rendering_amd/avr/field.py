@@ -218,16 +218,21 @@ class FusedField:
                          PRECISIONS[self.precision], int(uses_bn(mlp)), int(getattr(mlp, "use_spade", False)),
                          float(softplus_beta(mlp) or 0.0))
 
-    def packed(self, coarse):
+    def packed(self, coarse, bn_fold=True):
+        """bn_fold=False: the training-mode BatchNorm path's blob (avr.bn_train): x3, raw fc_0 weights (no
+        eval-BN folding, dims.bn = 0), cached beside the inference blob."""
         mlp = self._mlp(coarse)
         params = [p.detach() for p in mlp.parameters()] + [b for b in mlp.buffers() if b.is_floating_point()]
         # the precision is part of the key: an x3 blob holds only the fragments the x3 kernels read
         # (avr_field_pack), and net.fused() switches a FusedField's precision in place
-        key = (id(mlp), self.precision, _version_key(params))
-        hit = self._packed.get(coarse)
+        slot = coarse if bn_fold else (coarse, "bn_train")
+        key = (id(mlp), self.precision if bn_fold else "x3", _version_key(params))
+        hit = self._packed.get(slot)
         if hit is not None and hit[0] == key:
             return hit[1]
         dims = self.dims(mlp)
+        if not bn_fold:
+            dims.bn, dims.precision = 0, _lib.FIELD_X3
         n = ctypes.c_int64(0)
         _lib.check(_lib.load().avr_field_packed_floats(ctypes.byref(dims), ctypes.byref(n)), "avr_field_packed_floats")
         dev = params[0].device
@@ -265,7 +270,7 @@ class FusedField:
         entry = _Packed(dims, packed, None)
         entry._keep = keep
         entry.weights = w
-        self._packed[coarse] = (key, entry)
+        self._packed[slot] = (key, entry)
         return entry
 
     def packed_bwd(self, coarse, entry=None):
@@ -300,12 +305,13 @@ class FusedField:
         entry.tables[sb] = (key, table, lat)  # holding `lat` keeps its address from being reused
         return table
 
-    def tables_batch(self, coarse, n_scenes, fast=False):
+    def tables_batch(self, coarse, n_scenes, fast=False, bn_fold=True):
         """The lin_z tables of scenes 0 .. n_scenes-1 back to back, (n_scenes,
         max(n_tables, 1), H*W, d_hidden): one buffer for the multi-scene launches.
         fast (the training path, which recomputes them every step): on the split-fp16
-        GEMM (table_x3_kernel); otherwise exact fp32 products."""
-        entry = self.packed(coarse)
+        GEMM (table_x3_kernel); otherwise exact fp32 products. bn_fold: which blob's
+        cache holds them (packed())."""
+        entry = self.packed(coarse, bn_fold)
         lat = self.net.encoder.latent
         key = (n_scenes, bool(fast), lat.data_ptr(), lat._version, tuple(lat.shape))
         cache = entry.__dict__.setdefault("batch_tables", {})

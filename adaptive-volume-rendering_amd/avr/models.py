@@ -292,7 +292,17 @@ class NewPixelNeRFNet(nn.Module):
             return self.fused().forward_points_multiview(xyz, viewdirs, coarse)
         if not return_features and self.can_train_fused(xyz, viewdirs):
             return self.fused().forward_train(xyz, viewdirs, coarse)
+        if not return_features and self.can_train_bn(xyz, viewdirs):
+            from .bn_train import forward_train_bn
+            return forward_train_bn(self.fused(), xyz, viewdirs, coarse)
         return self.forward_torch(xyz, coarse, viewdirs, far, return_features)
+
+    def can_train_bn(self, xyz, viewdirs):
+        """train.py --bn in training mode (batch statistics): the layer-by-layer HIP path (avr.bn_train), with
+        or without autograd; points must not need gradients through it (view directions never)."""
+        from .bn_train import bn_train_eligible
+        return (self.use_fused and self.hip_backward and xyz.is_cuda and viewdirs is not None
+                and not viewdirs.requires_grad and xyz.shape[0] * xyz.shape[1] >= 2 and bn_train_eligible(self))
 
     def mlp_inputs(self, xyz, viewdirs, latent=None):
         """(latent features (SB*B, d_latent), z_feature (SB*B, d_in)) at the

@@ -23,7 +23,7 @@ from typing import Tuple
 import torch
 from torch import nn
 
-from . import ops
+from . import _lib, ops
 
 
 def _noise(shape, like, kind):
@@ -294,9 +294,32 @@ class _LSTMMarch(nn.Module):
         return (ros.shape[0] == 1 and not torch.is_grad_enabled() and hasattr(phi, "can_fuse")
                 and phi.can_fuse(ros) and phi.encoder.latent.shape[1] == self.n_feature_channels)
 
+    def can_train_fused(self, phi, ros, rds, init_dist):
+        """Autograd through the march on HIP (avr_raymarch_train / _bwd): the net's latent lookup is the fused
+        field's (bilinear / border, one source view per scene), the LSTM has its biases, and only the LSTM /
+        out_layer parameters and the latent may need gradients (cameras and start distances do not)."""
+        from .bn_train import bn_train_eligible
+        from .field import fused_eligible
+        if not (torch.is_grad_enabled() and ros.is_cuda and getattr(phi, "use_fused", False)
+                and getattr(phi, "hip_backward", False) and hasattr(phi, "fused")):
+            return False
+        if ros.requires_grad or rds.requires_grad or init_dist.requires_grad:
+            return False
+        lat = phi.encoder.latent
+        SB = ros.shape[0]
+        if not (1 <= SB <= _lib.AVR_MAX_SCENES and lat.shape[1] == self.n_feature_channels
+                and lat.shape[0] in (1, SB) and self.lstm.bias and self.lstm.hidden_size == 16):
+            return False
+        return fused_eligible(phi) or bn_train_eligible(phi)
+
     def march(self, ros, rds, init_dist, phi):
         """-> final world coordinates (SB, R, 3)."""
         SB, num_rays, _ = ros.shape
+        if self.can_train_fused(phi, ros, rds, init_dist):
+            self.last_path = "hip_train"
+            lstm, out = self.lstm, self.out_layer
+            return _MarchTrain.apply(self.steps, phi, ros, rds, init_dist, phi.encoder.latent, lstm.weight_ih,
+                                     lstm.weight_hh, lstm.bias_ih, lstm.bias_hh, out.weight, out.bias)
         if self.can_fuse(phi, ros):
             self.last_path = "fused"
             world, _ = ops.raymarch(phi.fused().view(0), self._gate_table(phi), self.lstm, self.out_layer,
@@ -314,6 +337,75 @@ class _LSTMMarch(nn.Module):
             world_coords.append(world_coords[-1] + rds * signed_distance)
             states.append(state)
         return world_coords[-1]
+
+
+class _MarchTrain(torch.autograd.Function):
+    """Autograd of the LSTM march (renderers.py:413-432 / :320-343) on HIP: forward avr_raymarch_train on the
+    per-texel gate tables (latent^T W_ih^T, one library GEMM per scene), backward avr_raymarch_bwd (reverse
+    steps per ray: out_layer, the clamp hook, LSTMCell, the lookup's table and position gradients), then W_ih's
+    and the latent's gradients from the table gradient (two more GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, steps, phi, ros, rds, init_dist, latent, w_ih, w_hh, b_ih, b_hh, w_out, b_out):
+        SB, R, _ = ros.shape
+        dev = ros.device
+        fused = phi.fused()
+        with torch.no_grad():
+            lat = latent.detach().float()
+            L, C, H, W = lat.shape
+            lat_t = lat.reshape(L, C, H * W)
+            tables = torch.matmul(lat_t.transpose(1, 2), w_ih.detach().float().t())        # (L, H*W, 64)
+            if L != SB:
+                tables = tables.expand(SB, -1, -1)
+            tables = tables.contiguous()
+            n = SB * R
+            world = torch.empty(n, 3, device=dev, dtype=torch.float32)
+            trace = torch.empty(steps + 1, n, 3, device=dev, dtype=torch.float32)
+            state = torch.empty(max(steps, 1), n, 96, device=dev, dtype=torch.float32)
+            views = (_lib.ViewDesc * SB)(*[fused.view(s) for s in range(SB)])
+            P = [t.detach().float().contiguous() for t in (w_hh, b_ih, b_hh, w_out, b_out)]
+            ro = ros.detach().float().reshape(n, 3).contiguous()
+            rd = rds.detach().float().reshape(n, 3).contiguous()
+            d0 = init_dist.detach().float().reshape(n).contiguous()
+            _lib.call("avr_raymarch_train", views, SB, _lib.ptr(tables), *[_lib.ptr(t) for t in P], _lib.ptr(ro),
+                      _lib.ptr(rd), _lib.ptr(d0), R, steps, _lib.ptr(world), _lib.ptr(trace), _lib.ptr(state),
+                      _lib.stream_of(world))
+        ctx.steps, ctx.phi, ctx.views, ctx.L = steps, phi, views, L
+        ctx.keep = (tables, trace, state, rd, P, lat_t)
+        ctx.save_for_backward(latent, w_ih)
+        return world.reshape(SB, R, 3)
+
+    @staticmethod
+    def backward(ctx, grad_world):
+        latent, w_ih = ctx.saved_tensors
+        tables, trace, state, rd, P, lat_t = ctx.keep
+        ctx.keep = None
+        SB = tables.shape[0]
+        n = rd.shape[0]
+        R = n // SB
+        with torch.no_grad():
+            d_tab = torch.zeros_like(tables)
+            d_grads = torch.zeros(64 * 16 + 64 + 16 + 1, device=rd.device, dtype=torch.float32)
+            gw = grad_world.float().reshape(n, 3).contiguous()
+            _lib.call("avr_raymarch_bwd", ctx.views, SB, _lib.ptr(tables), _lib.ptr(P[0]), _lib.ptr(P[3]),
+                      _lib.ptr(rd), _lib.ptr(trace), _lib.ptr(state), _lib.ptr(gw), R, ctx.steps, _lib.ptr(d_tab),
+                      _lib.ptr(d_grads), _lib.stream_of(gw))
+            d_whh = d_grads[:1024].reshape(64, 16)
+            d_b = d_grads[1024:1088]
+            d_wout = d_grads[1088:1104].reshape(1, 16)
+            d_bout = d_grads[1104:1105]
+            if ctx.L == SB:
+                d_wih = torch.einsum("sth,sct->hc", d_tab, lat_t)
+            else:
+                d_wih = torch.einsum("th,ct->hc", d_tab.sum(0), lat_t[0])
+            d_lat = None
+            if ctx.needs_input_grad[5] and not getattr(ctx.phi, "stop_encoder_grad", False):
+                dl = torch.matmul(d_tab, w_ih.detach().float())                         # (SB, H*W, C)
+                if ctx.L != SB:
+                    dl = dl.sum(0, keepdim=True)
+                d_lat = dl.transpose(1, 2).reshape(latent.shape).to(latent.dtype)
+        return (None, None, None, None, None, d_lat, d_wih.to(w_ih.dtype), d_whh, d_b.clone(), d_b.clone(), d_wout,
+                d_bout)
 
 
 class Raymarcher(_LSTMMarch):

@@ -11,7 +11,7 @@ import torch
 INTRINSICS = [[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]
 
 
-def synthetic_scene(device, seed=0, conf=None, latent_hw=(64, 64), sigma_bias=0.0):
+def synthetic_scene(device, seed=0, conf=None, latent_hw=(64, 64), sigma_bias=0.0, bn=False):
     """NewPixelNeRFNet on `device` (eval, no grad) with the synthetic latent
     and source view. sigma_bias is added to both MLPs' density output bias
     (0 = the measured fog of a random-init field; > 0 makes rays saturate,
@@ -19,7 +19,7 @@ def synthetic_scene(device, seed=0, conf=None, latent_hw=(64, 64), sigma_bias=0.
     from .conf import default_conf
     from .models import NewPixelNeRFNet
     torch.manual_seed(seed)
-    net = NewPixelNeRFNet(conf if conf is not None else default_conf()["model"])
+    net = NewPixelNeRFNet(conf if conf is not None else default_conf()["model"], bn=bn)   # bn: train.py --bn
     with torch.no_grad():
         for mlp in (net.mlp_coarse, net.mlp_fine):
             for blk in mlp.blocks:

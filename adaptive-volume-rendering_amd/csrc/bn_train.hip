@@ -1,0 +1,427 @@
+// Training-mode BatchNorm of ResnetFC(bn=True) on the HIP path: train.py --bn (train.py:210, :265) builds
+// ResnetBlockFC(bn=True), whose forward is relu(bn_0(x)) -> fc_0 -> relu(bn_0(net)) -> fc_1, + x
+// (models.py:454-461; bn_0 applied twice, bn_1 unused), with batch statistics over every row of the field
+// call in training mode.
+//
+// The fused field kernels carry a 64-sample tile through every layer in one workgroup; batch statistics are a
+// reduction over all rows between two GEMMs, so this net runs layer by layer. One launch per GEMM over
+// row-major fp32 rows (bn_layer_kernel): the operand -- the layer input normalised and relu'd (forward), or
+// the BatchNorm backward of the gradient (backward) -- is built in the prologue from the rows, split into
+// fp16 hi/lo under one power-of-two scale per workgroup and staged in LDS in the fused kernels' B-fragment
+// order; the K loop is theirs (x3: three v_mfma_f32_16x16x32_f16 per product, fp32 accumulate, weights
+// streamed one chunk ahead); the epilogue adds bias / residual / lin_z rows (forward) or applies the relu mask
+// (backward), stores the rows and reduces this workgroup's column statistics. A finalize launch between
+// layers (bn_stats_kernel / bn_grad_stats_kernel) combines the workgroups' partials in fp64.
+#include "x3_gemm.h"
+
+namespace avr {
+
+struct BnArgs {
+  int64_t M;
+  int prologue, kin, K;
+  const float* src; int64_t ld_src;
+  const float* src_pre; const float* src_res;
+  const float* in_mu; const float* in_scale; const float* in_shift;
+  const float* in_m1; const float* in_m2; const float* in_invstd;
+  float* opnd_out; unsigned* opnd_max;
+  const float* w;               // this layer's x3 fragments (chunk 0, tile 0)
+  const unsigned* hdr; int hdr_idx;   // the blob header's max |W| bits of the layer (the pack's power-of-two scale)
+  int KC;
+  const float* bias; const float* add1; const float* add2;
+  float* out;
+  const float* mask_rows; const float* pre_rows; const float* out_mu; const float* out_invstd;
+  float* part;
+};
+
+__device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
+
+// 16 lanes of one lane group g (lanes 16g .. 16g + 15): sum over j
+__device__ __forceinline__ floatx4 sum16(floatx4 v) {
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) {
+    v.x += __shfl_xor(v.x, d, 64);
+    v.y += __shfl_xor(v.y, d, 64);
+    v.z += __shfl_xor(v.z, d, 64);
+    v.w += __shfl_xor(v.w, d, 64);
+  }
+  return v;
+}
+
+template <int FT, int NW, bool TWO>
+__device__ __forceinline__ void bn_gemm(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W, int KC,
+                                        int cstride, const uint4* X16, int lane) {
+  if constexpr (TWO)
+    gemm_x3_sg<FT, true, FT>(acc, A0, W, KC, cstride, X16, lane);
+  else
+    gemm_x3<FT, true, false>(acc, A0, W, KC, cstride, X16, lane);
+}
+
+// MODE 0 forward, 1 backward. Workgroup = 64 rows; lane = row in the prologue (wave w builds the operand
+// columns [K/NW * w, K/NW * (w + 1)) of all 64 rows: one 16-B load per row and column group, written into
+// the slots of its sample -- conflict-free LDS stores), then the fused kernels' GEMM and register layout:
+// lane (g, j) of wave w holds features 16 (FT w + ft) + 4 g .. +3 of rows 16 sg + j.
+template <int FT, int NW, int MODE>
+__global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
+  constexpr int HID = 16 * FT * NW, NTT = FT * NW;
+  constexpr bool TWO = NW > 4;
+  constexpr int MAXQ = 512 / 4 / NW;        // operand column groups per wave (K <= 512)
+  extern __shared__ float lds[];
+  uint4* X16 = reinterpret_cast<uint4*>(lds);
+  float* red = lds + a.KC * 2048;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int64_t m0 = (int64_t)blockIdx.x * kX3Samples;
+  const int nvalid = a.M - m0 < kX3Samples ? (int)(a.M - m0) : kX3Samples;
+  const uint4* W = reinterpret_cast<const uint4*>(a.w) + 2 * 64 * FT * wid;
+  FragX3 A0[FT];
+  prefetch_a<FT, TWO ? FT : kPrefetch>(A0, W, lane);
+
+  // ---------------------------------------------------------------- operand
+  const int qpw = a.K / 4 / NW;              // column groups of this wave
+  const bool valid = lane < nvalid;
+  const int64_t row = m0 + (valid ? lane : 0);
+  floatx4 xv[MAXQ];
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXQ; ++i) {
+    xv[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (i < qpw) {
+      const int k = 4 * (qpw * wid + i);
+      floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (k + 4 <= a.kin) {
+        v = ld4(a.src + row * a.ld_src + k);
+      } else if (k < a.kin) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = k + r < a.kin ? a.src[row * a.ld_src + k + r] : 0.f;
+      }
+      if (k < a.kin) {
+        if (a.prologue == AVR_BN_RELU) {
+          const floatx4 mu = ld4(a.in_mu + k), sc = ld4(a.in_scale + k), sh = ld4(a.in_shift + k);
+          v = (v - mu) * sc + sh;
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        } else if (a.prologue == AVR_BN_GRAD) {
+          const floatx4 xh = (ld4(a.src_pre + row * a.ld_src + k) - ld4(a.in_mu + k)) * ld4(a.in_invstd + k);
+          v = (v - ld4(a.in_m1 + k) - xh * ld4(a.in_m2 + k)) * ld4(a.in_scale + k);
+          if (a.src_res) v += ld4(a.src_res + row * a.ld_src + k);
+        }
+      }
+      if (!valid) v = floatx4{0.f, 0.f, 0.f, 0.f};
+      else if (a.opnd_out)
+        __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a.opnd_out + (m0 + lane) * a.K + k));
+      xv[i] = v;
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wid] = mx;
+  lds_barrier();
+  const float wgmax = red_max<NW>(red);
+  if (a.opnd_max && wid == 0 && lane == 0 && wgmax > 0.f) atomicMax(a.opnd_max, __float_as_uint(wgmax));
+  const float s_x = pow2_scale_for(wgmax);
+  char* xb = reinterpret_cast<char*>(X16);
+#pragma unroll
+  for (int i = 0; i < MAXQ; ++i) {
+    if (i < qpw) {
+      const int k = 4 * (qpw * wid + i);
+      uint2 hi, lo;
+      split4(xv[i], s_x, hi, lo);
+      const int c = k >> 5, gq = (k >> 2) & 3, half = (k >> 4) & 1;
+      *reinterpret_cast<uint2*>(xb + xidx(c, 0, gq, lane) * 16 + 8 * half) = hi;
+      *reinterpret_cast<uint2*>(xb + xidx(c, 1, gq, lane) * 16 + 8 * half) = lo;
+    }
+  }
+  lds_barrier();
+
+  // ---------------------------------------------------------------- GEMM
+  floatx4 acc[FT][4];
+  bn_gemm<FT, NW, TWO>(acc, A0, W, a.KC, 64 * NTT, X16, lane);
+  const float inv = 1.0f / (pow2_scale_for(__uint_as_float(a.hdr[a.hdr_idx])) * s_x);
+
+  // ---------------------------------------------------------------- epilogue
+  float* part = a.part + (int64_t)blockIdx.x * 2 * HID;
+  const float rn = 1.0f / (float)nvalid;
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    const int f0 = 16 * (FT * wid + ft) + 4 * g;
+    floatx4 s1 = floatx4{0.f, 0.f, 0.f, 0.f}, s2 = s1;
+    if constexpr (MODE == AVR_BN_FWD) {
+      const floatx4 b = a.bias ? ld4(a.bias + f0) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        const int s = 16 * sg + j;
+        const int64_t m = m0 + (s < nvalid ? s : 0);
+        floatx4 y = acc[ft][sg] * inv + b;
+        if (a.add1) y += ld4(a.add1 + m * HID + f0);
+        if (a.add2) y += ld4(a.add2 + m * HID + f0);
+        acc[ft][sg] = y;
+        if (s < nvalid) {
+          *reinterpret_cast<floatx4*>(a.out + m * HID + f0) = y;
+          s1 += y;
+        }
+      }
+      const floatx4 mean = sum16(s1) * rn;     // this workgroup's column means, then sum of squared deviations
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        const floatx4 d = acc[ft][sg] - mean;
+        if (16 * sg + j < nvalid) s2 += d * d;
+      }
+      s2 = sum16(s2);
+      s1 = mean;
+    } else {
+      const floatx4 mu = ld4(a.out_mu + f0), is = ld4(a.out_invstd + f0);
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        const int s = 16 * sg + j;
+        const int64_t m = m0 + (s < nvalid ? s : 0);
+        const floatx4 d = acc[ft][sg] * inv;
+        const floatx4 z = ld4(a.mask_rows + m * HID + f0);
+        floatx4 gp;
+        gp.x = z.x > 0.f ? d.x : 0.f; gp.y = z.y > 0.f ? d.y : 0.f;
+        gp.z = z.z > 0.f ? d.z : 0.f; gp.w = z.w > 0.f ? d.w : 0.f;
+        if (s < nvalid) {
+          *reinterpret_cast<floatx4*>(a.out + m * HID + f0) = gp;
+          const floatx4 xh = (ld4(a.pre_rows + m * HID + f0) - mu) * is;
+          s1 += gp;
+          s2 += gp * xh;
+        }
+      }
+      s1 = sum16(s1);
+      s2 = sum16(s2);
+    }
+    if (j == 0) {
+      *reinterpret_cast<floatx4*>(part + f0) = s1;
+      *reinterpret_cast<floatx4*>(part + HID + f0) = s2;
+    }
+  }
+}
+
+template <int FT, int NW, int MODE>
+static int launch_bn_layer(const BnArgs& a, hipStream_t s) {
+  const size_t shm = (size_t)a.KC * 8192 + 64;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&bn_layer_kernel<FT, NW, MODE>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 16 * 8192 + 64) != hipSuccess)
+      return fail(AVR_E_HIP, "bn_layer_kernel: cannot set dynamic LDS");
+    attr = true;
+  }
+  const int64_t blocks = (a.M + kX3Samples - 1) / kX3Samples;
+  AVR_REQUIRE(blocks < (1ll << 31), "avr_bn_layer_run: too many rows");
+  bn_layer_kernel<FT, NW, MODE><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
+  return check_launch("bn_layer_kernel");
+}
+
+template <int MODE>
+static int dispatch_bn_layer(int H, const BnArgs& a, hipStream_t s) {
+  switch (H) {
+    case 64: return launch_bn_layer<1, 4, MODE>(a, s);
+    case 128: return launch_bn_layer<2, 4, MODE>(a, s);
+    case 256: return launch_bn_layer<4, 4, MODE>(a, s);
+    case 512: return launch_bn_layer<4, 8, MODE>(a, s);
+  }
+  return fail(AVR_E_UNSUPPORTED, "avr_bn_layer_run: d_hidden %d", H);
+}
+
+// ------------------------------------------------------------------ finalize
+// Block = 256 threads over 16 columns: thread (w, c) combines the partials of workgroups w, w + 16, ... of
+// column c in fp64, then the 16 threads of a column meet in LDS.
+constexpr int kBnCols = 16, kBnLanesPerCol = 16;
+
+__global__ void __launch_bounds__(256) bn_stats_kernel(const float* __restrict__ part, int64_t M, int N,
+                                                       const float* __restrict__ gamma, float eps, float momentum,
+                                                       float* running_mean, float* running_var, float* mu_out,
+                                                       float* invstd_out, float* scale_out) {
+  __shared__ double sn[256], smean[256], sm2[256];
+  const int c = blockIdx.x * kBnCols + (threadIdx.x % kBnCols);
+  const int w0 = threadIdx.x / kBnCols;
+  const int64_t nwg = (M + kX3Samples - 1) / kX3Samples;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  if (c < N) {
+    for (int64_t w = w0; w < nwg; w += kBnLanesPerCol) {   // Chan: combine (n, mean, M2) of two sets
+      const double nb = (double)(M - w * kX3Samples < kX3Samples ? M - w * kX3Samples : kX3Samples);
+      const double mb = part[w * 2 * N + c], m2b = part[w * 2 * N + N + c];
+      const double nt = n + nb, d = mb - mean;
+      mean += d * nb / nt;
+      m2 += m2b + d * d * n * nb / nt;
+      n = nt;
+    }
+  }
+  sn[threadIdx.x] = n; smean[threadIdx.x] = mean; sm2[threadIdx.x] = m2;
+  __syncthreads();
+  if (w0 == 0 && c < N) {
+    for (int t = 1; t < kBnLanesPerCol; ++t) {
+      const int i = t * kBnCols + threadIdx.x;
+      const double nb = sn[i];
+      if (nb == 0.0) continue;
+      const double nt = n + nb, d = smean[i] - mean;
+      mean += d * nb / nt;
+      m2 += sm2[i] + d * d * n * nb / nt;
+      n = nt;
+    }
+    const double var = m2 / n;                                  // biased: the normalisation (torch)
+    const float istd = (float)(1.0 / sqrt(var + (double)eps));
+    mu_out[c] = (float)mean;
+    invstd_out[c] = istd;
+    scale_out[c] = gamma[c] * istd;
+    if (running_mean) {                                         // torch: unbiased variance in the running stat
+      const float unb = (float)(n > 1.0 ? m2 / (n - 1.0) : var);
+      running_mean[c] = momentum * (float)mean + (1.0f - momentum) * running_mean[c];
+      running_var[c] = momentum * unb + (1.0f - momentum) * running_var[c];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_grad_stats_kernel(const float* __restrict__ part, int64_t M, int N,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ invstd, float* coef, float* m1,
+                                                            float* m2, float* dgamma, float* dbeta) {
+  __shared__ double s1[256], s2[256];
+  const int c = blockIdx.x * kBnCols + (threadIdx.x % kBnCols);
+  const int w0 = threadIdx.x / kBnCols;
+  const int64_t nwg = (M + kX3Samples - 1) / kX3Samples;
+  double a = 0.0, b = 0.0;
+  if (c < N)
+    for (int64_t w = w0; w < nwg; w += kBnLanesPerCol) {
+      a += part[w * 2 * N + c];
+      b += part[w * 2 * N + N + c];
+    }
+  s1[threadIdx.x] = a; s2[threadIdx.x] = b;
+  __syncthreads();
+  if (w0 == 0 && c < N) {
+    for (int t = 1; t < kBnLanesPerCol; ++t) {
+      a += s1[t * kBnCols + threadIdx.x];
+      b += s2[t * kBnCols + threadIdx.x];
+    }
+    m1[c] = (float)(a / (double)M);
+    m2[c] = (float)(b / (double)M);
+    coef[c] = gamma[c] * invstd[c];
+    dbeta[c] += (float)a;       // bn_0 is applied twice per block: both applications add into its gradients
+    dgamma[c] += (float)b;
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_grad_rows_kernel(int64_t n4, int N4, const floatx4* __restrict__ gr,
+                                                           const floatx4* __restrict__ pre,
+                                                           const floatx4* __restrict__ res,
+                                                           const floatx4* __restrict__ coef,
+                                                           const floatx4* __restrict__ m1,
+                                                           const floatx4* __restrict__ m2,
+                                                           const floatx4* __restrict__ mu,
+                                                           const floatx4* __restrict__ invstd, floatx4* out,
+                                                           unsigned* out_max) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float mx = 0.f;
+  if (i < n4) {
+    const int c = (int)(i % N4);
+    const floatx4 xh = (pre[i] - mu[c]) * invstd[c];
+    floatx4 v = (gr[i] - m1[c] - xh * m2[c]) * coef[c];
+    if (res) v += res[i];
+    out[i] = v;
+    mx = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+  }
+  mx = wave_max(mx);
+  if (out_max && (threadIdx.x & 63) == 0 && mx > 0.f) atomicMax(out_max, __float_as_uint(mx));
+}
+
+}  // namespace avr
+
+using namespace avr;
+
+extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* l, void* stream) {
+  Layout L;
+  int rc = field_layout(dims, &L);
+  if (rc) return rc;
+  AVR_REQUIRE(l, "avr_bn_layer_run: null layer");
+  AVR_REQUIRE(dims->precision == AVR_FIELD_X3 && !dims->bn && !dims->spade && !(dims->beta > 0.f),
+              "avr_bn_layer_run: an x3 blob packed without eval-BN folding (dims->bn = 0), ReLU, no use_spade");
+  AVR_REQUIRE(l->mode == AVR_BN_FWD || l->mode == AVR_BN_BWD, "avr_bn_layer_run: bad mode %d", l->mode);
+  AVR_REQUIRE(l->prologue >= AVR_BN_PLAIN && l->prologue <= AVR_BN_GRAD, "avr_bn_layer_run: bad prologue");
+  AVR_REQUIRE(l->n_rows >= 0, "avr_bn_layer_run: bad row count");
+  if (l->n_rows == 0) return AVR_OK;
+  const int H = dims->d_hidden, nb = dims->n_blocks;
+  BnArgs a{};
+  a.M = l->n_rows;
+  a.prologue = l->prologue;
+  a.K = l->in_dim;
+  a.kin = l->in_valid;
+  a.KC = l->in_dim / 32;
+  AVR_REQUIRE(l->in_dim % 64 == 0 && l->in_dim >= 64 && l->in_dim <= 512 && l->in_dim / 4 % (H == 512 ? 8 : 4) == 0,
+              "avr_bn_layer_run: in_dim %d", l->in_dim);
+  AVR_REQUIRE(l->in_valid > 0 && l->in_valid <= l->in_dim, "avr_bn_layer_run: in_valid %d", l->in_valid);
+  AVR_REQUIRE(l->src && l->out && l->partial && l->blob, "avr_bn_layer_run: null pointer");
+  AVR_REQUIRE(l->ld_src >= l->in_valid && l->ld_src % 4 == 0,
+              "avr_bn_layer_run: ld_src %lld (>= in_valid, a multiple of 4: 16-B rows)", (long long)l->ld_src);
+  AVR_REQUIRE(l->prologue != AVR_BN_RELU || (l->in_mu && l->in_scale && l->in_shift),
+              "avr_bn_layer_run: AVR_BN_RELU needs in_mu / in_scale / in_shift");
+  AVR_REQUIRE(l->prologue != AVR_BN_GRAD || (l->src_pre && l->in_mu && l->in_scale && l->in_m1 && l->in_m2 &&
+                                             l->in_invstd),
+              "avr_bn_layer_run: AVR_BN_GRAD needs src_pre, in_mu / scale / m1 / m2 / invstd");
+  a.src = l->src; a.ld_src = l->ld_src; a.src_pre = l->src_pre; a.src_res = l->src_res;
+  a.in_mu = l->in_mu; a.in_scale = l->in_scale; a.in_shift = l->in_shift;
+  a.in_m1 = l->in_m1; a.in_m2 = l->in_m2; a.in_invstd = l->in_invstd;
+  a.opnd_out = l->operand_out;
+  a.opnd_max = l->operand_max;
+  // the layer's fragments and its header word (0 lin_in, 2 + 2b fc_0[b], 3 + 2b fc_1[b])
+  const int ly = l->layer;
+  AVR_REQUIRE(ly == 0 || (ly >= 2 && ly < 2 + 2 * nb), "avr_bn_layer_run: layer %d", ly);
+  const unsigned* hdr;
+  if (l->mode == AVR_BN_FWD) {
+    AVR_REQUIRE(ly != 0 || l->in_dim == 64, "avr_bn_layer_run: lin_in's operand is 64 columns");
+    AVR_REQUIRE(ly == 0 || l->in_dim == H, "avr_bn_layer_run: a hidden layer's operand is d_hidden columns");
+    a.w = l->blob + (ly == 0 ? L.x3_in : (ly % 2 == 0 ? L.x3_fc0[(ly - 2) / 2] : L.x3_fc1[(ly - 2) / 2]));
+    hdr = reinterpret_cast<const unsigned*>(l->blob + L.x3_hdr);
+    a.bias = l->bias; a.add1 = l->add1; a.add2 = l->add2;
+  } else {
+    AVR_REQUIRE(ly >= 2 && l->in_dim == H, "avr_bn_layer_run: the backward runs fc_0 / fc_1 (d_hidden columns)");
+    AVR_REQUIRE(l->mask_rows && l->pre_rows && l->out_mu && l->out_invstd,
+                "avr_bn_layer_run: AVR_BN_BWD needs mask_rows, pre_rows, out_mu, out_invstd");
+    BwdLayout LB;
+    if ((rc = field_bwd_layout(dims, &LB))) return rc;
+    a.w = l->blob + (ly % 2 == 0 ? LB.fc0t[(ly - 2) / 2] : LB.fc1t[(ly - 2) / 2]);
+    hdr = reinterpret_cast<const unsigned*>(l->blob);
+    a.mask_rows = l->mask_rows; a.pre_rows = l->pre_rows; a.out_mu = l->out_mu; a.out_invstd = l->out_invstd;
+  }
+  a.hdr = hdr;
+  a.hdr_idx = ly;
+  a.out = l->out;
+  a.part = l->partial;
+  hipStream_t s = as_stream(stream);   // the weight scale is read on the device (the pack launch wrote it)
+  return l->mode == AVR_BN_FWD ? dispatch_bn_layer<AVR_BN_FWD>(H, a, s) : dispatch_bn_layer<AVR_BN_BWD>(H, a, s);
+}
+
+extern "C" int avr_bn_stats(const float* partial, int64_t n_rows, int n_cols, const float* gamma, float eps,
+                            float momentum, float* running_mean, float* running_var, float* mu, float* invstd,
+                            float* scale, void* stream) {
+  AVR_REQUIRE(n_rows >= 2, "avr_bn_stats: BatchNorm in training mode needs more than 1 value per channel");
+  AVR_REQUIRE(n_cols > 0 && partial && gamma && mu && invstd && scale, "avr_bn_stats: bad argument");
+  AVR_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "avr_bn_stats: running mean / var together");
+  bn_stats_kernel<<<(unsigned)((n_cols + kBnCols - 1) / kBnCols), 256, 0, as_stream(stream)>>>(
+      partial, n_rows, n_cols, gamma, eps, momentum, running_mean, running_var, mu, invstd, scale);
+  return check_launch("bn_stats_kernel");
+}
+
+extern "C" int avr_bn_grad_stats(const float* partial, int64_t n_rows, int n_cols, const float* gamma,
+                                 const float* invstd, float* coef, float* m1, float* m2, float* dgamma, float* dbeta,
+                                 void* stream) {
+  AVR_REQUIRE(n_rows >= 1 && n_cols > 0, "avr_bn_grad_stats: bad sizes");
+  AVR_REQUIRE(partial && gamma && invstd && coef && m1 && m2 && dgamma && dbeta, "avr_bn_grad_stats: null pointer");
+  bn_grad_stats_kernel<<<(unsigned)((n_cols + kBnCols - 1) / kBnCols), 256, 0, as_stream(stream)>>>(
+      partial, n_rows, n_cols, gamma, invstd, coef, m1, m2, dgamma, dbeta);
+  return check_launch("bn_grad_stats_kernel");
+}
+
+extern "C" int avr_bn_grad_rows(int64_t n_rows, int n_cols, const float* g, const float* pre, const float* res,
+                                const float* coef, const float* m1, const float* m2, const float* mu,
+                                const float* invstd, float* out, uint32_t* out_max, void* stream) {
+  AVR_REQUIRE(n_rows >= 0 && n_cols > 0 && n_cols % 4 == 0, "avr_bn_grad_rows: bad sizes");
+  if (n_rows == 0) return AVR_OK;
+  AVR_REQUIRE(g && pre && coef && m1 && m2 && mu && invstd && out, "avr_bn_grad_rows: null pointer");
+  const int64_t n4 = n_rows * (n_cols / 4);
+  bn_grad_rows_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, as_stream(stream)>>>(
+      n4, n_cols / 4, reinterpret_cast<const floatx4*>(g), reinterpret_cast<const floatx4*>(pre),
+      reinterpret_cast<const floatx4*>(res), reinterpret_cast<const floatx4*>(coef),
+      reinterpret_cast<const floatx4*>(m1), reinterpret_cast<const floatx4*>(m2),
+      reinterpret_cast<const floatx4*>(mu), reinterpret_cast<const floatx4*>(invstd),
+      reinterpret_cast<floatx4*>(out), out_max);
+  return check_launch("bn_grad_rows_kernel");
+}

@@ -102,6 +102,13 @@ static int make_bwd_layout(const avr_field_dims* d, BwdLayout* LB) {
   return AVR_OK;
 }
 
+int field_layout(const avr_field_dims* d, Layout* L) { return make_layout(d, L); }
+int field_bwd_layout(const avr_field_dims* d, BwdLayout* LB) {
+  Layout L;
+  const int rc = make_layout(d, &L);
+  return rc ? rc : make_bwd_layout(d, LB);
+}
+
 // ----------------------------------------------------------------- packing
 // fp32 fragments: dst[(t*NTo + ot)*64 + l][r] = W[16ot + (l&15)][16t + 4(l>>4) + r] (zero padded);
 // bias vectors: dst[i] = a[i] + b[i] (b may be null), zero beyond n.

@@ -291,6 +291,10 @@ __device__ __forceinline__ float pow2_scale_for(float maxabs) {
 }
 
 int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s);
+// The packed blob's layout for dims (field.hip make_layout / make_bwd_layout), for the kernels of other units
+// (bn_train.hip: the layer-by-layer BatchNorm training GEMMs read the same fragments).
+int field_layout(const avr_field_dims* d, Layout* L);
+int field_bwd_layout(const avr_field_dims* d, BwdLayout* LB);
 // lin_z / scale_z tables on the x3 GEMM (L.x3_tables): table[t][texel][d_hidden], t < L.n_tables, for
 // n_scenes latent maps (stride d_latent * HW) into tables back to back (stride max(n_tables, 1) * HW * d_hidden)
 int dispatch_table_x3(const float* packed, const Layout& L, const float* latent, int HW, int d_latent, int d_hidden,

@@ -84,9 +84,320 @@ __global__ void __launch_bounds__(256) raymarch_kernel(View v, const float* __re
   if (k == 0 && final_dist) final_dist[ray] = fdiv(fsub(x0, r0), e0);   // renderers.py:490 (x component only)
 }
 
+// ------------------------------------------------------------------ training (ABI 11)
+// The same march with autograd for train.py (AdaptiveVolumeRenderer / Raymarcher training: the reference
+// backpropagates through 10 LSTMCell steps on grid_sample'd 512-channel features, renderers.py:413-432,
+// :320-343, ~half of the train step in torch.profiler, profiles/r04b_train_profile_adaptive_mv.log).
+// Forward: the kernel above over SB scenes (ray r of scene r / n_per_scene, its view and gate table), storing
+// per step the point, h, c and the four gate activations. Backward, one ray per 16 lanes in reverse step order:
+//   dsd = rd . dx;  dh = clamp(w_out dsd + W_hh^T dg_next, -10, 10)   (the reference's hook on state[0])
+//   LSTMCell backward -> dg (64 gate pre-activations)
+//   d table[texel] += w_corner dg (atomics: W_ih's gradient is then dT^T latent, the latent's W_ih^T dT)
+//   dx += R^T d(xc) of the bilinear lookup's position gradient (grid_sample border / align_corners=True
+//         backward: zero where the coordinate was clipped)
+// with W_hh, the biases and out_layer's gradients summed per workgroup.
+struct MarchScenes {
+  View v[AVR_MAX_SCENES];
+};
+constexpr int kMarchState = 6 * kHid;   // per ray and step: h, c, i, f, g, o
+
+// Lookup geometry of a point with the derivatives of the continuous texel coordinates (ix, iy) with respect
+// to the camera point xc (models.py:753-760, SpatialEncoder.index :260-273, grid_sample align_corners=True,
+// border: clipped coordinates have zero gradient, torch's clip_coordinates_set_grad).
+struct LookupGrad {
+  Bilinear bl;
+  float wx0, wx1, wy0, wy1;
+  float dix[3], diy[3];   // d ix / d xc, d iy / d xc (0 where clipped)
+};
+
+__device__ __forceinline__ LookupGrad lookup_grad(const View& v, float x0, float x1, float x2) {
+  LookupGrad L;
+  const float xr0 = dot3(v.R + 0, x0, x1, x2), xr1 = dot3(v.R + 3, x0, x1, x2), xr2 = dot3(v.R + 6, x0, x1, x2);
+  const float xc0 = fadd(xr0, v.t[0]), xc1 = fadd(xr1, v.t[1]), xc2 = fadd(xr2, v.t[2]);
+  const float u = fadd(fmul(fdiv(-xc0, xc2), v.focal[0]), v.c[0]);
+  const float w = fadd(fmul(fdiv(-xc1, xc2), v.focal[1]), v.c[1]);
+  const float gx = fsub(fmul(u, v.scale[0]), 1.0f), gy = fsub(fmul(w, v.scale[1]), 1.0f);
+  const float ixr = fmul(fdiv(fadd(gx, 1.0f), 2.0f), (float)(v.W - 1));
+  const float iyr = fmul(fdiv(fadd(gy, 1.0f), 2.0f), (float)(v.H - 1));
+  const float ix = fminf(fmaxf(ixr, 0.f), (float)(v.W - 1));
+  const float iy = fminf(fmaxf(iyr, 0.f), (float)(v.H - 1));
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  L.wx1 = fsub(ix, fx0); L.wy1 = fsub(iy, fy0);
+  L.wx0 = fsub(fadd(fx0, 1.0f), ix); L.wy0 = fsub(fadd(fy0, 1.0f), iy);
+  const int X0 = (int)fx0, Y0 = (int)fy0;
+  const int X1 = X0 + 1 < v.W ? X0 + 1 : v.W - 1, Y1 = Y0 + 1 < v.H ? Y0 + 1 : v.H - 1;
+  L.bl.tex[0] = Y0 * v.W + X0; L.bl.w[0] = fmul(L.wx0, L.wy0);
+  L.bl.tex[1] = Y0 * v.W + X1; L.bl.w[1] = fmul(L.wx1, L.wy0);
+  L.bl.tex[2] = Y1 * v.W + X0; L.bl.w[2] = fmul(L.wx0, L.wy1);
+  L.bl.tex[3] = Y1 * v.W + X1; L.bl.w[3] = fmul(L.wx1, L.wy1);
+  const bool cx = ixr > 0.f && ixr < (float)(v.W - 1), cy = iyr > 0.f && iyr < (float)(v.H - 1);
+  const float ax = cx ? 0.5f * (float)(v.W - 1) * v.scale[0] * v.focal[0] : 0.f;
+  const float ay = cy ? 0.5f * (float)(v.H - 1) * v.scale[1] * v.focal[1] : 0.f;
+  const float iz = 1.0f / xc2;
+  L.dix[0] = -ax * iz; L.dix[1] = 0.f; L.dix[2] = ax * xc0 * iz * iz;
+  L.diy[0] = 0.f; L.diy[1] = -ay * iz; L.diy[2] = ay * xc1 * iz * iz;
+  return L;
+}
+
+__global__ void __launch_bounds__(256) raymarch_train_kernel(MarchScenes sc, const float* __restrict__ tables,
+                                                             int64_t table_stride, const float* __restrict__ w_hh,
+                                                             const float* __restrict__ b_ih,
+                                                             const float* __restrict__ b_hh,
+                                                             const float* __restrict__ w_out,
+                                                             const float* __restrict__ b_out,
+                                                             const float* __restrict__ ro,
+                                                             const float* __restrict__ rd,
+                                                             const float* __restrict__ d0, int64_t n_per_scene,
+                                                             int64_t n_rays, int steps, float* __restrict__ world,
+                                                             float* __restrict__ trace, float* __restrict__ state) {
+  const int k = threadIdx.x & (kHid - 1);
+  const int64_t ray_raw = (int64_t)blockIdx.x * (blockDim.x / kHid) + threadIdx.x / kHid;
+  const bool live = ray_raw < n_rays;
+  const int64_t ray = live ? ray_raw : n_rays - 1;
+  const int scene = (int)(ray / n_per_scene);
+  const View& v = sc.v[scene];
+  const float* table = tables + scene * table_stride;
+  float wr[4][kHid], bias[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int j = 0; j < kHid; ++j) wr[q][j] = w_hh[(q * kHid + k) * kHid + j];
+    bias[q] = fadd(b_ih[q * kHid + k], b_hh[q * kHid + k]);
+  }
+  const float wo = w_out[k], bo = b_out[0];
+  const float e0 = rd[3 * ray], e1 = rd[3 * ray + 1], e2 = rd[3 * ray + 2];
+  const float dist0 = d0[ray];
+  float x0 = fadd(ro[3 * ray], fmul(e0, dist0)), x1 = fadd(ro[3 * ray + 1], fmul(e1, dist0));
+  float x2 = fadd(ro[3 * ray + 2], fmul(e2, dist0));
+  if (live && k < 3) trace[3 * ray + k] = k == 0 ? x0 : (k == 1 ? x1 : x2);
+  float h = 0.f, c = 0.f;
+  for (int s = 0; s < steps; ++s) {
+    const Bilinear bl = bilinear_at(v, x0, x1, x2);
+    float g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = q * kHid + k;
+      const float p = ((table[(int64_t)bl.tex[0] * kGates + row] * bl.w[0] +
+                        table[(int64_t)bl.tex[1] * kGates + row] * bl.w[1]) +
+                       table[(int64_t)bl.tex[2] * kGates + row] * bl.w[2]) +
+                      table[(int64_t)bl.tex[3] * kGates + row] * bl.w[3];
+      g[q] = p + bias[q];
+    }
+#pragma unroll
+    for (int j = 0; j < kHid; ++j) {
+      const float hj = __shfl(h, j, kHid);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[q] = fmaf(wr[q][j], hj, g[q]);
+    }
+    const float ig = sigmoid_(g[0]), fg = sigmoid_(g[1]), gg = tanhf(g[2]), og = sigmoid_(g[3]);
+    c = fadd(fmul(fg, c), fmul(ig, gg));
+    h = fmul(og, tanhf(c));
+    if (live) {
+      float* st = state + ((int64_t)s * n_rays + ray) * kMarchState;
+      st[k] = h; st[kHid + k] = c;
+      st[2 * kHid + k] = ig; st[3 * kHid + k] = fg; st[4 * kHid + k] = gg; st[5 * kHid + k] = og;
+    }
+    float sd = fmul(wo, h);
+#pragma unroll
+    for (int d = kHid / 2; d > 0; d >>= 1) sd = fadd(sd, __shfl_xor(sd, d, kHid));
+    sd = fadd(sd, bo);
+    x0 = fadd(x0, fmul(e0, sd));
+    x1 = fadd(x1, fmul(e1, sd));
+    x2 = fadd(x2, fmul(e2, sd));
+    if (live && k < 3) trace[(int64_t)(s + 1) * n_rays * 3 + 3 * ray + k] = k == 0 ? x0 : (k == 1 ? x1 : x2);
+  }
+  if (live && k < 3) world[3 * ray + k] = k == 0 ? x0 : (k == 1 ? x1 : x2);
+}
+
+// Gradient accumulators of one workgroup: d W_hh (64 x 16), d bias (64; b_ih and b_hh alike), d w_out (16),
+// d b_out (1).
+constexpr int kMarchGrads = kGates * kHid + kGates + kHid + 1;
+
+__global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const float* __restrict__ tables,
+                                                           int64_t table_stride, const float* __restrict__ w_hh,
+                                                           const float* __restrict__ w_out,
+                                                           const float* __restrict__ rd,
+                                                           const float* __restrict__ trace,
+                                                           const float* __restrict__ state,
+                                                           const float* __restrict__ grad_world, int64_t n_per_scene,
+                                                           int64_t n_rays, int steps, float* __restrict__ d_tables,
+                                                           float* __restrict__ d_grads) {
+  __shared__ float red[256 / kHid][kHid][kHid + 1];   // W_hh^T dg: (ray, unit k, column j)
+  __shared__ float gsum[kMarchGrads];
+  for (int i = threadIdx.x; i < kMarchGrads; i += blockDim.x) gsum[i] = 0.f;
+  const int k = threadIdx.x & (kHid - 1), rl = threadIdx.x / kHid;
+  const int64_t ray_raw = (int64_t)blockIdx.x * (blockDim.x / kHid) + rl;
+  const bool live = ray_raw < n_rays;
+  const int64_t ray = live ? ray_raw : n_rays - 1;
+  const int scene = (int)(ray / n_per_scene);
+  const View& v = sc.v[scene];
+  const float* table = tables + scene * table_stride;
+  float* dtab = d_tables + scene * table_stride;
+  float wr[4][kHid];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < kHid; ++j) wr[q][j] = w_hh[(q * kHid + k) * kHid + j];
+  const float wo = w_out[k];
+  const float e0 = rd[3 * ray], e1 = rd[3 * ray + 1], e2 = rd[3 * ray + 2];
+  float dx0 = live ? grad_world[3 * ray] : 0.f, dx1 = live ? grad_world[3 * ray + 1] : 0.f;
+  float dx2 = live ? grad_world[3 * ray + 2] : 0.f;
+  float dWhh[4][kHid], db[4] = {0.f, 0.f, 0.f, 0.f}, dwo = 0.f, dbo = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < kHid; ++j) dWhh[q][j] = 0.f;
+  float dh_next = 0.f, dc_next = 0.f;
+  __syncthreads();
+  for (int s = steps - 1; s >= 0; --s) {
+    const float* st = state + ((int64_t)s * n_rays + ray) * kMarchState;
+    const float h = st[k], c = st[kHid + k];
+    const float ig = st[2 * kHid + k], fg = st[3 * kHid + k], gg = st[4 * kHid + k], og = st[5 * kHid + k];
+    const float c_prev = s > 0 ? state[((int64_t)(s - 1) * n_rays + ray) * kMarchState + kHid + k] : 0.f;
+    const float h_prev = s > 0 ? state[((int64_t)(s - 1) * n_rays + ray) * kMarchState + k] : 0.f;
+    // x_{s+1} = x_s + rd * sd_s;  sd_s = w_out . h_s + b_out
+    const float dsd = e0 * dx0 + e1 * dx1 + e2 * dx2;
+    dwo += dsd * h;
+    dbo += dsd;
+    float dh = wo * dsd + dh_next;
+    dh = fminf(fmaxf(dh, -10.f), 10.f);               // state[0].register_hook(clamp(-10, 10))
+    const float tc = tanhf(c);
+    const float dc = dh * og * (1.f - tc * tc) + dc_next;
+    float dg[4];
+    dg[0] = dc * gg * ig * (1.f - ig);                // i
+    dg[1] = dc * c_prev * fg * (1.f - fg);            // f
+    dg[2] = dc * ig * (1.f - gg * gg);                // g
+    dg[3] = dh * tc * og * (1.f - og);                // o
+    dc_next = dc * fg;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) db[q] += dg[q];
+    // W_hh^T dg -> dh of step s - 1 (unit j), and d W_hh += dg h_{s-1}^T
+    float part[kHid];
+#pragma unroll
+    for (int j = 0; j < kHid; ++j) {
+      const float hj = __shfl(h_prev, j, kHid);
+      part[j] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        part[j] = fmaf(wr[q][j], dg[q], part[j]);
+        dWhh[q][j] = fmaf(dg[q], hj, dWhh[q][j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kHid; ++j) red[rl][k][j] = part[j];
+    // the lookup at x_s: table gradient and the position gradient
+    const float* xs = trace + (int64_t)s * n_rays * 3 + 3 * ray;
+    const LookupGrad L = lookup_grad(v, xs[0], xs[1], xs[2]);
+    float gix = 0.f, giy = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = q * kHid + k;
+      const float tnw = table[(int64_t)L.bl.tex[0] * kGates + row], tne = table[(int64_t)L.bl.tex[1] * kGates + row];
+      const float tsw = table[(int64_t)L.bl.tex[2] * kGates + row], tse = table[(int64_t)L.bl.tex[3] * kGates + row];
+      gix += dg[q] * (L.wy0 * (tne - tnw) + L.wy1 * (tse - tsw));
+      giy += dg[q] * (L.wx0 * (tsw - tnw) + L.wx1 * (tse - tne));
+      if (live) {
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+          atomicAdd(dtab + (int64_t)L.bl.tex[cc] * kGates + row, L.bl.w[cc] * dg[q]);
+      }
+    }
+#pragma unroll
+    for (int d = kHid / 2; d > 0; d >>= 1) {
+      gix += __shfl_xor(gix, d, kHid);
+      giy += __shfl_xor(giy, d, kHid);
+    }
+    const float dxc0 = gix * L.dix[0] + giy * L.diy[0];
+    const float dxc1 = gix * L.dix[1] + giy * L.diy[1];
+    const float dxc2 = gix * L.dix[2] + giy * L.diy[2];
+    // xc = R x + t: dx += R^T dxc (x_s feeds the lookup and, by identity, x_{s+1})
+    dx0 += v.R[0] * dxc0 + v.R[3] * dxc1 + v.R[6] * dxc2;
+    dx1 += v.R[1] * dxc0 + v.R[4] * dxc1 + v.R[7] * dxc2;
+    dx2 += v.R[2] * dxc0 + v.R[5] * dxc1 + v.R[8] * dxc2;
+    __syncthreads();   // red written
+    float acc = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < kHid; ++kk) acc += red[rl][kk][k];
+    dh_next = acc;
+    __syncthreads();   // red read before the next step overwrites it
+  }
+  // this workgroup's parameter gradients (dead rays contribute nothing)
+  if (!live) {
+    dwo = dbo = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      db[q] = 0.f;
+#pragma unroll
+      for (int j = 0; j < kHid; ++j) dWhh[q][j] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int j = 0; j < kHid; ++j) atomicAdd(&gsum[(q * kHid + k) * kHid + j], dWhh[q][j]);
+    atomicAdd(&gsum[kGates * kHid + q * kHid + k], db[q]);
+  }
+  atomicAdd(&gsum[kGates * kHid + kGates + k], dwo);
+  if (k == 0) atomicAdd(&gsum[kGates * kHid + kGates + kHid], dbo);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kMarchGrads; i += blockDim.x) atomicAdd(d_grads + i, gsum[i]);
+}
+
 }  // namespace avr
 
 using namespace avr;
+
+static int march_scenes(const avr_view_desc* views, int n_scenes, MarchScenes* sc, const char* what) {
+  AVR_REQUIRE(views && n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES, "%s: 1..%d scenes", what, AVR_MAX_SCENES);
+  for (int s = 0; s < n_scenes; ++s) {
+    AVR_REQUIRE(views[s].latent_h == views[0].latent_h && views[s].latent_w == views[0].latent_w &&
+                    views[s].latent_h > 0 && views[s].latent_w > 0,
+                "%s: scenes need latent maps of one (positive) size", what);
+    view_from_desc(&views[s], &sc->v[s]);
+  }
+  return AVR_OK;
+}
+
+extern "C" int avr_raymarch_train(const avr_view_desc* views, int n_scenes, const float* gate_tables,
+                                  const float* w_hh, const float* b_ih, const float* b_hh, const float* w_out,
+                                  const float* b_out, const float* ro, const float* rd, const float* init_dist,
+                                  int64_t n_per_scene, int steps, float* world, float* trace, float* state,
+                                  void* stream) {
+  AVR_REQUIRE(n_per_scene >= 0 && steps >= 0, "avr_raymarch_train: negative size");
+  if (n_per_scene == 0) return AVR_OK;
+  MarchScenes sc;
+  int rc = march_scenes(views, n_scenes, &sc, "avr_raymarch_train");
+  if (rc) return rc;
+  AVR_REQUIRE(gate_tables && w_hh && b_ih && b_hh && w_out && b_out && ro && rd && init_dist && world && trace &&
+                  (state || steps == 0),
+              "avr_raymarch_train: null pointer");
+  const int64_t n = n_per_scene * n_scenes;
+  const int64_t stride = (int64_t)views[0].latent_h * views[0].latent_w * kGates;
+  const int per_block = 256 / kHid;
+  raymarch_train_kernel<<<(unsigned)((n + per_block - 1) / per_block), 256, 0, as_stream(stream)>>>(
+      sc, gate_tables, stride, w_hh, b_ih, b_hh, w_out, b_out, ro, rd, init_dist, n_per_scene, n, steps, world,
+      trace, state);
+  return check_launch("raymarch_train_kernel");
+}
+
+extern "C" int avr_raymarch_bwd(const avr_view_desc* views, int n_scenes, const float* gate_tables,
+                                const float* w_hh, const float* w_out, const float* rd, const float* trace,
+                                const float* state, const float* grad_world, int64_t n_per_scene, int steps,
+                                float* d_tables, float* d_grads, void* stream) {
+  AVR_REQUIRE(n_per_scene >= 0 && steps >= 0, "avr_raymarch_bwd: negative size");
+  if (n_per_scene == 0 || steps == 0) return AVR_OK;
+  MarchScenes sc;
+  int rc = march_scenes(views, n_scenes, &sc, "avr_raymarch_bwd");
+  if (rc) return rc;
+  AVR_REQUIRE(gate_tables && w_hh && w_out && rd && trace && state && grad_world && d_tables && d_grads,
+              "avr_raymarch_bwd: null pointer");
+  const int64_t n = n_per_scene * n_scenes;
+  const int64_t stride = (int64_t)views[0].latent_h * views[0].latent_w * kGates;
+  const int per_block = 256 / kHid;
+  raymarch_bwd_kernel<<<(unsigned)((n + per_block - 1) / per_block), 256, 0, as_stream(stream)>>>(
+      sc, gate_tables, stride, w_hh, w_out, rd, trace, state, grad_world, n_per_scene, n, steps, d_tables, d_grads);
+  return check_launch("raymarch_bwd_kernel");
+}
 
 extern "C" int avr_raymarch(const avr_view_desc* view, const float* gate_table, const float* w_hh, const float* b_ih,
                             const float* b_hh, const float* w_out, const float* b_out, const float* ro,

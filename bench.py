@@ -50,13 +50,13 @@ def reference_flops_per_sample(d_in=42, d_latent=512, d_hidden=512, n_blocks=3, 
                 + d_hidden * d_out)
 
 
-def build_scene(device, seed=0, sigma_bias=0.0, conf="default"):
+def build_scene(device, seed=0, sigma_bias=0.0, conf="default", bn=False):
     """avr.scene.synthetic_scene: the default.conf field (or default_mv.conf's: 5 blocks, combine_layer 3)
     with fc_1 ~ N(0, 0.02), random 512x64x64 latent."""
     from avr.conf import default_conf
     from avr.scene import synthetic_scene
     model = default_conf(multiview=conf == "default_mv")["model"]
-    return synthetic_scene(device, seed, model, sigma_bias=sigma_bias)
+    return synthetic_scene(device, seed, model, sigma_bias=sigma_bias, bn=bn)
 
 
 def orbit_c2w(angle, radius=1.3, z_height=0.4):
@@ -417,7 +417,7 @@ def run_train(args, device):
     from avr.conf import default_conf
     from avr.renderers import AdaptiveVolumeRenderer, VolumeRenderer
     SB, R = 4, 512
-    net = build_scene(device, conf=args.conf)
+    net = build_scene(device, conf=args.conf, bn=args.bn)
     g = torch.Generator(device="cpu").manual_seed(7)
     net.encoder.set_latent(torch.randn(SB, net.d_latent, 64, 64, generator=g).to(device))
     net.num_objs = SB
@@ -480,9 +480,11 @@ def run_train(args, device):
         "value": round(SB * R / res["hip"], 1), "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(res["hip"] * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (field products as 3 fp16 MFMA terms)",
-        "data": f"synthetic: random-init {args.conf}.conf field, 4 random 512x64x64 latents, random pixels/targets",
+        "data": f"synthetic: random-init {args.conf}.conf field{' with --bn (training-mode BatchNorm)' if args.bn else ''}, "
+                "4 random 512x64x64 latents, random pixels/targets",
         "config": {"workload": wl + f", field of conf/{args.conf}.conf ({net.mlp_coarse.n_blocks} x "
-                               f"{net.mlp_coarse.d_hidden} ResnetFC, combine_layer {net.mlp_coarse.combine_layer})",
+                               f"{net.mlp_coarse.d_hidden} ResnetFC, combine_layer {net.mlp_coarse.combine_layer}"
+                               + (", bn=True: training-mode BatchNorm, avr.bn_train)" if args.bn else ")"),
                    "field_samples_per_step": SB * R * spr},
     }
     if "torch" in res:
@@ -868,6 +870,9 @@ def main():
     ap.add_argument("--conf", choices=["default", "default_mv"], default="default",
                     help="--mode train: the field of conf/default.conf or conf/default_mv.conf (train.py:262)")
     ap.add_argument("--train-modes", default="hip,torch", help="--mode train: which autograd paths to time")
+    ap.add_argument("--bn", action="store_true",
+                    help="--mode train: train.py --bn (ResnetBlockFC(bn=True), training-mode BatchNorm: the "
+                         "layer-by-layer HIP path avr.bn_train)")
     ap.add_argument("--renderer", choices=["volume", "adaptive"], default="volume",
                     help="--mode train: VolumeRenderer (train.py 'VR*' runs) or AdaptiveVolumeRenderer (train.py's "
                          "default for other run names, train.py:268-273)")

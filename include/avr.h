@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 10
+#define AVR_ABI_VERSION 11
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -344,6 +344,61 @@ int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int64_t n_rows
 int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_split, float* const* dw,
                             float* const* db, void* stream);
 
+/* ------------------------------------------------ training-mode BatchNorm (ABI 11)
+ * train.py --bn (train.py:210, :265) builds ResnetBlockFC(bn=True): relu(bn_0(x)) -> fc_0 -> relu(bn_0(net))
+ * -> fc_1 (+ x), bn_0 twice per block with batch statistics over every row of the field call
+ * (models.py:430-432, 454-461; bn_1 is unused). The statistics are a reduction over all rows between two
+ * GEMMs, so this path runs the MLP layer by layer over row-major fp32 rows (n_rows, in_dim / out_dim):
+ *
+ * avr_bn_layer: one x3 GEMM of a layer over all rows (split-fp16 MFMA, fp32 accumulate, as the fused kernels).
+ *   mode AVR_BN_FWD: out = W . op + bias (+ add1) (+ add2) with W = the forward blob's layer `layer` (header
+ *     numbering: 0 lin_in, 2 + 2b fc_0[b], 3 + 2b fc_1[b]; pack with dims->bn = 0: no eval-BN folding);
+ *     partial (n_wg, 2, out_dim) = per 64-row workgroup (mean, sum of squared deviations) of out's columns.
+ *   mode AVR_BN_BWD: gp = (W^T . op) * [mask_rows > 0] with W^T from the backward blob (avr_field_pack_bwd);
+ *     out = gp; partial = per workgroup (sum gp, sum gp * xhat), xhat = (pre_rows - out_mu) * out_invstd.
+ *   The operand op (n_rows, in_dim), read from src (columns >= in_valid are 0):
+ *     AVR_BN_PLAIN op = src;
+ *     AVR_BN_RELU  op = relu((src - in_mu) * in_scale + in_shift)                 (forward: relu(bn_0(x)));
+ *     AVR_BN_GRAD  op = src_res + in_scale * (src - in_m1 - (src_pre - in_mu) * in_invstd * in_m2)
+ *                  (src = d loss / d bn output, torch's batch_norm backward; src_res may be NULL).
+ *   operand_out (ld in_dim) / operand_max (float bits, atomicMax): the operand as the GEMM used it, or NULL.
+ * avr_bn_stats: the forward partials -> batch mean / invstd (fp64 Chan combine), scale = gamma * invstd, and
+ *   the running statistics updated as torch does (momentum; unbiased variance).
+ * avr_bn_grad_stats: the backward partials -> m1 = mean gp, m2 = mean gp * xhat, coef = gamma * invstd, and
+ *   dgamma += sum gp * xhat, dbeta += sum gp.
+ * avr_bn_grad_rows: out = res + coef * (g - m1 - (pre - mu) * invstd * m2) (the last BN backward, no GEMM after
+ *   it), out_max as operand_max.                                                                               */
+#define AVR_BN_FWD 0
+#define AVR_BN_BWD 1
+#define AVR_BN_PLAIN 0
+#define AVR_BN_RELU 1
+#define AVR_BN_GRAD 2
+typedef struct {
+  int64_t n_rows;
+  int mode, prologue;
+  int in_dim, in_valid;     /* in_dim: 32 * chunks (64 for lin_in, d_hidden otherwise); in_valid <= in_dim  */
+  const float* src; int64_t ld_src;
+  const float* src_pre;     /* AVR_BN_GRAD: pre-BN rows (ld ld_src) */
+  const float* src_res;     /* AVR_BN_GRAD: rows added (ld ld_src) or NULL */
+  const float* in_mu; const float* in_scale; const float* in_shift;
+  const float* in_m1; const float* in_m2; const float* in_invstd;
+  float* operand_out; uint32_t* operand_max;
+  const float* blob; int layer;
+  const float* bias; const float* add1; const float* add2;   /* AVR_BN_FWD (rows ld d_hidden) */
+  float* out;                                                 /* (n_rows, d_hidden) */
+  const float* mask_rows; const float* pre_rows;              /* AVR_BN_BWD (ld d_hidden) */
+  const float* out_mu; const float* out_invstd;
+  float* partial;           /* (ceil(n_rows / 64), 2, d_hidden) */
+} avr_bn_layer;
+int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* l, void* stream);
+int avr_bn_stats(const float* partial, int64_t n_rows, int n_cols, const float* gamma, float eps, float momentum,
+                 float* running_mean, float* running_var, float* mu, float* invstd, float* scale, void* stream);
+int avr_bn_grad_stats(const float* partial, int64_t n_rows, int n_cols, const float* gamma, const float* invstd,
+                      float* coef, float* m1, float* m2, float* dgamma, float* dbeta, void* stream);
+int avr_bn_grad_rows(int64_t n_rows, int n_cols, const float* g, const float* pre, const float* res,
+                     const float* coef, const float* m1, const float* m2, const float* mu, const float* invstd,
+                     float* out, uint32_t* out_max, void* stream);
+
 /* Latent features at points — SpatialEncoder.index (models.py:245-274) as
  * NewPixelNeRFNet.forward uses it (models.py:753-810): bilinear / border /
  * align_corners=True lookup of latent_hwc (H*W, channels), the source view's
@@ -370,6 +425,23 @@ int avr_raymarch(const avr_view_desc* view, const float* gate_table, const float
                  const float* b_hh, const float* w_out, const float* b_out, const float* ro, const float* rd,
                  const float* init_dist, int64_t n_rays, int steps, float* world, float* final_dist, float* trace,
                  void* stream);
+
+/* Training (ABI 11): the march with autograd for train.py's AdaptiveVolumeRenderer / Raymarcher step
+ * (renderers.py:413-432, :320-343). n_scenes (<= AVR_MAX_SCENES) scenes of n_per_scene rays each (ray r in
+ * scene r / n_per_scene, its view and gate table; gate_tables (n_scenes, H*W, 64)). Forward: world (n, 3),
+ * trace ((steps + 1), n, 3) = every point, state (steps, n, 96) = h, c, i, f, g, o per step (the backward's
+ * input). Backward, given grad_world (n, 3): d_tables (n_scenes, H*W, 64) += d loss / d gate table (W_ih's
+ * gradient is then sum_s d_tables[s]^T latent_s^T, the latent's W_ih^T d_tables[s]), d_grads (64*16 + 64 + 16
+ * + 1) += d W_hh, d (b_ih = b_hh), d w_out, d b_out, with the reference's clamp(-10, 10) of every h gradient
+ * (state[0].register_hook) and grid_sample's border / align_corners=True position gradient. Zero both first. */
+int avr_raymarch_train(const avr_view_desc* views, int n_scenes, const float* gate_tables, const float* w_hh,
+                       const float* b_ih, const float* b_hh, const float* w_out, const float* b_out, const float* ro,
+                       const float* rd, const float* init_dist, int64_t n_per_scene, int steps, float* world,
+                       float* trace, float* state, void* stream);
+int avr_raymarch_bwd(const avr_view_desc* views, int n_scenes, const float* gate_tables, const float* w_hh,
+                     const float* w_out, const float* rd, const float* trace, const float* state,
+                     const float* grad_world, int64_t n_per_scene, int steps, float* d_tables, float* d_grads,
+                     void* stream);
 
 /* ------------------------------------------------------------ measurement
  * Streaming device copy dst[0, n_bytes) = src[0, n_bytes) (16-B aligned,

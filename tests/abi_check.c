@@ -180,6 +180,51 @@ int main(void) {
   expect("raymarch null", avr_raymarch(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 4, 10, NULL, NULL,
                                        NULL, NULL), AVR_E_INVALID);
 
+  /* training-mode BatchNorm (ABI 11): argument checks, no launch */
+  d.d_hidden = 512; d.bn = 0; d.spade = 0; d.beta = 0.f; d.precision = AVR_FIELD_X3;
+  {
+    avr_bn_layer l;
+    memset(&l, 0, sizeof l);
+    l.n_rows = 100; l.mode = AVR_BN_FWD; l.prologue = AVR_BN_PLAIN; l.in_dim = 512; l.in_valid = 512;
+    l.src = buf; l.ld_src = 512; l.blob = buf; l.layer = 2; l.out = buf; l.partial = buf;
+    expect("bn_layer null layer", avr_bn_layer_run(&d, NULL, NULL), AVR_E_INVALID);
+    l.mode = 7;
+    expect("bn_layer bad mode", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    l.mode = AVR_BN_FWD; l.in_dim = 96;
+    expect("bn_layer bad in_dim", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    l.in_dim = 512; l.ld_src = 510;
+    expect("bn_layer bad ld", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    l.ld_src = 512; l.prologue = AVR_BN_RELU;
+    expect("bn_layer relu without stats", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    l.prologue = AVR_BN_PLAIN; l.layer = 2 + 2 * d.n_blocks;
+    expect("bn_layer bad layer", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    l.layer = 2; l.mode = AVR_BN_BWD;
+    expect("bn_layer bwd without mask rows", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    l.mode = AVR_BN_FWD; d.bn = 1;
+    expect("bn_layer folded blob", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    d.bn = 0; l.n_rows = 0;
+    expect("bn_layer empty", avr_bn_layer_run(&d, &l, NULL), AVR_OK);
+  }
+  expect("bn_stats one row", avr_bn_stats(buf, 1, 512, buf, 1e-5f, 0.1f, NULL, NULL, buf, buf, buf, NULL),
+         AVR_E_INVALID);
+  expect("bn_stats half running", avr_bn_stats(buf, 8, 512, buf, 1e-5f, 0.1f, buf, NULL, buf, buf, buf, NULL),
+         AVR_E_INVALID);
+  expect("bn_grad_stats null", avr_bn_grad_stats(buf, 8, 512, NULL, buf, buf, buf, buf, buf, buf, NULL), AVR_E_INVALID);
+  expect("bn_grad_rows odd cols", avr_bn_grad_rows(8, 6, buf, buf, NULL, buf, buf, buf, buf, buf, buf, NULL, NULL),
+         AVR_E_INVALID);
+  expect("bn_grad_rows empty", avr_bn_grad_rows(0, 8, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL),
+         AVR_OK);
+  /* LSTM march training (ABI 11) */
+  expect("raymarch_train too many scenes",
+         avr_raymarch_train(&v, AVR_MAX_SCENES + 1, buf, buf, buf, buf, buf, buf, buf, buf, buf, 4, 10, buf, buf, buf,
+                            NULL), AVR_E_INVALID);
+  expect("raymarch_train null", avr_raymarch_train(&v, 1, buf, NULL, buf, buf, buf, buf, buf, buf, buf, 4, 10, buf, buf,
+                                                   buf, NULL), AVR_E_INVALID);
+  expect("raymarch_bwd null", avr_raymarch_bwd(&v, 1, buf, buf, buf, buf, buf, buf, NULL, 4, 10, buf, buf, NULL),
+         AVR_E_INVALID);
+  expect("raymarch_bwd no steps", avr_raymarch_bwd(&v, 1, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 4, 0, NULL, NULL,
+                                                   NULL), AVR_OK);
+
   /* measurement */
   expect("copy odd size", avr_stream_copy(buf, buf + 8, 15, NULL), AVR_E_INVALID);
   expect("copy null", avr_stream_copy(NULL, buf, 16, NULL), AVR_E_INVALID);

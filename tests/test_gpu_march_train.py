@@ -1,0 +1,123 @@
+"""Autograd of the LSTM march on HIP (avr.renderers._MarchTrain: avr_raymarch_train / avr_raymarch_bwd) --
+train.py's AdaptiveVolumeRenderer / Raymarcher step (renderers.py:413-432, :320-343; train.py:268-273)
+against PyTorch autograd of the reference loop (LSTMCell on grid_sample'd features, the clamp hook on every
+h gradient): the march alone (world points, every LSTM / out_layer / W_ih gradient, the latent's gradient)
+against a float64 run of the same loop, and a whole AdaptiveVolumeRenderer training step."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_train import _net
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def _march_inputs(sb, R, seed=0):
+    from avr import ops
+    from avr.scene import INTRINSICS
+    g = torch.Generator().manual_seed(seed)
+    x_pix = torch.rand(sb, R, 2, generator=g).to(DEV)
+    c2w = torch.eye(4).reshape(1, 1, 4, 4).repeat(sb, R, 1, 1)
+    c2w[..., 2, 3] = -1.3 - 0.1 * torch.arange(sb).reshape(sb, 1)
+    c2w[..., 0, 3] = 0.05 * torch.randn(sb, R, generator=g)
+    K = torch.tensor([INTRINSICS] * sb, device=DEV)
+    ros, rds, _ = ops.world_rays(x_pix, K, c2w.to(DEV))
+    init = (0.8 + 0.05 * torch.randn(sb, R, 1, generator=g)).to(DEV)
+    return ros, rds, init, x_pix, c2w.to(DEV), K
+
+
+def _renderer(C, steps=10, cls="adaptive", seed=3):
+    from avr.renderers import AdaptiveVolumeRenderer, Raymarcher
+    torch.manual_seed(seed)
+    r = AdaptiveVolumeRenderer(C, steps, 0.15, 20, True) if cls == "adaptive" else Raymarcher(C, steps)
+    return r.to(DEV)
+
+
+def _march_grads(rend, net, ros, rds, init, w, hip, latent_grad=True):
+    net.hip_backward = hip
+    rend.zero_grad(set_to_none=True)
+    lat = net.encoder.latent.detach().clone().requires_grad_(latent_grad)
+    net.encoder.latent = lat
+    world = rend.march(ros, rds, init, net)
+    (world * w).sum().backward()
+    g = {n: p.grad.detach().clone() for n, p in rend.named_parameters()}
+    if latent_grad:
+        g["latent"] = lat.grad.detach().clone()
+    return world.detach(), g, rend.last_path
+
+
+@pytest.mark.parametrize("sb,R,steps", [(1, 300, 10), (3, 257, 10), (2, 64, 1)])
+def test_march_autograd_matches_fp64(sb, R, steps):
+    net = _net(64, 2, 64, (8, 8), sb=sb)
+    rend = _renderer(64, steps)
+    ros, rds, init, *_ = _march_inputs(sb, R, seed=sb)
+    # loss weights large enough that some h gradients exceed 10: the reference's clamp hook engages
+    w = 300.0 * torch.randn(sb, R, 3, generator=torch.Generator().manual_seed(7)).to(DEV)
+    wh, gh, path = _march_grads(rend, net, ros, rds, init, w, hip=True)
+    assert path == "hip_train"
+    wt, gt, path_t = _march_grads(rend, net, ros, rds, init, w, hip=False)
+    assert path_t == "module"
+    np.testing.assert_allclose(wh.cpu().numpy(), wt.cpu().numpy(), atol=1e-3)   # sanity; the bar is the fp64 one
+    # float64 reference of the reference loop
+    net.double()
+    rend.double()
+    net.use_fused = False
+    try:
+        wd, gd, _ = _march_grads(rend, net, ros.double(), rds.double(), init.double(), w.double(), hip=False)
+    finally:
+        net.float()
+        rend.float()
+        net.use_fused = True
+    ew = float((wh.double() - wd).abs().max())
+    et_w = float((wt.double() - wd).abs().max())
+    assert ew <= 2.0 * et_w + 1e-5, (ew, et_w)
+    assert set(gh) == set(gt) == set(gd)
+    worst = 0.0
+    for k in gd:
+        ref = gd[k].double()
+        s = float(ref.abs().max()) or 1.0
+        eh = float((gh[k].double() - ref).abs().max()) / s
+        et = float((gt[k].double() - ref).abs().max()) / s
+        worst = max(worst, eh)
+        assert eh <= 2.0 * et + 1e-4, f"{k}: HIP err {eh:.2e} vs fp32 autograd err {et:.2e} of max |grad| {s:.2e}"
+    print(f"march sb={sb} R={R} steps={steps}: worst HIP gradient error vs float64 {worst:.2e}")
+
+
+def test_adaptive_renderer_training_step_hip_vs_torch():
+    """AdaptiveVolumeRenderer (conf adaptive_renderer: 10 steps, band of 20, epsilon 0.15) training step on
+    the default_mv-shaped net (combine_layer 3): loss and every gradient (net, LSTM, out_layer) of the HIP
+    march + HIP field against PyTorch autograd of the same modules."""
+    sb, R = 2, 256
+    net = _net(128, 5, 64, (8, 8), combine_layer=3, sb=sb)
+    rend = _renderer(64)
+    _, _, _, x_pix, c2w, K = _march_inputs(sb, R, seed=11)
+    g = torch.Generator().manual_seed(12)
+    noise = {"initial_distance": (0.8 + 0.05 * torch.randn(sb, R, 1, generator=g)).to(DEV),
+             "band": torch.rand(sb, R, 20, generator=g).to(DEV)}
+    gt = torch.rand(sb, R, 3, generator=g).to(DEV)
+
+    def step(hip):
+        net.hip_backward = hip
+        net.zero_grad(set_to_none=True)
+        rend.zero_grad(set_to_none=True)
+        rgb_c, rgb, _, _ = rend(c2w, K, x_pix, net, noise=noise)
+        loss = ((rgb_c - gt) ** 2).mean() + ((rgb - gt) ** 2).mean()
+        loss.backward()
+        grads = {n: p.grad.detach().clone() for n, p in list(net.named_parameters()) + list(rend.named_parameters())
+                 if p.grad is not None}
+        return float(loss), grads, rend.last_path
+
+    lh, gh, ph = step(True)
+    lt, gt_, pt = step(False)
+    assert ph == "hip_train" and pt == "module"
+    assert abs(lh - lt) <= 1e-5 * max(1.0, abs(lt))
+    assert set(gh) == set(gt_)
+    # fp32 against fp32 (the renderer's ray kernels are fp32-only, so no float64 run of the whole step): the
+    # march's points move by fp32 noise between the two paths, and a point sitting on the latent lookup's
+    # border clip or a relu kink takes the other branch in one of them -- the march-alone test above holds
+    # every gradient to twice PyTorch's own error against float64; here 1e-2 of each parameter's max |grad|
+    for k in gt_:
+        s = float(gt_[k].abs().max()) or 1.0
+        err = float((gh[k] - gt_[k]).abs().max())
+        assert err <= 1e-2 * s + 1e-7, f"{k}: {err:.3e} of {s:.3e}"
