@@ -126,7 +126,7 @@ _SIGS = {
                                    c_void_p, c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, c_void_p, c_void_p,
                                    c_int, c_void_p, c_void_p],
     "avr_field_bwd": [ctypes.POINTER(FieldDims), c_void_p, c_void_p, c_int, i64, c_void_p, c_void_p, c_void_p,
-                      c_void_p, i64, c_void_p, c_void_p],
+                      c_void_p, i64, c_void_p, i64, c_void_p, c_void_p],
     "avr_weight_grads": [ctypes.POINTER(WGradLayer), c_int, i64, c_int, c_void_p],
     "avr_weight_grads_reduce": [ctypes.POINTER(WGradLayer), c_int, c_int, ctypes.POINTER(c_void_p),
                                 ctypes.POINTER(c_void_p), c_void_p],

@@ -37,9 +37,9 @@ def softplus_beta(mlp):
 
 
 def inference_only(mlp):
-    """ResnetFC options the x3 kernel runs for inference only (training: the module path):
-    eval BatchNorm, use_spade, Softplus."""
-    return uses_bn(mlp) or getattr(mlp, "use_spade", False) or bool(softplus_beta(mlp))
+    """ResnetFC options the fused x3 kernels run for inference only: BatchNorm (training mode trains layer by
+    layer, avr.bn_train) and use_spade (module path). Softplus(beta) trains on the fused kernels (ABI 11)."""
+    return uses_bn(mlp) or getattr(mlp, "use_spade", False)
 
 
 def _bn_ok(blk):
@@ -560,12 +560,13 @@ class _FieldTrain(torch.autograd.Function):
         grad_out = grad_out.to(F32).contiguous()
         G = torch.empty(n_l, Mt, H, device=dev, dtype=F32)
         g_max = torch.zeros(n_l, device=dev, dtype=torch.int32)
+        act = ctx.act
         for g0, n, mask in ctx.masks:
             call("avr_field_bwd", ctypes.byref(dims), ptr(entry.packed), ptr(bwd), n, B, ptr(out[g0]),
-                 ptr(grad_out[g0]), ptr(mask), ctypes.c_void_p(G.data_ptr() + g0 * B * H * 4), Mt, ptr(g_max),
-                 stream_of(G))
+                 ptr(grad_out[g0]), ptr(mask), ctypes.c_void_p(act.data_ptr() + g0 * B * H * 4), Mt,
+                 ctypes.c_void_p(G.data_ptr() + g0 * B * H * 4), Mt, ptr(g_max), stream_of(G))
         entry.dims.precision = PRECISIONS[fused.precision]
-        act, act_max, zf = ctx.act, ctx.act_max, ctx.zf
+        act_max, zf = ctx.act_max, ctx.zf
         ctx.act = ctx.act_max = ctx.masks = ctx.zf = None
         # MLP inputs the lin_z / lin_in gradients contract against: the latent
         # features (avr_latent_features, row-major) and z_feature (the training forward

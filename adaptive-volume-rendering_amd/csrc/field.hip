@@ -719,8 +719,8 @@ extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_
   int rc = field_common(dims, views, packed, tables, &a);
   if (rc) return rc;
   AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_fwd_points_train: the training path is x3 only");
-  AVR_REQUIRE(!dims->bn && !dims->spade && !(dims->beta > 0.f),
-              "avr_field_fwd_points_train: BatchNorm / use_spade / Softplus nets train on the module path");
+  AVR_REQUIRE(!dims->bn && !dims->spade,
+              "avr_field_fwd_points_train: BatchNorm nets train on avr_bn_layer_run, use_spade nets on the module path");
   AVR_REQUIRE(n_points >= 0, "avr_field_fwd_points_train: bad size");
   AVR_REQUIRE(n_points == 0 || (xyz && viewdirs && out && act && mask), "avr_field_fwd_points_train: null pointer");
   AVR_REQUIRE(act_rows >= n_scenes * n_points, "avr_field_fwd_points_train: act_rows < n_scenes * n_points");
@@ -749,13 +749,19 @@ extern "C" int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_
 
 extern "C" int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd, int n_scenes,
                              int64_t n_points, const float* out, const float* grad_out, const uint32_t* mask,
-                             float* grads, int64_t grads_rows, uint32_t* grads_max, void* stream) {
+                             const float* act, int64_t act_rows, float* grads, int64_t grads_rows,
+                             uint32_t* grads_max, void* stream) {
   BwdArgs a{};
   int rc = make_layout(dims, &a.L);
   if (rc) return rc;
   AVR_REQUIRE(dims->precision == AVR_FIELD_X3, "avr_field_bwd: the training path is x3 only");
-  AVR_REQUIRE(!dims->bn && !dims->spade && !(dims->beta > 0.f),
-              "avr_field_bwd: BatchNorm / use_spade / Softplus nets train on the module path");
+  AVR_REQUIRE(!dims->bn && !dims->spade,
+              "avr_field_bwd: BatchNorm nets train on avr_bn_layer_run, use_spade nets on the module path");
+  AVR_REQUIRE(!(dims->beta > 0.f) || (act && act_rows >= (int64_t)n_scenes * n_points),
+              "avr_field_bwd: Softplus nets need the forward's act rows (act_rows >= n_scenes * n_points)");
+  a.act = act;
+  a.act_stride = act_rows * dims->d_hidden;
+  a.beta = dims->beta;
   AVR_REQUIRE(n_points >= 0 && n_scenes >= 1, "avr_field_bwd: bad size");
   if (n_points == 0) return AVR_OK;
   AVR_REQUIRE(packed && packed_bwd && out && grad_out && mask && grads, "avr_field_bwd: null pointer");

@@ -42,6 +42,26 @@ __device__ __forceinline__ void load_mask(unsigned (&mb)[mask_words(FT)], const 
   for (int q = 0; q < MW; ++q) mb[q] = mk[q * 64];
 }
 
+// d act(x) / dx applied to v: ReLU from the forward's mask bits; Softplus(beta) from the saved activation
+// y = softplus(x) of row m, features f0 .. f0+3 of layer `layer`: torch's softplus_backward is
+// g * sigmoid(beta x) = g * (1 - exp(-beta y)) (-expm1: no cancellation where the slope is tiny; where torch
+// takes the linear branch, beta x > 20, this is 1 to fp32 precision)
+template <int FT, int ACT>
+__device__ __forceinline__ floatx4 dact(const floatx4& v, const unsigned* mb, const BwdArgs& a, int layer,
+                                        int64_t row, int f0, int ft, int sg) {
+  if constexpr (ACT == 0) {
+    return masked<FT>(v, mb, ft, sg);
+  } else {
+    const floatx4 y = *reinterpret_cast<const floatx4*>(a.act + (int64_t)layer * a.act_stride + row + f0);
+    floatx4 r;
+    r.x = v.x * -expm1f(-a.beta * y.x);
+    r.y = v.y * -expm1f(-a.beta * y.y);
+    r.z = v.z * -expm1f(-a.beta * y.z);
+    r.w = v.w * -expm1f(-a.beta * y.w);
+    return r;
+  }
+}
+
 template <int FT, int NW>
 __device__ __forceinline__ void store_rows(float* G, const floatx4 (&v)[FT][4], int64_t base, int64_t M, int wid,
                                            int g, int j) {
@@ -82,7 +102,7 @@ __device__ __forceinline__ float bwd_scale(const float* packed_bwd, int layer) {
   return pow2_scale_for(__uint_as_float(reinterpret_cast<const unsigned*>(packed_bwd)[layer]));
 }
 
-template <int FT, int NW>
+template <int FT, int NW, int ACT>
 __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   constexpr int HID = 16 * FT * NW;
   constexpr int KC = HID / 32;
@@ -99,6 +119,11 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   const int64_t roff = (int64_t)scene * a.M;
   const int nb = a.n_blocks;
   const uint4* PB = reinterpret_cast<const uint4*>(a.packed_bwd);
+  // Softplus: offset of the saved activation row of sample group sg (rows past M read the last row: unused)
+  const auto arow = [&](int sg) -> int64_t {
+    const int64_t m = base + 16 * sg + j;
+    return (roff + (m < a.M ? m : a.M - 1)) * HID;
+  };
 
   floatx4 dx[FT][4], t[FT][4];
   unsigned mb[MW];
@@ -126,7 +151,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) {
       const floatx4 acc = ((w[0] * d4[sg][0] + w[1] * d4[sg][1]) + w[2] * d4[sg][2]) + w[3] * d4[sg][3];
-      dx[ft][sg] = masked<FT>(acc, mb, ft, sg);
+      dx[ft][sg] = dact<FT, ACT>(acc, mb, a, 2 * nb, arow(sg), 16 * tile + 4 * g, ft, sg);
     }
   }
 
@@ -145,7 +170,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
-      for (int sg = 0; sg < 4; ++sg) t[ft][sg] = masked<FT>(t[ft][sg] * inv, mb, ft, sg);
+      for (int sg = 0; sg < 4; ++sg)
+        t[ft][sg] = dact<FT, ACT>(t[ft][sg] * inv, mb, a, 2 * b + 1, arow(sg), 16 * (FT * wid + ft) + 4 * g, ft, sg);
     mx = absmax<FT>(t);
     // ---- fc_0^T
     const uint4* W0 = PB + a.LB.fc0t[b] / 4 + 2 * 64 * FT * wid;
@@ -157,7 +183,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
-      for (int sg = 0; sg < 4; ++sg) dx[ft][sg] += masked<FT>(t[ft][sg] * inv, mb, ft, sg);
+      for (int sg = 0; sg < 4; ++sg)
+        dx[ft][sg] += dact<FT, ACT>(t[ft][sg] * inv, mb, a, 2 * b, arow(sg), 16 * (FT * wid + ft) + 4 * g, ft, sg);
   }
   // G_in (nothing waits on these stores any more), then the layer maxima: one atomic per workgroup and
   // layer for the GEMM operands (the workgroup max publish recorded), one per wave for G_in
@@ -169,31 +196,36 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   }
 }
 
-template <int FT, int NW>
+template <int FT, int NW, int ACT>
 static int launch_bwd(const BwdArgs& a, hipStream_t s) {
   constexpr int HID = 16 * FT * NW;
   const size_t shm = (size_t)(HID / 32) * 8192 + 64 + 4 * kX3MaxLayers;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bwd_x3_kernel<FT, NW>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&field_bwd_x3_kernel<FT, NW, ACT>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
       return fail(AVR_E_HIP, "field_bwd_x3_kernel: cannot set dynamic LDS to %zu", shm);
     attr = true;
   }
   const int64_t blocks = a.blocks_per_scene * a.n_scenes;
   AVR_REQUIRE(blocks < (1ll << 31), "field backward: too many points");
-  field_bwd_x3_kernel<FT, NW><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
+  field_bwd_x3_kernel<FT, NW, ACT><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("field_bwd_x3_kernel");
 }
 
-int dispatch_field_bwd_x3(int d_hidden, const BwdArgs& a, hipStream_t s) {
+template <int ACT>
+static int dispatch_bwd_act(int d_hidden, const BwdArgs& a, hipStream_t s) {
   switch (d_hidden) {
-    case 64: return launch_bwd<1, 4>(a, s);
-    case 128: return launch_bwd<2, 4>(a, s);
-    case 256: return launch_bwd<4, 4>(a, s);
-    case 512: return launch_bwd<8, 4>(a, s);
+    case 64: return launch_bwd<1, 4, ACT>(a, s);
+    case 128: return launch_bwd<2, 4, ACT>(a, s);
+    case 256: return launch_bwd<4, 4, ACT>(a, s);
+    case 512: return launch_bwd<8, 4, ACT>(a, s);
   }
   return fail(AVR_E_UNSUPPORTED, "field backward: d_hidden %d", d_hidden);
+}
+
+int dispatch_field_bwd_x3(int d_hidden, const BwdArgs& a, hipStream_t s) {
+  return a.beta > 0.f ? dispatch_bwd_act<1>(d_hidden, a, s) : dispatch_bwd_act<0>(d_hidden, a, s);
 }
 
 }  // namespace avr

@@ -315,6 +315,11 @@ struct BwdArgs {
   unsigned* g_max;          // per-layer max |G| as float bits (atomicMax), or null
   int n_scenes;             // M points per scene, rows scene * M + m
   int64_t blocks_per_scene; // workgroup b: scene b / blocks_per_scene (the forward's map)
+  // Softplus(beta) nets (beta > 0, ABI 11): the activation's derivative from the forward's saved GEMM inputs
+  // y = softplus(x) (act, layer l at act + l * act_stride): sigmoid(beta x) = 1 - exp(-beta y), no masks
+  const float* act;
+  int64_t act_stride;
+  float beta;
 };
 
 int dispatch_field_bwd_x3(int d_hidden, const BwdArgs& a, hipStream_t s);

@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   static_assert(!(SAVE && TWO), "the training forward keeps the 4-wave layout");
   static_assert(!(SAVE && BN), "BatchNorm nets train on the module path");
   static_assert(!(SAVE && SPADE) && !(BN && SPADE), "use_spade: inference without BatchNorm only");
-  static_assert(ACT == 0 || (!SAVE && !BN), "Softplus: inference without BatchNorm only");
+  static_assert(ACT == 0 || !BN, "Softplus: without BatchNorm only");
   const float beta = a.beta;
   const floatx4 bz[FT] = {};
   // 8 waves: waves 0-3 at priority 1 leave each GEMM first, so their epilogue VALU overlaps the last MFMAs of
@@ -816,8 +816,17 @@ int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s) {
     }
     return fail(AVR_E_UNSUPPORTED, "field x3: d_hidden %d", d_hidden);
   }
-  if (a.L.spade || a.beta > 0.f) {   // use_spade and / or Softplus (inference only)
-    AVR_REQUIRE(!a.act, "field x3: use_spade / Softplus nets train on the module path");
+  if (a.beta > 0.f && !a.L.spade && a.act) {   // Softplus training forward (4-wave SAVE layout, ABI 11)
+    switch (d_hidden) {
+      case 64: return launch_x3<1, 4, true, false, false, 1>(a, s);
+      case 128: return launch_x3<2, 4, true, false, false, 1>(a, s);
+      case 256: return launch_x3<4, 4, true, false, false, 1>(a, s);
+      case 512: return launch_x3<8, 4, true, false, false, 1>(a, s);
+    }
+    return fail(AVR_E_UNSUPPORTED, "field x3: d_hidden %d", d_hidden);
+  }
+  if (a.L.spade || a.beta > 0.f) {   // use_spade and / or Softplus (inference)
+    AVR_REQUIRE(!a.act, "field x3: use_spade nets train on the module path");
     const int v = (a.L.spade ? 1 : 0) | (a.beta > 0.f ? 2 : 0);
 #define AVR_X3_OPT(FT, NW)                                      \
   switch (v) {                                                  \

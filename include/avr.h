@@ -313,9 +313,12 @@ int avr_field_fwd_points_train(const avr_field_dims* dims, const avr_view_desc* 
                                const float* packed, const float* tables, const float* xyz, const float* viewdirs,
                                int64_t n_points, float* out, float* act, int64_t act_rows, uint32_t* mask,
                                uint32_t* act_max, float* z_feature, int ld_z, uint32_t* z_max, void* stream);
+/* ABI 11: act / act_rows = the forward's act buffer and its rows per layer (as passed to
+ * avr_field_fwd_points_train): read for Softplus(beta) nets (dims->beta > 0), whose activation derivative
+ * comes from the saved activations instead of the relu masks; may be NULL for ReLU nets. */
 int avr_field_bwd(const avr_field_dims* dims, const float* packed, const float* packed_bwd, int n_scenes,
-                  int64_t n_points, const float* out, const float* grad_out, const uint32_t* mask, float* grads,
-                  int64_t grads_rows, uint32_t* grads_max, void* stream);
+                  int64_t n_points, const float* out, const float* grad_out, const uint32_t* mask, const float* act,
+                  int64_t act_rows, float* grads, int64_t grads_rows, uint32_t* grads_max, void* stream);
 
 /* Weight gradients of linear layers, dW = G^T X and db = sum_rows G (the
  * parameter half of nn.Linear's autograd, models.py:541-592), for up to

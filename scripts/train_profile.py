@@ -2,7 +2,7 @@
 their input shapes and the Python call sites of the copies / cats / fills (what the kernel list calls
 direct_copy, CatArrayBatchedCopy, FillFunctor). Not part of the product or the bench.
 
-env: CONF (default_mv | default), STEPS, RENDERER (volume | adaptive: AdaptiveVolumeRenderer, train.py:268-273)
+env: CONF (default_mv | default), STEPS, BN (1: train.py --bn), RENDERER (volume | adaptive: AdaptiveVolumeRenderer, train.py:268-273)
 """
 import os
 import sys
@@ -19,7 +19,7 @@ from avr.renderers import AdaptiveVolumeRenderer, VolumeRenderer  # noqa: E402
 
 dev = torch.device("cuda:0")
 SB, R = 4, 512
-net = bench.build_scene(dev, conf=os.environ.get("CONF", "default_mv"))
+net = bench.build_scene(dev, conf=os.environ.get("CONF", "default_mv"), bn=os.environ.get("BN", "0") == "1")
 g = torch.Generator(device="cpu").manual_seed(7)
 net.encoder.set_latent(torch.randn(SB, net.d_latent, 64, 64, generator=g).to(dev))
 net.num_objs = SB

@@ -127,9 +127,12 @@ int main(void) {
   d.spade = 0;
   d.beta = -1.f;
   expect("negative beta", avr_field_packed_floats(&d, &n), AVR_E_INVALID);
-  d.beta = 2.f;
-  expect("softplus training rejected", avr_field_fwd_points_train(&d, &v, 1, buf, buf, buf, buf, 4, buf, buf, 4,
-                                                                  (uint32_t*)buf, NULL, NULL, 0, NULL, NULL), AVR_E_INVALID);
+  d.beta = 0.f; d.spade = 1;   /* use_spade trains on the module path (Softplus trains on HIP since ABI 11) */
+  expect("spade training rejected", avr_field_fwd_points_train(&d, &v, 1, buf, buf, buf, buf, 4, buf, buf, 4,
+                                                               (uint32_t*)buf, NULL, NULL, 0, NULL, NULL), AVR_E_INVALID);
+  d.spade = 0; d.beta = 2.f;
+  expect("softplus backward without act rows", avr_field_bwd(&d, buf, buf, 1, 4, buf, buf, (uint32_t*)buf, NULL, 0,
+                                                             buf, 4, NULL, NULL), AVR_E_INVALID);
   d.precision = AVR_FIELD_FP32;
   expect("softplus on fp32 rejected", avr_field_fwd_points(&d, &v, buf, buf, buf, buf, 4, buf, NULL), AVR_E_INVALID);
   d.precision = AVR_FIELD_X3;

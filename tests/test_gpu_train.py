@@ -13,12 +13,13 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
 
 
-def _net(d_hidden, n_blocks=3, d_latent=64, hw=(8, 8), combine_layer=1000, sb=1, seed=0):
+def _net(d_hidden, n_blocks=3, d_latent=64, hw=(8, 8), combine_layer=1000, sb=1, seed=0, beta=0.0):
     from avr.conf import Conf, default_conf
     from avr.scene import synthetic_scene
     conf = default_conf()["model"]
     d = dict(conf)
-    mlp = {"type": "resnet", "n_blocks": n_blocks, "d_hidden": d_hidden, "combine_layer": combine_layer}
+    mlp = {"type": "resnet", "n_blocks": n_blocks, "d_hidden": d_hidden, "combine_layer": combine_layer,
+           "beta": beta}
     d["mlp_coarse"], d["mlp_fine"] = dict(mlp), dict(mlp)
     d["encoder"] = {"backbone": "resnet34", "pretrained": False,
                     "num_layers": {64: 1, 128: 2, 256: 3, 512: 4}[d_latent]}
@@ -118,6 +119,26 @@ def test_field_train_grads_match_torch_autograd(d_hidden, n_blocks, combine_laye
     _, g_d, _ = _fp64(net, lambda: _grads(net, xyz.double(), vd.double(), w.double(), True, hip=False))
     worst = _compare64(g_h, g_t, g_d)
     print(f"d_hidden {d_hidden}: worst HIP gradient error vs float64 {worst:.2e} of max |grad|")
+
+
+@pytest.mark.parametrize("d_hidden,n_blocks,combine_layer,beta", [(64, 3, 1000, 1.0), (128, 5, 3, 2.0),
+                                                                 (512, 5, 3, 1.5)])
+def test_field_train_softplus_grads_match_fp64(d_hidden, n_blocks, combine_layer, beta):
+    """ResnetFC(beta > 0): Softplus(beta) everywhere the ReLU would be (models.py:442-445, 536-537), trained on
+    the fused kernels (ABI 11): the training forward's SAVE instantiation with the Softplus epilogues, the
+    backward chain taking the activation's slope from the saved activations (1 - exp(-beta y))."""
+    from avr.field import softplus_beta
+    d_latent = 512 if d_hidden == 512 else 64
+    net = _net(d_hidden, n_blocks, d_latent, (16, 16) if d_hidden == 512 else (8, 8), combine_layer, beta=beta)
+    assert softplus_beta(net.mlp_coarse) == beta
+    xyz, vd, w = _points(1, 900, seed=5)
+    assert net.can_train_fused(xyz, vd)
+    out_h, g_h, _ = _grads(net, xyz, vd, w, True, hip=True)
+    out_t, g_t, _ = _grads(net, xyz, vd, w, True, hip=False)
+    np.testing.assert_allclose(out_h.cpu().numpy(), out_t.cpu().numpy(), atol=1e-4)
+    _, g_d, _ = _fp64(net, lambda: _grads(net, xyz.double(), vd.double(), w.double(), True, hip=False))
+    worst = _compare64(g_h, g_t, g_d)
+    print(f"softplus({beta}) d_hidden {d_hidden}: worst HIP gradient error vs float64 {worst:.2e} of max |grad|")
 
 
 def test_field_train_multi_scene_fine_mlp_and_latent_grad():
