@@ -78,6 +78,13 @@ def _run(dims, layer, stream):
     call("avr_bn_layer_run", ctypes.byref(dims), ctypes.byref(layer), stream)
 
 
+def _partial(M, H, dev):
+    """The per-workgroup column partials of avr_bn_layer_run plus the fold scratch of avr_bn_stats."""
+    n = ctypes.c_int64(0)
+    call("avr_bn_partial_floats", M, H, ctypes.byref(n))
+    return torch.empty(n.value, device=dev, dtype=F32)
+
+
 def _momentum(bn):
     """torch's BatchNorm momentum, None = cumulative average (1 / num_batches_tracked after the increment)."""
     if bn.momentum is None:
@@ -167,8 +174,7 @@ class _FieldTrainBN(torch.autograd.Function):
             N = torch.empty(max(nb, 1), M, H, device=dev, dtype=F32)    # fc_0 outputs (pre-BN)
             A = torch.empty(2 * nb, M, H, device=dev, dtype=F32)        # GEMM inputs (after BN + relu)
             amax = torch.zeros(2 * nb + 2, device=dev, dtype=torch.int32)
-            n_wg = -(-M // 64)
-            part = torch.empty(n_wg, 2, H, device=dev, dtype=F32)
+            part = _partial(M, H, dev)
             st1 = [_Stats(H, dev) for _ in range(nb)]
             st2 = [_Stats(H, dev) for _ in range(nb)]
             bns = _bn_blocks(mlp)
@@ -230,8 +236,7 @@ class _FieldTrainBN(torch.autograd.Function):
             dn_max = torch.zeros(max(nb, 1), device=dev, dtype=torch.int32)
             gp2 = torch.empty(M, H, device=dev, dtype=F32)
             gp1 = torch.empty(max(nb, 1), M, H, device=dev, dtype=F32)
-            n_wg = -(-M // 64)
-            part = torch.empty(n_wg, 2, H, device=dev, dtype=F32)
+            part = _partial(M, H, dev)
             dgam = torch.zeros(nb, H, device=dev, dtype=F32)
             dbet = torch.zeros(nb, H, device=dev, dtype=F32)
             gs1 = [torch.empty(3, H, device=dev, dtype=F32) for _ in range(nb)]   # coef, m1, m2 of point 1

@@ -67,7 +67,9 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   constexpr int MAXQ = 512 / 4 / NW;        // operand column groups per wave (K <= 512)
   extern __shared__ float lds[];
   uint4* X16 = reinterpret_cast<uint4*>(lds);
-  float* red = lds + a.KC * 2048;
+  // the stages (prologue K + 4, epilogue HID + 4 floats a row; X aliases them), the column sums, then red
+  const int stage_f = kX3Samples * ((a.K > HID ? a.K : HID) + 4);
+  float* red = lds + stage_f + NW * HID;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, j = lane & 15;
   const int64_t m0 = (int64_t)blockIdx.x * kX3Samples;
@@ -77,27 +79,33 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   prefetch_a<FT, TWO ? FT : kPrefetch>(A0, W, lane);
 
   // ---------------------------------------------------------------- operand
-  const int qpw = a.K / 4 / NW;              // column groups of this wave
-  const bool valid = lane < nvalid;
-  const int64_t row = m0 + (valid ? lane : 0);
-  floatx4 xv[MAXQ];
+  // Phase A, coalesced: wave w takes rows w, w + NW, ...; lane l column groups l, l + 64, ... of the row (one
+  // 1-KB row segment per load), applies the prologue's transform with its columns' parameters and writes the
+  // fp32 values into an LDS stage, row stride 4 K + 16 B. Phase B: lane = row reads its operand columns back
+  // (the +16 B row pad spreads the 64 rows over the banks) and splits them into X, which aliases the stage
+  // (the values wait in registers across the barrier).
+  const int G4 = a.K / 4;                    // column groups of a row
+  const int rs = a.K + 4;                    // stage row stride (floats)
   float mx = 0.f;
+  // pair i of this lane: row wid + NW (i >> 1), column group lane + 64 (i & 1) (K <= 512: <= 2 per row);
+  // fully unrolled so every load of a pair is issued before the first one is used
 #pragma unroll
   for (int i = 0; i < MAXQ; ++i) {
-    xv[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-    if (i < qpw) {
-      const int k = 4 * (qpw * wid + i);
+    const int r = wid + NW * (i >> 1), q = lane + 64 * (i & 1);
+    if (r < kX3Samples && q < G4) {
+      const bool live = r < nvalid;
+      const int64_t row = m0 + (live ? r : 0);
+      const int k = 4 * q;
       floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
       if (k + 4 <= a.kin) {
         v = ld4(a.src + row * a.ld_src + k);
       } else if (k < a.kin) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = k + r < a.kin ? a.src[row * a.ld_src + k + r] : 0.f;
+        for (int t = 0; t < 4; ++t) v[t] = k + t < a.kin ? a.src[row * a.ld_src + k + t] : 0.f;
       }
       if (k < a.kin) {
         if (a.prologue == AVR_BN_RELU) {
-          const floatx4 mu = ld4(a.in_mu + k), sc = ld4(a.in_scale + k), sh = ld4(a.in_shift + k);
-          v = (v - mu) * sc + sh;
+          v = (v - ld4(a.in_mu + k)) * ld4(a.in_scale + k) + ld4(a.in_shift + k);
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         } else if (a.prologue == AVR_BN_GRAD) {
           const floatx4 xh = (ld4(a.src_pre + row * a.ld_src + k) - ld4(a.in_mu + k)) * ld4(a.in_invstd + k);
@@ -105,10 +113,9 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
           if (a.src_res) v += ld4(a.src_res + row * a.ld_src + k);
         }
       }
-      if (!valid) v = floatx4{0.f, 0.f, 0.f, 0.f};
-      else if (a.opnd_out)
-        __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a.opnd_out + (m0 + lane) * a.K + k));
-      xv[i] = v;
+      if (!live) v = floatx4{0.f, 0.f, 0.f, 0.f};
+      else if (a.opnd_out) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a.opnd_out + row * a.K + k));
+      *reinterpret_cast<floatx4*>(lds + r * rs + k) = v;
       mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
   }
@@ -118,6 +125,12 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   const float wgmax = red_max<NW>(red);
   if (a.opnd_max && wid == 0 && lane == 0 && wgmax > 0.f) atomicMax(a.opnd_max, __float_as_uint(wgmax));
   const float s_x = pow2_scale_for(wgmax);
+  const int qpw = a.K / 4 / NW;              // phase B: column groups of this wave
+  floatx4 xv[MAXQ];
+#pragma unroll
+  for (int i = 0; i < MAXQ; ++i)
+    if (i < qpw) xv[i] = *reinterpret_cast<const floatx4*>(lds + lane * rs + 4 * (qpw * wid + i));
+  lds_barrier();
   char* xb = reinterpret_cast<char*>(X16);
 #pragma unroll
   for (int i = 0; i < MAXQ; ++i) {
@@ -138,70 +151,124 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   const float inv = 1.0f / (pow2_scale_for(__uint_as_float(a.hdr[a.hdr_idx])) * s_x);
 
   // ---------------------------------------------------------------- epilogue
-  float* part = a.part + (int64_t)blockIdx.x * 2 * HID;
-  const float rn = 1.0f / (float)nvalid;
+  // The accumulators (feature-major in the registers) go to an fp32 stage in LDS (row-major, aliasing X), and
+  // the rows are finished like the prologue's: wave = rows, lane = column groups, so the addend / mask / pre-BN
+  // row loads and the row stores are coalesced 1-KB segments. The workgroup's column statistics are per-lane
+  // sums over the wave's rows, met across the waves in LDS.
+  constexpr int EQ = HID / 4;                // column groups of an output row
+  constexpr int es = HID + 4;                // stage row stride (floats)
+  float* colred = lds + stage_f;             // (NW, HID) per-wave column sums, past the stages
+  __syncthreads();                           // every wave has left the GEMM (the stage overwrites X)
 #pragma unroll
   for (int ft = 0; ft < FT; ++ft) {
     const int f0 = 16 * (FT * wid + ft) + 4 * g;
-    floatx4 s1 = floatx4{0.f, 0.f, 0.f, 0.f}, s2 = s1;
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) *reinterpret_cast<floatx4*>(lds + (16 * sg + j) * es + f0) = acc[ft][sg] * inv;
+  }
+  __syncthreads();
+  floatx4 yv[MAXQ];
+  floatx4 s1[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}}, s2[2] = {s1[0], s1[0]};
+  floatx4 cp0[2], cp1[2];                    // per-column parameters of the lane's two groups
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int f = 4 * (lane + 64 * h) < HID ? 4 * (lane + 64 * h) : 0;
     if constexpr (MODE == AVR_BN_FWD) {
-      const floatx4 b = a.bias ? ld4(a.bias + f0) : floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int sg = 0; sg < 4; ++sg) {
-        const int s = 16 * sg + j;
-        const int64_t m = m0 + (s < nvalid ? s : 0);
-        floatx4 y = acc[ft][sg] * inv + b;
-        if (a.add1) y += ld4(a.add1 + m * HID + f0);
-        if (a.add2) y += ld4(a.add2 + m * HID + f0);
-        acc[ft][sg] = y;
-        if (s < nvalid) {
-          *reinterpret_cast<floatx4*>(a.out + m * HID + f0) = y;
-          s1 += y;
-        }
-      }
-      const floatx4 mean = sum16(s1) * rn;     // this workgroup's column means, then sum of squared deviations
-#pragma unroll
-      for (int sg = 0; sg < 4; ++sg) {
-        const floatx4 d = acc[ft][sg] - mean;
-        if (16 * sg + j < nvalid) s2 += d * d;
-      }
-      s2 = sum16(s2);
-      s1 = mean;
+      cp0[h] = a.bias ? ld4(a.bias + f) : floatx4{0.f, 0.f, 0.f, 0.f};
+      cp1[h] = cp0[h];
     } else {
-      const floatx4 mu = ld4(a.out_mu + f0), is = ld4(a.out_invstd + f0);
+      cp0[h] = ld4(a.out_mu + f);
+      cp1[h] = ld4(a.out_invstd + f);
+    }
+  }
 #pragma unroll
-      for (int sg = 0; sg < 4; ++sg) {
-        const int s = 16 * sg + j;
-        const int64_t m = m0 + (s < nvalid ? s : 0);
-        const floatx4 d = acc[ft][sg] * inv;
-        const floatx4 z = ld4(a.mask_rows + m * HID + f0);
+  for (int i = 0; i < MAXQ; ++i) {
+    const int r = wid + NW * (i >> 1), q = lane + 64 * (i & 1);
+    yv[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (r < kX3Samples && q < EQ) {
+      const bool live = r < nvalid;
+      const int64_t row = m0 + (live ? r : 0);
+      const int f = 4 * q;
+      floatx4 v = *reinterpret_cast<const floatx4*>(lds + r * es + f);
+      if constexpr (MODE == AVR_BN_FWD) {
+        v += cp0[i & 1];
+        if (a.add1) v += ld4(a.add1 + row * HID + f);
+        if (a.add2) v += ld4(a.add2 + row * HID + f);
+        if (live) {
+          *reinterpret_cast<floatx4*>(a.out + row * HID + f) = v;
+          s1[i & 1] += v;
+          yv[i] = v;
+        }
+      } else {
+        const floatx4 z = ld4(a.mask_rows + row * HID + f);
         floatx4 gp;
-        gp.x = z.x > 0.f ? d.x : 0.f; gp.y = z.y > 0.f ? d.y : 0.f;
-        gp.z = z.z > 0.f ? d.z : 0.f; gp.w = z.w > 0.f ? d.w : 0.f;
-        if (s < nvalid) {
-          *reinterpret_cast<floatx4*>(a.out + m * HID + f0) = gp;
-          const floatx4 xh = (ld4(a.pre_rows + m * HID + f0) - mu) * is;
-          s1 += gp;
-          s2 += gp * xh;
+        gp.x = z.x > 0.f ? v.x : 0.f; gp.y = z.y > 0.f ? v.y : 0.f;
+        gp.z = z.z > 0.f ? v.z : 0.f; gp.w = z.w > 0.f ? v.w : 0.f;
+        if (live) {
+          *reinterpret_cast<floatx4*>(a.out + row * HID + f) = gp;
+          const floatx4 xh = (ld4(a.pre_rows + row * HID + f) - cp0[i & 1]) * cp1[i & 1];
+          s1[i & 1] += gp;
+          s2[i & 1] += gp * xh;
         }
       }
-      s1 = sum16(s1);
-      s2 = sum16(s2);
     }
-    if (j == 0) {
-      *reinterpret_cast<floatx4*>(part + f0) = s1;
-      *reinterpret_cast<floatx4*>(part + HID + f0) = s2;
+  }
+  float* part = a.part + (int64_t)blockIdx.x * 2 * HID;
+  // the waves' column sums meet in one LDS slot (NW x HID), used twice: sums of y (-> the means, needed by
+  // every lane for the squared deviations) or of gp, then M2 or the sums of gp * xhat
+  const auto put = [&](const floatx4 (&v)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (lane + 64 * h < EQ) *reinterpret_cast<floatx4*>(colred + wid * HID + 4 * (lane + 64 * h)) = v[h];
+  };
+  const auto total = [&](int h) {
+    floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (lane + 64 * h < EQ)
+      for (int w = 0; w < NW; ++w) t += *reinterpret_cast<const floatx4*>(colred + w * HID + 4 * (lane + 64 * h));
+    return t;
+  };
+  put(s1);
+  __syncthreads();
+  floatx4 t1[2] = {total(0), total(1)};
+  __syncthreads();
+  if constexpr (MODE == AVR_BN_FWD) {
+    const float rn = 1.0f / (float)nvalid;
+    t1[0] *= rn;                             // this workgroup's column means
+    t1[1] *= rn;
+#pragma unroll
+    for (int i = 0; i < MAXQ; ++i) {
+      const int r = wid + NW * (i >> 1);
+      if (r < nvalid) {
+        const floatx4 d = yv[i] - t1[i & 1];
+        s2[i & 1] += d * d;
+      }
+    }
+  }
+  put(s2);
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const floatx4 t2 = total(h);
+      const int f = 4 * (lane + 64 * h);
+      if (f < HID) {
+        *reinterpret_cast<floatx4*>(part + f) = t1[h];
+        *reinterpret_cast<floatx4*>(part + HID + f) = t2;
+      }
     }
   }
 }
 
 template <int FT, int NW, int MODE>
 static int launch_bn_layer(const BnArgs& a, hipStream_t s) {
-  const size_t shm = (size_t)a.KC * 8192 + 64;
+  // the larger of the prologue's and the epilogue's fp32 stage (X aliases them) + the column sums + red
+  constexpr int HID = 16 * FT * NW;
+  const size_t stage = (size_t)kX3Samples * ((a.K > HID ? a.K : HID) + 4) * 4;
+  const size_t shm = stage + (size_t)NW * HID * 4 + 64;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&bn_layer_kernel<FT, NW, MODE>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 16 * 8192 + 64) != hipSuccess)
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kX3Samples * (512 + 4) * 4 + NW * HID * 4 + 64) != hipSuccess)
       return fail(AVR_E_HIP, "bn_layer_kernel: cannot set dynamic LDS");
     attr = true;
   }
@@ -223,84 +290,52 @@ static int dispatch_bn_layer(int H, const BnArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ finalize
-// Block = 256 threads over 16 columns: thread (w, c) combines the partials of workgroups w, w + 16, ... of
-// column c in fp64, then the 16 threads of a column meet in LDS.
-constexpr int kBnCols = 16, kBnLanesPerCol = 16;
-
-__global__ void __launch_bounds__(256) bn_stats_kernel(const float* __restrict__ part, int64_t M, int N,
-                                                       const float* __restrict__ gamma, float eps, float momentum,
-                                                       float* running_mean, float* running_var, float* mu_out,
-                                                       float* invstd_out, float* scale_out) {
-  __shared__ double sn[256], smean[256], sm2[256];
-  const int c = blockIdx.x * kBnCols + (threadIdx.x % kBnCols);
-  const int w0 = threadIdx.x / kBnCols;
-  const int64_t nwg = (M + kX3Samples - 1) / kX3Samples;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  if (c < N) {
-    for (int64_t w = w0; w < nwg; w += kBnLanesPerCol) {   // Chan: combine (n, mean, M2) of two sets
-      const double nb = (double)(M - w * kX3Samples < kX3Samples ? M - w * kX3Samples : kX3Samples);
-      const double mb = part[w * 2 * N + c], m2b = part[w * 2 * N + N + c];
-      const double nt = n + nb, d = mb - mean;
-      mean += d * nb / nt;
-      m2 += m2b + d * d * n * nb / nt;
-      n = nt;
-    }
-  }
-  sn[threadIdx.x] = n; smean[threadIdx.x] = mean; sm2[threadIdx.x] = m2;
-  __syncthreads();
-  if (w0 == 0 && c < N) {
-    for (int t = 1; t < kBnLanesPerCol; ++t) {
-      const int i = t * kBnCols + threadIdx.x;
-      const double nb = sn[i];
-      if (nb == 0.0) continue;
-      const double nt = n + nb, d = smean[i] - mean;
-      mean += d * nb / nt;
-      m2 += sm2[i] + d * d * n * nb / nt;
-      n = nt;
-    }
-    const double var = m2 / n;                                  // biased: the normalisation (torch)
-    const float istd = (float)(1.0 / sqrt(var + (double)eps));
-    mu_out[c] = (float)mean;
-    invstd_out[c] = istd;
-    scale_out[c] = gamma[c] * istd;
-    if (running_mean) {                                         // torch: unbiased variance in the running stat
-      const float unb = (float)(n > 1.0 ? m2 / (n - 1.0) : var);
-      running_mean[c] = momentum * (float)mean + (1.0f - momentum) * running_mean[c];
-      running_var[c] = momentum * unb + (1.0f - momentum) * running_var[c];
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256) bn_grad_stats_kernel(const float* __restrict__ part, int64_t M, int N,
-                                                            const float* __restrict__ gamma,
-                                                            const float* __restrict__ invstd, float* coef, float* m1,
-                                                            float* m2, float* dgamma, float* dbeta) {
-  __shared__ double s1[256], s2[256];
-  const int c = blockIdx.x * kBnCols + (threadIdx.x % kBnCols);
-  const int w0 = threadIdx.x / kBnCols;
-  const int64_t nwg = (M + kX3Samples - 1) / kX3Samples;
+__global__ void __launch_bounds__(64) bn_stats_kernel(const double* __restrict__ fold, int nfold, int64_t M, int N,
+                                                      const float* __restrict__ gamma, float eps, float momentum,
+                                                      float* running_mean, float* running_var, float* mu_out,
+                                                      float* invstd_out, float* scale_out) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= N) return;
   double a = 0.0, b = 0.0;
-  if (c < N)
-    for (int64_t w = w0; w < nwg; w += kBnLanesPerCol) {
-      a += part[w * 2 * N + c];
-      b += part[w * 2 * N + N + c];
-    }
-  s1[threadIdx.x] = a; s2[threadIdx.x] = b;
-  __syncthreads();
-  if (w0 == 0 && c < N) {
-    for (int t = 1; t < kBnLanesPerCol; ++t) {
-      a += s1[t * kBnCols + threadIdx.x];
-      b += s2[t * kBnCols + threadIdx.x];
-    }
-    m1[c] = (float)(a / (double)M);
-    m2[c] = (float)(b / (double)M);
-    coef[c] = gamma[c] * invstd[c];
-    dbeta[c] += (float)a;       // bn_0 is applied twice per block: both applications add into its gradients
-    dgamma[c] += (float)b;
+  for (int f = 0; f < nfold; ++f) {
+    a += fold[(int64_t)f * 2 * N + c];
+    b += fold[(int64_t)f * 2 * N + N + c];
+  }
+  const double n = (double)M, mean = a / n;
+  const double m2 = fmax(b - n * mean * mean, 0.0);
+  const double var = m2 / n;                                    // biased: the normalisation (torch)
+  const float istd = (float)(1.0 / sqrt(var + (double)eps));
+  mu_out[c] = (float)mean;
+  invstd_out[c] = istd;
+  scale_out[c] = gamma[c] * istd;
+  if (running_mean) {                                           // torch: unbiased variance in the running stat
+    const float unb = (float)(n > 1.0 ? m2 / (n - 1.0) : var);
+    running_mean[c] = momentum * (float)mean + (1.0f - momentum) * running_mean[c];
+    running_var[c] = momentum * unb + (1.0f - momentum) * running_var[c];
   }
 }
 
-__global__ void __launch_bounds__(256) bn_grad_rows_kernel(int64_t n4, int N4, const floatx4* __restrict__ gr,
+__global__ void __launch_bounds__(64) bn_grad_stats_kernel(const double* __restrict__ fold, int nfold, int64_t M,
+                                                           int N, const float* __restrict__ gamma,
+                                                           const float* __restrict__ invstd, float* coef, float* m1,
+                                                           float* m2, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= N) return;
+  double a = 0.0, b = 0.0;
+  for (int f = 0; f < nfold; ++f) {
+    a += fold[(int64_t)f * 2 * N + c];
+    b += fold[(int64_t)f * 2 * N + N + c];
+  }
+  m1[c] = (float)(a / (double)M);
+  m2[c] = (float)(b / (double)M);
+  coef[c] = gamma[c] * invstd[c];
+  dbeta[c] += (float)a;       // bn_0 is applied twice per block: both applications add into its gradients
+  dgamma[c] += (float)b;
+}
+
+// Grid (column groups of 4 x 64, rows / 4): thread (x, y) handles column group 64 blockIdx.x + (x & 63) of row
+// 4 blockIdx.y + (x >> 6): coalesced 1-KB row segments, the column parameters loaded once per thread.
+__global__ void __launch_bounds__(256) bn_grad_rows_kernel(int64_t n_rows, int N4, const floatx4* __restrict__ gr,
                                                            const floatx4* __restrict__ pre,
                                                            const floatx4* __restrict__ res,
                                                            const floatx4* __restrict__ coef,
@@ -309,21 +344,56 @@ __global__ void __launch_bounds__(256) bn_grad_rows_kernel(int64_t n4, int N4, c
                                                            const floatx4* __restrict__ mu,
                                                            const floatx4* __restrict__ invstd, floatx4* out,
                                                            unsigned* out_max) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int64_t r0 = (int64_t)blockIdx.y * 16 + (threadIdx.x >> 6);
   float mx = 0.f;
-  if (i < n4) {
-    const int c = (int)(i % N4);
-    const floatx4 xh = (pre[i] - mu[c]) * invstd[c];
-    floatx4 v = (gr[i] - m1[c] - xh * m2[c]) * coef[c];
-    if (res) v += res[i];
-    out[i] = v;
-    mx = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+  if (c < N4) {
+    const floatx4 cf = coef[c], a1 = m1[c], a2 = m2[c], u = mu[c], is = invstd[c];
+#pragma unroll 4
+    for (int64_t r = r0; r < n_rows && r < (int64_t)blockIdx.y * 16 + 16; r += 4) {
+      const int64_t i = r * N4 + c;
+      floatx4 v = (gr[i] - a1 - (pre[i] - u) * is * a2) * cf;
+      if (res) v += res[i];
+      out[i] = v;
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
   }
   mx = wave_max(mx);
   if (out_max && (threadIdx.x & 63) == 0 && mx > 0.f) atomicMax(out_max, __float_as_uint(mx));
 }
 
+// Two-stage finalize: stage 1 (grid column blocks x row groups of 16 partials, one wave each: lane = column,
+// coalesced 256-B partial rows) folds 16 workgroups' partials into fp64 sums; stage 2 (one wave per 64 columns)
+// folds those. Forward partials are per-workgroup (mean, M2) of n_i rows: A1 = sum n_i mean_i and
+// A2 = sum (M2_i + n_i mean_i^2), then M2 = A2 - n mean^2 (fp64: no Chan divisions, no cancellation at fp32
+// scale). Backward partials are plain sums.
+constexpr int kBnFold = 16;
+
+template <bool FWD>
+__global__ void __launch_bounds__(64) bn_fold_kernel(const float* __restrict__ part, int64_t M, int N,
+                                                     double* __restrict__ fold) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  const int64_t nwg = (M + kX3Samples - 1) / kX3Samples;
+  double a = 0.0, b = 0.0;
+  if (c < N) {
+    for (int64_t w = (int64_t)blockIdx.y * kBnFold; w < nwg && w < (int64_t)(blockIdx.y + 1) * kBnFold; ++w) {
+      const float p0 = part[w * 2 * N + c], p1 = part[w * 2 * N + N + c];
+      if constexpr (FWD) {
+        const double n = (double)(M - w * kX3Samples < kX3Samples ? M - w * kX3Samples : kX3Samples);
+        a += n * (double)p0;
+        b += (double)p1 + n * (double)p0 * (double)p0;
+      } else {
+        a += (double)p0;
+        b += (double)p1;
+      }
+    }
+    fold[(int64_t)blockIdx.y * 2 * N + c] = a;
+    fold[(int64_t)blockIdx.y * 2 * N + N + c] = b;
+  }
+}
+
 }  // namespace avr
+
 
 using namespace avr;
 
@@ -389,14 +459,44 @@ extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* 
   return l->mode == AVR_BN_FWD ? dispatch_bn_layer<AVR_BN_FWD>(H, a, s) : dispatch_bn_layer<AVR_BN_BWD>(H, a, s);
 }
 
+// The fold scratch (fp64, 2 x n_cols per 16 partials) lives in the partial buffer past the partials
+// (avr_bn_partial_floats sizes it), so the entry points allocate nothing.
+static int64_t bn_n_fold(int64_t n_rows) { return ((n_rows + kX3Samples - 1) / kX3Samples + kBnFold - 1) / kBnFold; }
+
+extern "C" int avr_bn_partial_floats(int64_t n_rows, int n_cols, int64_t* n_floats) {
+  AVR_REQUIRE(n_rows >= 0 && n_cols > 0 && n_floats, "avr_bn_partial_floats: bad argument");
+  const int64_t nwg = (n_rows + kX3Samples - 1) / kX3Samples;
+  // partials (nwg, 2, n_cols) fp32, then 8-B aligned fold rows (n_fold, 2, n_cols) fp64
+  *n_floats = (nwg * 2 * n_cols + 1) / 2 * 2 + bn_n_fold(n_rows) * 2 * n_cols * 2;
+  return AVR_OK;
+}
+
+static const float* bn_fold(const float* partial, int64_t n_rows, int n_cols, bool fwd, double** fold,
+                            hipStream_t s) {
+  const int64_t nwg = (n_rows + kX3Samples - 1) / kX3Samples;
+  *fold = reinterpret_cast<double*>(const_cast<float*>(partial) + (nwg * 2 * n_cols + 1) / 2 * 2);
+  const dim3 grid((unsigned)((n_cols + 63) / 64), (unsigned)bn_n_fold(n_rows));
+  if (fwd)
+    bn_fold_kernel<true><<<grid, 64, 0, s>>>(partial, n_rows, n_cols, *fold);
+  else
+    bn_fold_kernel<false><<<grid, 64, 0, s>>>(partial, n_rows, n_cols, *fold);
+  return partial;
+}
+
 extern "C" int avr_bn_stats(const float* partial, int64_t n_rows, int n_cols, const float* gamma, float eps,
                             float momentum, float* running_mean, float* running_var, float* mu, float* invstd,
                             float* scale, void* stream) {
   AVR_REQUIRE(n_rows >= 2, "avr_bn_stats: BatchNorm in training mode needs more than 1 value per channel");
   AVR_REQUIRE(n_cols > 0 && partial && gamma && mu && invstd && scale, "avr_bn_stats: bad argument");
   AVR_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "avr_bn_stats: running mean / var together");
-  bn_stats_kernel<<<(unsigned)((n_cols + kBnCols - 1) / kBnCols), 256, 0, as_stream(stream)>>>(
-      partial, n_rows, n_cols, gamma, eps, momentum, running_mean, running_var, mu, invstd, scale);
+  hipStream_t s = as_stream(stream);
+  double* fold;
+  bn_fold(partial, n_rows, n_cols, true, &fold, s);
+  int rc = check_launch("bn_fold_kernel");
+  if (rc) return rc;
+  bn_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 64, 0, s>>>(fold, (int)bn_n_fold(n_rows), n_rows, n_cols, gamma,
+                                                                 eps, momentum, running_mean, running_var, mu, invstd,
+                                                                 scale);
   return check_launch("bn_stats_kernel");
 }
 
@@ -405,8 +505,13 @@ extern "C" int avr_bn_grad_stats(const float* partial, int64_t n_rows, int n_col
                                  void* stream) {
   AVR_REQUIRE(n_rows >= 1 && n_cols > 0, "avr_bn_grad_stats: bad sizes");
   AVR_REQUIRE(partial && gamma && invstd && coef && m1 && m2 && dgamma && dbeta, "avr_bn_grad_stats: null pointer");
-  bn_grad_stats_kernel<<<(unsigned)((n_cols + kBnCols - 1) / kBnCols), 256, 0, as_stream(stream)>>>(
-      partial, n_rows, n_cols, gamma, invstd, coef, m1, m2, dgamma, dbeta);
+  hipStream_t s = as_stream(stream);
+  double* fold;
+  bn_fold(partial, n_rows, n_cols, false, &fold, s);
+  int rc = check_launch("bn_fold_kernel");
+  if (rc) return rc;
+  bn_grad_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 64, 0, s>>>(fold, (int)bn_n_fold(n_rows), n_rows, n_cols,
+                                                                      gamma, invstd, coef, m1, m2, dgamma, dbeta);
   return check_launch("bn_grad_stats_kernel");
 }
 
@@ -416,9 +521,10 @@ extern "C" int avr_bn_grad_rows(int64_t n_rows, int n_cols, const float* g, cons
   AVR_REQUIRE(n_rows >= 0 && n_cols > 0 && n_cols % 4 == 0, "avr_bn_grad_rows: bad sizes");
   if (n_rows == 0) return AVR_OK;
   AVR_REQUIRE(g && pre && coef && m1 && m2 && mu && invstd && out, "avr_bn_grad_rows: null pointer");
-  const int64_t n4 = n_rows * (n_cols / 4);
-  bn_grad_rows_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, as_stream(stream)>>>(
-      n4, n_cols / 4, reinterpret_cast<const floatx4*>(g), reinterpret_cast<const floatx4*>(pre),
+  const int N4 = n_cols / 4;
+  const dim3 grid((unsigned)((N4 + 63) / 64), (unsigned)((n_rows + 15) / 16));
+  bn_grad_rows_kernel<<<grid, 256, 0, as_stream(stream)>>>(
+      n_rows, N4, reinterpret_cast<const floatx4*>(g), reinterpret_cast<const floatx4*>(pre),
       reinterpret_cast<const floatx4*>(res), reinterpret_cast<const floatx4*>(coef),
       reinterpret_cast<const floatx4*>(m1), reinterpret_cast<const floatx4*>(m2),
       reinterpret_cast<const floatx4*>(mu), reinterpret_cast<const floatx4*>(invstd),

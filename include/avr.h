@@ -391,9 +391,12 @@ typedef struct {
   float* out;                                                 /* (n_rows, d_hidden) */
   const float* mask_rows; const float* pre_rows;              /* AVR_BN_BWD (ld d_hidden) */
   const float* out_mu; const float* out_invstd;
-  float* partial;           /* (ceil(n_rows / 64), 2, d_hidden) */
+  float* partial;           /* (ceil(n_rows / 64), 2, d_hidden), within avr_bn_partial_floats floats */
 } avr_bn_layer;
 int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* l, void* stream);
+/* Floats of an avr_bn_layer partial buffer for n_rows rows of n_cols columns: the per-workgroup partials
+ * followed by the fp64 scratch avr_bn_stats / avr_bn_grad_stats fold them through (no allocation inside). */
+int avr_bn_partial_floats(int64_t n_rows, int n_cols, int64_t* n_floats);
 int avr_bn_stats(const float* partial, int64_t n_rows, int n_cols, const float* gamma, float eps, float momentum,
                  float* running_mean, float* running_var, float* mu, float* invstd, float* scale, void* stream);
 int avr_bn_grad_stats(const float* partial, int64_t n_rows, int n_cols, const float* gamma, const float* invstd,
