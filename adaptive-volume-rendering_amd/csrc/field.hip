@@ -19,6 +19,8 @@
 // lin_z is applied to the latent map per texel (avr_field_latent_table) and
 // bilinearly interpolated per sample; every bias (b_in + bz0, b1 + bz_{b+1},
 // ...) is pre-summed at pack time.
+#include <mutex>
+
 #include "field_common.h"
 
 namespace avr {
@@ -567,9 +569,44 @@ static int field_common(const avr_field_dims* dims, const avr_view_desc* view, c
   return AVR_OK;
 }
 
+// The precision each blob was packed for (avr_field_pack): an AVR_FIELD_X3 blob holds no fp32 fragments of
+// lin_in / fc_0 / fc_1, so the fp32 kernel must not run on it. A small host-side table keyed by the blob's
+// address (the last kPackTags packs; the device header is not read back: that would synchronise the stream).
+namespace {
+constexpr int kPackTags = 128;
+struct PackTag {
+  const float* p;
+  int precision;
+};
+std::mutex g_pack_mu;
+PackTag g_pack_tags[kPackTags] = {};
+int g_pack_next = 0;
+
+void record_pack(const float* p, int precision) {
+  std::lock_guard<std::mutex> lock(g_pack_mu);
+  for (PackTag& t : g_pack_tags)
+    if (t.p == p) {
+      t.precision = precision;
+      return;
+    }
+  g_pack_tags[g_pack_next] = PackTag{p, precision};
+  g_pack_next = (g_pack_next + 1) % kPackTags;
+}
+
+int packed_precision(const float* p) {   // -1: not packed by this library instance (or evicted)
+  std::lock_guard<std::mutex> lock(g_pack_mu);
+  for (const PackTag& t : g_pack_tags)
+    if (t.p == p) return t.precision;
+  return -1;
+}
+}  // namespace
+
 static int dispatch_field(const avr_field_dims* dims, const FieldArgs& a, hipStream_t s) {
   const int d_hidden = dims->d_hidden;
   if (dims->precision == AVR_FIELD_X3) return dispatch_field_x3(d_hidden, a, s);
+  AVR_REQUIRE(packed_precision(a.packed) != AVR_FIELD_X3,
+              "field: the blob was packed for AVR_FIELD_X3 (no fp32 lin_in / fc_0 / fc_1 fragments): pack it with "
+              "AVR_FIELD_FP32 to run the fp32 kernel");
   AVR_REQUIRE(!dims->bn, "field: BatchNorm nets run on the x3 path only");
   AVR_REQUIRE(!dims->spade && !(dims->beta > 0.f), "field: use_spade / Softplus nets run on the x3 path only");
   AVR_REQUIRE(dims->precision == AVR_FIELD_FP32, "field: unknown precision %d", dims->precision);
@@ -661,7 +698,9 @@ extern "C" int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_wei
     if ((rc = add_x3(bt, Wt, H, dims->d_latent, dims->d_latent / 32, NT, hdr + kX3TabHdr + t, packed + L.x3_tab[t])))
       return rc;
   }
-  return run_x3(bt, s);
+  if ((rc = run_x3(bt, s))) return rc;
+  record_pack(packed, dims->precision);
+  return AVR_OK;
 }
 
 extern "C" int avr_field_bwd_packed_floats(const avr_field_dims* dims, int64_t* n_floats) {

@@ -220,7 +220,9 @@ typedef struct {
 int avr_field_packed_floats(const avr_field_dims* dims, int64_t* n_floats);
 /* Repack one ResnetFC into MFMA fragment order (device -> device). dims->precision selects what is packed:
  * AVR_FIELD_FP32 both the fp32 and the split-fp16 fragments, AVR_FIELD_X3 only what the x3 kernels and the
- * tables read (ABI 9) -- run the field kernels with the precision the blob was packed for. */
+ * tables read (ABI 9) -- run the field kernels with the precision the blob was packed for: the fp32 field
+ * entry points reject a blob this library packed for AVR_FIELD_X3 (AVR_E_INVALID; host-side record of the
+ * last 128 packs, round 4). */
 int avr_field_pack(const avr_field_dims* dims, const avr_resnetfc_weights* w, float* packed, void* stream);
 /* table (n_lin_z, H*W, d_hidden) = lin_z[b].weight @ latent[:, texel] (no bias;
  * the bias is folded into the packed biases). latent (d_latent, H, W).

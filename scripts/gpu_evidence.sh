@@ -7,13 +7,14 @@
 #   prof   rocprofv3 --kernel-trace --stats of a short bench command        -> $OUT/bench_kernel_stats.csv
 #   train  bench.py --mode train for each conf in CONFS (+ TRAIN_ARGS)      -> $OUT/bench_train_<conf>.log
 #   tprof  rocprofv3 kernel stats of the HIP train step (CONFS' last conf)  -> $OUT/train_kernel_stats.csv
+#   trainx the --bn and the AdaptiveVolumeRenderer train steps (default_mv) -> $OUT/bench_train_{bn,adaptive}_mv.log
 # env: TAG (default r04), STEPS (default all), PYTEST_ARGS (extra pytest args, e.g. "-k philox"), CONFS.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r04}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
-STEPS=${STEPS:-tests smoke bench prof train tprof}
+STEPS=${STEPS:-tests smoke bench prof train tprof trainx}
 CONFS=${CONFS:-default default_mv}
 export AVR_TEST_REPORT=$OUT/philox_c3_flip_rates.jsonl
 has() { [[ " $STEPS " == *" $1 "* ]]; }
@@ -50,5 +51,11 @@ if has tprof; then
   rc=$?; [ $rc -eq 0 ] || { echo "train rocprof rc=$rc"; tail -5 $OUT/tprof.log; exit $rc; }
   cp "$(find $OUT/tprof -name '*kernel_stats.csv' | head -1)" $OUT/train_kernel_stats.csv
   head -6 $OUT/train_kernel_stats.csv | cut -c1-160
+fi
+if has trainx; then
+  for x in "bn:--bn" "adaptive:--renderer adaptive"; do
+    timeout -k 10 300 python -u bench.py --mode train --conf default_mv ${x#*:} --steps 20 --warmup 5 > $OUT/bench_train_${x%%:*}_mv.log 2>&1
+    rc=$?; tail -1 $OUT/bench_train_${x%%:*}_mv.log | cut -c1-300; echo; [ $rc -eq 0 ] || { echo "train ${x%%:*} rc=$rc"; exit $rc; }
+  done
 fi
 exit 0

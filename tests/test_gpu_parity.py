@@ -644,6 +644,33 @@ def test_errors_are_loud():
         ops.sample_fine(torch.zeros(2, 300, device=DEV), torch.zeros(2, 300, device=DEV), 0.8, 1.8, 8, 0, 0.0)
 
 
+def test_fp32_kernel_rejects_x3_only_blob(golden):
+    """an AVR_FIELD_X3 blob has no fp32 lin_in / fc_0 / fc_1 fragments; the fp32 field entry points
+    refuse it instead of multiplying uninitialised memory, and accept the same net packed for AVR_FIELD_FP32."""
+    import ctypes
+    from avr import _lib
+    from avr.field import FusedField
+    g = golden("g4_field_small.npz")
+    net = build_net(g, DEV, "x3")
+    f = FusedField(net, "x3")
+    entry = f.packed(True)
+    xyz, vd = T(g["xyz"]), T(g["viewdirs"])
+    p, v = xyz[0].contiguous(), vd.reshape(xyz.shape)[0].contiguous()
+    out = torch.empty(p.shape[0], 4, device=DEV)
+    table = f.table(True)
+    dims = _lib.FieldDims.from_buffer_copy(entry.dims)
+    dims.precision = _lib.FIELD_FP32
+    with pytest.raises(_lib.AVRError, match="packed for AVR_FIELD_X3"):
+        _lib.call("avr_field_fwd_points", ctypes.byref(dims), ctypes.byref(f.view(0)), _lib.ptr(entry.packed),
+                  _lib.ptr(table), _lib.ptr(p), _lib.ptr(v), p.shape[0], _lib.ptr(out), _lib.stream_of(p))
+    f32 = FusedField(net, "fp32")
+    e32 = f32.packed(True)
+    _lib.call("avr_field_fwd_points", ctypes.byref(e32.dims), ctypes.byref(f32.view(0)), _lib.ptr(e32.packed),
+              _lib.ptr(f32.table(True)), _lib.ptr(p), _lib.ptr(v), p.shape[0], _lib.ptr(out), _lib.stream_of(p))
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(out).all())
+
+
 def test_field_x3_tracks_fp32_at_scale(golden):
     """Split-fp16 field vs fp32 field on 200k random samples of the 512-wide net:
     the difference stays at fp32-accumulation level."""
