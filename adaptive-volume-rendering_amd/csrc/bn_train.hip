@@ -290,17 +290,32 @@ static int dispatch_bn_layer(int H, const BnArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ finalize
-__global__ void __launch_bounds__(64) bn_stats_kernel(const double* __restrict__ fold, int nfold, int64_t M, int N,
-                                                      const float* __restrict__ gamma, float eps, float momentum,
-                                                      float* running_mean, float* running_var, float* mu_out,
-                                                      float* invstd_out, float* scale_out) {
-  const int c = blockIdx.x * 64 + threadIdx.x;
-  if (c >= N) return;
-  double a = 0.0, b = 0.0;
-  for (int f = 0; f < nfold; ++f) {
-    a += fold[(int64_t)f * 2 * N + c];
-    b += fold[(int64_t)f * 2 * N + N + c];
-  }
+// Stage 2: block = 4 waves over 64 columns, wave q folds rows q, q + 4, ... of the stage-1 sums, LDS meets them.
+__device__ __forceinline__ void fold_rows(const double* __restrict__ fold, int nfold, int N, int c, double& a,
+                                          double& b) {
+  __shared__ double sa[256], sb[256];
+  const int q = threadIdx.x >> 6;
+  a = 0.0; b = 0.0;
+  if (c < N)
+    for (int f = q; f < nfold; f += 4) {
+      a += fold[(int64_t)f * 2 * N + c];
+      b += fold[(int64_t)f * 2 * N + N + c];
+    }
+  sa[threadIdx.x] = a;
+  sb[threadIdx.x] = b;
+  __syncthreads();
+  a = ((sa[threadIdx.x & 63] + sa[64 + (threadIdx.x & 63)]) + sa[128 + (threadIdx.x & 63)]) + sa[192 + (threadIdx.x & 63)];
+  b = ((sb[threadIdx.x & 63] + sb[64 + (threadIdx.x & 63)]) + sb[128 + (threadIdx.x & 63)]) + sb[192 + (threadIdx.x & 63)];
+}
+
+__global__ void __launch_bounds__(256) bn_stats_kernel(const double* __restrict__ fold, int nfold, int64_t M, int N,
+                                                       const float* __restrict__ gamma, float eps, float momentum,
+                                                       float* running_mean, float* running_var, float* mu_out,
+                                                       float* invstd_out, float* scale_out) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double a, b;
+  fold_rows(fold, nfold, N, c, a, b);
+  if (threadIdx.x >= 64 || c >= N) return;
   const double n = (double)M, mean = a / n;
   const double m2 = fmax(b - n * mean * mean, 0.0);
   const double var = m2 / n;                                    // biased: the normalisation (torch)
@@ -315,17 +330,14 @@ __global__ void __launch_bounds__(64) bn_stats_kernel(const double* __restrict__
   }
 }
 
-__global__ void __launch_bounds__(64) bn_grad_stats_kernel(const double* __restrict__ fold, int nfold, int64_t M,
-                                                           int N, const float* __restrict__ gamma,
-                                                           const float* __restrict__ invstd, float* coef, float* m1,
-                                                           float* m2, float* dgamma, float* dbeta) {
-  const int c = blockIdx.x * 64 + threadIdx.x;
-  if (c >= N) return;
-  double a = 0.0, b = 0.0;
-  for (int f = 0; f < nfold; ++f) {
-    a += fold[(int64_t)f * 2 * N + c];
-    b += fold[(int64_t)f * 2 * N + N + c];
-  }
+__global__ void __launch_bounds__(256) bn_grad_stats_kernel(const double* __restrict__ fold, int nfold, int64_t M,
+                                                            int N, const float* __restrict__ gamma,
+                                                            const float* __restrict__ invstd, float* coef, float* m1,
+                                                            float* m2, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double a, b;
+  fold_rows(fold, nfold, N, c, a, b);
+  if (threadIdx.x >= 64 || c >= N) return;
   m1[c] = (float)(a / (double)M);
   m2[c] = (float)(b / (double)M);
   coef[c] = gamma[c] * invstd[c];
@@ -376,6 +388,7 @@ __global__ void __launch_bounds__(64) bn_fold_kernel(const float* __restrict__ p
   const int64_t nwg = (M + kX3Samples - 1) / kX3Samples;
   double a = 0.0, b = 0.0;
   if (c < N) {
+#pragma unroll 8
     for (int64_t w = (int64_t)blockIdx.y * kBnFold; w < nwg && w < (int64_t)(blockIdx.y + 1) * kBnFold; ++w) {
       const float p0 = part[w * 2 * N + c], p1 = part[w * 2 * N + N + c];
       if constexpr (FWD) {
@@ -494,7 +507,7 @@ extern "C" int avr_bn_stats(const float* partial, int64_t n_rows, int n_cols, co
   bn_fold(partial, n_rows, n_cols, true, &fold, s);
   int rc = check_launch("bn_fold_kernel");
   if (rc) return rc;
-  bn_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 64, 0, s>>>(fold, (int)bn_n_fold(n_rows), n_rows, n_cols, gamma,
+  bn_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 256, 0, s>>>(fold, (int)bn_n_fold(n_rows), n_rows, n_cols, gamma,
                                                                  eps, momentum, running_mean, running_var, mu, invstd,
                                                                  scale);
   return check_launch("bn_stats_kernel");
@@ -510,7 +523,7 @@ extern "C" int avr_bn_grad_stats(const float* partial, int64_t n_rows, int n_col
   bn_fold(partial, n_rows, n_cols, false, &fold, s);
   int rc = check_launch("bn_fold_kernel");
   if (rc) return rc;
-  bn_grad_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 64, 0, s>>>(fold, (int)bn_n_fold(n_rows), n_rows, n_cols,
+  bn_grad_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 256, 0, s>>>(fold, (int)bn_n_fold(n_rows), n_rows, n_cols,
                                                                       gamma, invstd, coef, m1, m2, dgamma, dbeta);
   return check_launch("bn_grad_stats_kernel");
 }

@@ -106,6 +106,28 @@ def test_model_state_dict_keys_match_reference_layout():
     assert not fused_eligible(mv, multiview=True)
 
 
+def test_bn_training_route_eligibility():
+    """train.py --bn nets in training mode take the layer-by-layer HIP path (avr.bn_train), in eval mode the
+    fused kernel (running statistics folded); nets without BatchNorm neither."""
+    from avr.bn_train import bn_train_eligible
+    from avr.conf import default_conf
+    from avr.field import fused_eligible
+    from avr.models import NewPixelNeRFNet
+    net = NewPixelNeRFNet(default_conf(multiview=True)["model"], bn=True)
+    net.encoder.set_latent(torch.zeros(1, 512, 4, 4))
+    assert bn_train_eligible(net.train()) and not fused_eligible(net)
+    assert not bn_train_eligible(net.eval()) and fused_eligible(net)
+    plain = NewPixelNeRFNet(default_conf()["model"])
+    plain.encoder.set_latent(torch.zeros(1, 512, 4, 4))
+    assert not bn_train_eligible(plain.train())
+    net.train()
+    for m in (net.mlp_coarse, net.mlp_fine):   # Softplus with BatchNorm: module path
+        for blk in m.blocks:
+            blk.activation = torch.nn.Softplus(beta=2.0)
+        m.activation = torch.nn.Softplus(beta=2.0)
+    assert not bn_train_eligible(net)
+
+
 def test_graft_entry_build():
     """__graft_entry__.build(): make (no-op when built) + load + ABI check."""
     import importlib
