@@ -67,7 +67,8 @@ class _Stats:
         self.mu, self.invstd, self.scale = buf[0], buf[1], buf[2]
 
 
-def _layer(dims, **kw):
+def _layer(**kw):
+    """An avr_bn_layer from keyword fields (tensors become their device addresses)."""
     l = BnLayer()
     for k, v in kw.items():
         setattr(l, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
@@ -92,10 +93,10 @@ def _momentum(bn):
     return float(bn.momentum)
 
 
-def _bn_stats(bn, part, M, H, stats, stream, update_running):
-    """avr_bn_stats for one application of `bn` (the running statistics updated as torch's batch_norm does:
-    num_batches_tracked += 1, momentum, unbiased variance)."""
-    track = update_running and bn.track_running_stats and bn.running_mean is not None
+def _bn_stats(bn, part, M, H, stats, stream):
+    """avr_bn_stats for one training-mode application of `bn` (the running statistics updated as torch's
+    batch_norm does: num_batches_tracked += 1, momentum, unbiased variance)."""
+    track = bn.track_running_stats and bn.running_mean is not None
     if track:
         bn.num_batches_tracked.add_(1)
     call("avr_bn_stats", ptr(part), M, H, ptr(bn.weight), ctypes.c_float(bn.eps),
@@ -103,7 +104,7 @@ def _bn_stats(bn, part, M, H, stats, stream, update_running):
          ptr(bn.running_var) if track else None, ptr(stats.mu), ptr(stats.invstd), ptr(stats.scale), stream)
 
 
-def table_rows(fused, coarse, tables, xyz, b, out):
+def table_rows(fused, tables, xyz, b, out):
     """Rows (SB * B, d_hidden) of lin_z[b](latent features) at the points: the bilinear blend of the per-texel
     table b (tables (SB, n_tables, H*W, d_hidden), the x3 training tables) -- avr_latent_features per scene."""
     SB, B, _ = xyz.shape
@@ -151,7 +152,6 @@ class _FieldTrainBN(torch.autograd.Function):
         if M < 2:
             raise ValueError("Expected more than 1 value per channel when training (BatchNorm, "
                              f"got {M} rows)")
-        update = True     # training mode: batch statistics, and the running statistics updated (torch)
         with torch.no_grad():
             # lin_in's input: z_feature rows padded to 16 B (the fused kernels' zf layout)
             zf = net.z_features(xyz.detach(), viewdirs.detach()).to(F32)
@@ -162,7 +162,7 @@ class _FieldTrainBN(torch.autograd.Function):
             tables = fused.tables_batch(coarse, SB, fast=True, bn_fold=False)
             Tz = torch.empty(max(nz, 1), M, H, device=dev, dtype=F32)
             for b in range(nz):
-                table_rows(fused, coarse, tables, xyz, b, Tz[b])
+                table_rows(fused, tables, xyz, b, Tz[b])
             # biases with the lin_z biases folded where the tables (no bias) are added
             lz_b = [P[f"lin_z.{b}.bias"].detach() for b in range(nz)]
             b_in = P["lin_in.bias"].detach() + (lz_b[0] if nz > 0 else 0)
@@ -179,18 +179,18 @@ class _FieldTrainBN(torch.autograd.Function):
             st2 = [_Stats(H, dev) for _ in range(nb)]
             bns = _bn_blocks(mlp)
             blob = entry.packed
-            _run(dims, _layer(dims, n_rows=M, mode=_lib.BN_FWD, prologue=_lib.BN_PLAIN, in_dim=64, in_valid=d_in,
+            _run(dims, _layer(n_rows=M, mode=_lib.BN_FWD, prologue=_lib.BN_PLAIN, in_dim=64, in_valid=d_in,
                               src=zfp, ld_src=zs, blob=blob, layer=0, bias=b_in, add1=Tz[0] if nz > 0 else None,
                               out=X[0], partial=part), stream)
             for b in range(nb):
                 bn = bns[b]
-                _bn_stats(bn, part, M, H, st1[b], stream, update)
-                _run(dims, _layer(dims, n_rows=M, mode=_lib.BN_FWD, prologue=_lib.BN_RELU, in_dim=H, in_valid=H,
+                _bn_stats(bn, part, M, H, st1[b], stream)
+                _run(dims, _layer(n_rows=M, mode=_lib.BN_FWD, prologue=_lib.BN_RELU, in_dim=H, in_valid=H,
                                   src=X[b], ld_src=H, in_mu=st1[b].mu, in_scale=st1[b].scale, in_shift=betas[b],
                                   operand_out=A[2 * b], operand_max=amax[2 * b:], blob=blob, layer=2 + 2 * b,
                                   bias=b0[b], out=N[b], partial=part), stream)
-                _bn_stats(bn, part, M, H, st2[b], stream, update)
-                _run(dims, _layer(dims, n_rows=M, mode=_lib.BN_FWD, prologue=_lib.BN_RELU, in_dim=H, in_valid=H,
+                _bn_stats(bn, part, M, H, st2[b], stream)
+                _run(dims, _layer(n_rows=M, mode=_lib.BN_FWD, prologue=_lib.BN_RELU, in_dim=H, in_valid=H,
                                   src=N[b], ld_src=H, in_mu=st2[b].mu, in_scale=st2[b].scale, in_shift=betas[b],
                                   operand_out=A[2 * b + 1], operand_max=amax[2 * b + 1:], blob=blob,
                                   layer=3 + 2 * b, bias=b1[b], add1=X[b], add2=Tz[b + 1] if b + 1 < nz else None,
@@ -251,13 +251,13 @@ class _FieldTrainBN(torch.autograd.Function):
                     pro = dict(prologue=_lib.BN_GRAD, src=gp1[b + 1], ld_src=H, src_pre=X[b + 1], src_res=Gx[b + 2],
                                in_mu=st1[b + 1].mu, in_invstd=st1[b + 1].invstd, in_scale=c[0], in_m1=c[1],
                                in_m2=c[2], operand_out=Gx[b + 1], operand_max=gmax[b + 1:])
-                _run(dims, _layer(dims, n_rows=M, mode=_lib.BN_BWD, in_dim=H, in_valid=H, blob=bwd, layer=3 + 2 * b,
+                _run(dims, _layer(n_rows=M, mode=_lib.BN_BWD, in_dim=H, in_valid=H, blob=bwd, layer=3 + 2 * b,
                                   out=gp2, mask_rows=A[2 * b + 1], pre_rows=N[b], out_mu=st2[b].mu,
                                   out_invstd=st2[b].invstd, partial=part, **pro), stream)
                 call("avr_bn_grad_stats", ptr(part), M, H, ptr(gammas[b]), ptr(st2[b].invstd), ptr(gs2[0]),
                      ptr(gs2[1]), ptr(gs2[2]), ptr(dgam[b]), ptr(dbet[b]), stream)
                 # fc_0[b]^T: operand = d loss / d fc_0 output = BN backward of gp2 (stored as DN[b])
-                _run(dims, _layer(dims, n_rows=M, mode=_lib.BN_BWD, prologue=_lib.BN_GRAD, in_dim=H, in_valid=H,
+                _run(dims, _layer(n_rows=M, mode=_lib.BN_BWD, prologue=_lib.BN_GRAD, in_dim=H, in_valid=H,
                                   src=gp2, ld_src=H, src_pre=N[b], in_mu=st2[b].mu, in_invstd=st2[b].invstd,
                                   in_scale=gs2[0], in_m1=gs2[1], in_m2=gs2[2], operand_out=DN[b],
                                   operand_max=dn_max[b:], blob=bwd, layer=2 + 2 * b, out=gp1[b], mask_rows=A[2 * b],
