@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -55,7 +55,8 @@ AVR_WGRAD_MAX_LAYERS = 16
 class WGradLayer(ctypes.Structure):
     _fields_ = [("grad", c_void_p), ("ld_grad", i64), ("input", c_void_p), ("ld_input", i64),
                 ("out_dim", c_int), ("in_dim", c_int), ("grad_max", c_void_p), ("input_max", c_void_p),
-                ("partial", c_void_p), ("bias_partial", c_void_p)]
+                ("partial", c_void_p), ("bias_partial", c_void_p),
+                ("in_mu", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p)]
 
 
 BN_FWD, BN_BWD = 0, 1
@@ -63,7 +64,7 @@ BN_PLAIN, BN_RELU, BN_GRAD = 0, 1, 2
 
 
 class BnLayer(ctypes.Structure):
-    """avr_bn_layer (ABI 11): one layer GEMM of the training-mode BatchNorm path (see include/avr.h)."""
+    """avr_bn_layer (ABI 12): one layer GEMM of the training-mode BatchNorm path (see include/avr.h)."""
     _fields_ = [("n_rows", i64), ("mode", c_int), ("prologue", c_int), ("in_dim", c_int), ("in_valid", c_int),
                 ("src", c_void_p), ("ld_src", i64), ("src_pre", c_void_p), ("src_res", c_void_p),
                 ("in_mu", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p),
@@ -71,8 +72,11 @@ class BnLayer(ctypes.Structure):
                 ("operand_out", c_void_p), ("operand_max", c_void_p),
                 ("blob", c_void_p), ("layer", c_int),
                 ("bias", c_void_p), ("add1", c_void_p), ("add2", c_void_p), ("out", c_void_p),
-                ("mask_rows", c_void_p), ("pre_rows", c_void_p), ("out_mu", c_void_p), ("out_invstd", c_void_p),
-                ("partial", c_void_p)]
+                ("pre_rows", c_void_p), ("out_mu", c_void_p), ("out_invstd", c_void_p), ("out_scale", c_void_p),
+                ("out_shift", c_void_p),
+                ("partial", c_void_p),
+                ("lin_z_table", c_void_p), ("lin_z_scene_stride", i64), ("xyz", c_void_p), ("views", c_void_p),
+                ("n_views", c_int), ("rows_per_scene", i64)]
 
 
 # name -> argtypes (all return int status)

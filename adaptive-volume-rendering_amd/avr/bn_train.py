@@ -10,7 +10,8 @@ the epilogue; avr_bn_stats between launches turns them into the batch mean / inv
 updates the running statistics as torch does. The backward runs the same GEMMs on the transposed weights,
 with torch's batch_norm backward, (g - mean g - xhat mean(g xhat)) * gamma * invstd, built into the next
 GEMM's prologue (avr_bn_grad_stats reduces the two means, dgamma and dbeta); the weight gradients are the
-existing split-K x3 kernel (avr_weight_grads).
+existing split-K x3 kernel (avr_weight_grads). The relu'd operands relu(bn_0(.)) are never stored: the
+backward's relu masks and the weight gradients' staging rebuild them from the pre-BN rows (ABI 12).
 
 The thin ends stay in torch: the z_feature input (positional encoding, models.py:763-789), lin_out's 4
 outputs with sigmoid / relu, and the input gradients (grid_sample adjoint), as in avr.field._FieldTrain.
@@ -20,7 +21,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import BnLayer, call, ptr, stream_of
+from ._lib import BnLayer, ViewDesc, call, ptr, stream_of
 
 F32 = torch.float32
 
@@ -104,18 +105,6 @@ def _bn_stats(bn, part, M, H, stats, stream):
          ptr(bn.running_var) if track else None, ptr(stats.mu), ptr(stats.invstd), ptr(stats.scale), stream)
 
 
-def table_rows(fused, tables, xyz, b, out):
-    """Rows (SB * B, d_hidden) of lin_z[b](latent features) at the points: the bilinear blend of the per-texel
-    table b (tables (SB, n_tables, H*W, d_hidden), the x3 training tables) -- avr_latent_features per scene."""
-    SB, B, _ = xyz.shape
-    H = tables.shape[-1]
-    p = xyz.detach().to(F32).contiguous()
-    for s in range(SB):
-        call("avr_latent_features", ctypes.byref(fused.view(s)), ptr(tables[s, b]), H, ptr(p[s]), B,
-             ptr(out[s * B:(s + 1) * B]), stream_of(out))
-    return out
-
-
 def train_param_names_bn(mlp):
     from .field import train_param_names
     names = train_param_names(mlp)
@@ -159,10 +148,12 @@ class _FieldTrainBN(torch.autograd.Function):
             zs = d_in + (-d_in) % 4
             zfp = torch.zeros(M, zs, device=dev, dtype=F32)
             zfp[:, :d_in] = zf
+            # lin_z[b](latent features) rows: gathered from the per-texel tables in the layer epilogues
             tables = fused.tables_batch(coarse, SB, fast=True, bn_fold=False)
-            Tz = torch.empty(max(nz, 1), M, H, device=dev, dtype=F32)
-            for b in range(nz):
-                table_rows(fused, tables, xyz, b, Tz[b])
+            views = (ViewDesc * SB)(*[fused.view(s) for s in range(SB)])
+            p = xyz.detach().to(F32).contiguous()
+            lin_z = lambda b: dict(lin_z_table=tables[0, b], lin_z_scene_stride=tables.stride(0), xyz=p,  # noqa: E731
+                                   views=ctypes.addressof(views), n_views=SB, rows_per_scene=B) if b < nz else {}
             # biases with the lin_z biases folded where the tables (no bias) are added
             lz_b = [P[f"lin_z.{b}.bias"].detach() for b in range(nz)]
             b_in = P["lin_in.bias"].detach() + (lz_b[0] if nz > 0 else 0)
@@ -172,7 +163,8 @@ class _FieldTrainBN(torch.autograd.Function):
             betas = [P[f"blocks.{b}.bn_0.bias"].detach().to(F32).contiguous() for b in range(nb)]
             X = torch.empty(nb + 1, M, H, device=dev, dtype=F32)        # block inputs (pre-BN) + the last output
             N = torch.empty(max(nb, 1), M, H, device=dev, dtype=F32)    # fc_0 outputs (pre-BN)
-            A = torch.empty(2 * nb, M, H, device=dev, dtype=F32)        # GEMM inputs (after BN + relu)
+            # max |relu(bn_0(.))| of each hidden GEMM's operand (the operands themselves are not stored: the
+            # backward's relu masks and the weight gradients rebuild them from X / N and the statistics)
             amax = torch.zeros(2 * nb + 2, device=dev, dtype=torch.int32)
             part = _partial(M, H, dev)
             st1 = [_Stats(H, dev) for _ in range(nb)]
@@ -180,27 +172,27 @@ class _FieldTrainBN(torch.autograd.Function):
             bns = _bn_blocks(mlp)
             blob = entry.packed
             _run(dims, _layer(n_rows=M, mode=_lib.BN_FWD, prologue=_lib.BN_PLAIN, in_dim=64, in_valid=d_in,
-                              src=zfp, ld_src=zs, blob=blob, layer=0, bias=b_in, add1=Tz[0] if nz > 0 else None,
-                              out=X[0], partial=part), stream)
+                              src=zfp, ld_src=zs, blob=blob, layer=0, bias=b_in, out=X[0], partial=part,
+                              **lin_z(0)), stream)
             for b in range(nb):
                 bn = bns[b]
                 _bn_stats(bn, part, M, H, st1[b], stream)
                 _run(dims, _layer(n_rows=M, mode=_lib.BN_FWD, prologue=_lib.BN_RELU, in_dim=H, in_valid=H,
                                   src=X[b], ld_src=H, in_mu=st1[b].mu, in_scale=st1[b].scale, in_shift=betas[b],
-                                  operand_out=A[2 * b], operand_max=amax[2 * b:], blob=blob, layer=2 + 2 * b,
+                                  operand_max=amax[2 * b:], blob=blob, layer=2 + 2 * b,
                                   bias=b0[b], out=N[b], partial=part), stream)
                 _bn_stats(bn, part, M, H, st2[b], stream)
                 _run(dims, _layer(n_rows=M, mode=_lib.BN_FWD, prologue=_lib.BN_RELU, in_dim=H, in_valid=H,
                                   src=N[b], ld_src=H, in_mu=st2[b].mu, in_scale=st2[b].scale, in_shift=betas[b],
-                                  operand_out=A[2 * b + 1], operand_max=amax[2 * b + 1:], blob=blob,
-                                  layer=3 + 2 * b, bias=b1[b], add1=X[b], add2=Tz[b + 1] if b + 1 < nz else None,
-                                  out=X[b + 1], partial=part), stream)
+                                  operand_max=amax[2 * b + 1:], blob=blob,
+                                  layer=3 + 2 * b, bias=b1[b], add1=X[b], out=X[b + 1], partial=part,
+                                  **lin_z(b + 1)), stream)
             # lin_out on relu(x) (4 outputs; models.py:592), sigmoid rgb / relu sigma (models.py:856-862)
             a_out = torch.relu(X[nb])
             raw = torch.addmm(P["lin_out.bias"].detach().to(F32), a_out, P["lin_out.weight"].detach().to(F32).t())
             out = torch.cat([torch.sigmoid(raw[:, :3]), torch.relu(raw[:, 3:4])], -1).reshape(SB, B, 4)
         ctx.fused, ctx.coarse, ctx.names, ctx.entry = fused, coarse, names, entry
-        ctx.keep = (X, N, A, amax, a_out, zfp, st1, st2, betas)
+        ctx.keep = (X, N, amax, a_out, zfp, st1, st2, betas)
         ctx.save_for_backward(xyz, viewdirs, latent, out, *params)
         return out
 
@@ -209,7 +201,7 @@ class _FieldTrainBN(torch.autograd.Function):
         from .ops import _max_bits, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         fused, entry, names = ctx.fused, ctx.entry, ctx.names
-        X, N, A, amax, a_out, zfp, st1, st2, betas = ctx.keep
+        X, N, amax, a_out, zfp, st1, st2, betas = ctx.keep
         ctx.keep = None
         net = fused.net
         P = dict(zip(names, params))
@@ -252,16 +244,17 @@ class _FieldTrainBN(torch.autograd.Function):
                                in_mu=st1[b + 1].mu, in_invstd=st1[b + 1].invstd, in_scale=c[0], in_m1=c[1],
                                in_m2=c[2], operand_out=Gx[b + 1], operand_max=gmax[b + 1:])
                 _run(dims, _layer(n_rows=M, mode=_lib.BN_BWD, in_dim=H, in_valid=H, blob=bwd, layer=3 + 2 * b,
-                                  out=gp2, mask_rows=A[2 * b + 1], pre_rows=N[b], out_mu=st2[b].mu,
-                                  out_invstd=st2[b].invstd, partial=part, **pro), stream)
+                                  out=gp2, pre_rows=N[b], out_mu=st2[b].mu, out_invstd=st2[b].invstd,
+                                  out_scale=st2[b].scale, out_shift=betas[b], partial=part, **pro), stream)
                 call("avr_bn_grad_stats", ptr(part), M, H, ptr(gammas[b]), ptr(st2[b].invstd), ptr(gs2[0]),
                      ptr(gs2[1]), ptr(gs2[2]), ptr(dgam[b]), ptr(dbet[b]), stream)
                 # fc_0[b]^T: operand = d loss / d fc_0 output = BN backward of gp2 (stored as DN[b])
                 _run(dims, _layer(n_rows=M, mode=_lib.BN_BWD, prologue=_lib.BN_GRAD, in_dim=H, in_valid=H,
                                   src=gp2, ld_src=H, src_pre=N[b], in_mu=st2[b].mu, in_invstd=st2[b].invstd,
                                   in_scale=gs2[0], in_m1=gs2[1], in_m2=gs2[2], operand_out=DN[b],
-                                  operand_max=dn_max[b:], blob=bwd, layer=2 + 2 * b, out=gp1[b], mask_rows=A[2 * b],
-                                  pre_rows=X[b], out_mu=st1[b].mu, out_invstd=st1[b].invstd, partial=part), stream)
+                                  operand_max=dn_max[b:], blob=bwd, layer=2 + 2 * b, out=gp1[b], pre_rows=X[b],
+                                  out_mu=st1[b].mu, out_invstd=st1[b].invstd, out_scale=st1[b].scale,
+                                  out_shift=betas[b], partial=part), stream)
                 c = gs1[b]
                 call("avr_bn_grad_stats", ptr(part), M, H, ptr(gammas[b]), ptr(st1[b].invstd), ptr(c[0]), ptr(c[1]),
                      ptr(c[2]), ptr(dgam[b]), ptr(dbet[b]), stream)
@@ -269,7 +262,8 @@ class _FieldTrainBN(torch.autograd.Function):
                 c = gs1[0]
                 call("avr_bn_grad_rows", M, H, ptr(gp1[0]), ptr(X[0]), ptr(Gx[1]), ptr(c[0]), ptr(c[1]), ptr(c[2]),
                      ptr(st1[0].mu), ptr(st1[0].invstd), ptr(Gx[0]), ptr(gmax[0:1]), stream)
-            # weight gradients: fc_0 (DN, A[2b]), fc_1 (Gx[b+1], A[2b+1]), lin_z (Gx[b], latent features),
+            # weight gradients: fc_0 (DN, relu(bn_0(X[b]))), fc_1 (Gx[b+1], relu(bn_0(N[b]))) -- both operands
+            # rebuilt from the pre-BN rows in the kernel's staging --, lin_z (Gx[b], latent features),
             # lin_in (Gx[0], z_feature), lin_out (d4, relu(X[nb]))
             lat_feat = torch.empty(M, net.d_latent, device=dev, dtype=F32)
             if nz > 0:
@@ -283,8 +277,10 @@ class _FieldTrainBN(torch.autograd.Function):
             lat_max = fused.latent_max_bits(latent)
             layers = []
             for b in range(nb):
-                layers.append((DN[b], A[2 * b], dn_max[b:b + 1], amax[2 * b:2 * b + 1], True))
-                layers.append((Gx[b + 1], A[2 * b + 1], gmax[b + 1:b + 2], amax[2 * b + 1:2 * b + 2], True))
+                layers.append((DN[b], X[b], dn_max[b:b + 1], amax[2 * b:2 * b + 1], True,
+                               (st1[b].mu, st1[b].scale, betas[b])))
+                layers.append((Gx[b + 1], N[b], gmax[b + 1:b + 2], amax[2 * b + 1:2 * b + 2], True,
+                               (st2[b].mu, st2[b].scale, betas[b])))
             for b in range(nz):
                 layers.append((Gx[b], lat_feat, gmax[b:b + 1], lat_max, True))
             zf_max = _max_bits(zfp)

@@ -384,17 +384,19 @@ def _wgrad_splits(tiles, n_rows, dev):
 
 
 def weight_grads(layers, n_rows, n_split=None):
-    """dW = G^T X and db = colsum(G) for each (grad, input, grad_max, input_max, want_bias)
+    """dW = G^T X and db = colsum(G) for each (grad, input, grad_max, input_max, want_bias[, bn])
     of `layers` (avr_weight_grads: split-K x3 MFMA). grad (n_rows, out) / input
     (n_rows, in) fp32 row-major (row strides may exceed the widths); *_max: int32
-    (1,) float bits of max |.|. Returns [(dW (out, in), db (out,) or None)]."""
+    (1,) float bits of max |.|; bn = (mu, scale, shift) (in,) each: X = relu((input - mu) * scale + shift)
+    per column, a training-mode BatchNorm's operand rebuilt from its pre-BN rows (input_max then of X).
+    Returns [(dW (out, in), db (out,) or None)]."""
     if not layers:
         return []
     dev = layers[0][0].device
     if n_rows == 0:
-        return [(torch.zeros(g.shape[1], x.shape[1], device=dev), torch.zeros(g.shape[1], device=dev) if wb else None)
-                for g, x, _, _, wb in layers]
-    tiles = sum(-(-g.shape[1] // _DW_TILE) * -(-x.shape[1] // _DW_TILE) for g, x, *_ in layers)
+        return [(torch.zeros(l[0].shape[1], l[1].shape[1], device=dev), torch.zeros(l[0].shape[1], device=dev) if l[4] else None)
+                for l in layers]
+    tiles = sum(-(-l[0].shape[1] // _DW_TILE) * -(-l[1].shape[1] // _DW_TILE) for l in layers)
     if n_split is None:
         n_split = _wgrad_splits(tiles, n_rows, dev)
     out = []
@@ -403,20 +405,25 @@ def weight_grads(layers, n_rows, n_split=None):
         chunk = layers[base:base + _lib.AVR_WGRAD_MAX_LAYERS]
         arr = (_lib.WGradLayer * len(chunk))()
         # the partials of the whole chunk in one buffer (every piece a multiple of 16 B: O, I multiples of 4)
-        sizes = [n_split * g.shape[1] * (x.shape[1] + (1 if wb else 0)) for g, x, _, _, wb in chunk]
+        sizes = [n_split * l[0].shape[1] * (l[1].shape[1] + (1 if l[4] else 0)) for l in chunk]
         flat = torch.empty(sum(sizes), device=dev, dtype=torch.float32)
         dw_ptrs, db_ptrs = (ctypes.c_void_p * len(chunk))(), (ctypes.c_void_p * len(chunk))()
         res, off = [], 0
-        for k, (g, x, gmax, xmax, want_bias) in enumerate(chunk):
+        for k, (g, x, gmax, xmax, want_bias, *bn) in enumerate(chunk):
             O, I = g.shape[1], x.shape[1]
+            bn = bn[0] if bn else None
             for t in (g, x):
                 if t.dtype != torch.float32 or t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
                     raise _lib.AVRError("weight_grads: operands must be fp32 rows, 16-B aligned, unit column stride")
+            if bn is not None and any(t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != I
+                                      or t.data_ptr() % 16 for t in bn):
+                raise _lib.AVRError("weight_grads: the BatchNorm transform takes (in,) fp32 mu / scale / shift")
             part = flat[off:off + n_split * O * I]
             bpart = flat[off + n_split * O * I:off + sizes[k]] if want_bias else None
             off += sizes[k]
             arr[k] = _lib.WGradLayer(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), O, I, gmax.data_ptr(),
-                                     xmax.data_ptr(), part.data_ptr(), 0 if bpart is None else bpart.data_ptr())
+                                     xmax.data_ptr(), part.data_ptr(), 0 if bpart is None else bpart.data_ptr(),
+                                     *([t.data_ptr() for t in bn] if bn is not None else [None] * 3))
             dw = torch.empty(O, I, device=dev, dtype=torch.float32)
             db = torch.empty(O, device=dev, dtype=torch.float32) if want_bias else None
             dw_ptrs[k], db_ptrs[k] = dw.data_ptr(), (db.data_ptr() if want_bias else None)

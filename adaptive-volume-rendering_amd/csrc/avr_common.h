@@ -9,6 +9,15 @@ namespace avr {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// relu(bn_0(x)) of a training-mode BatchNorm (models.py:456-461) per column: relu((x - mu) * scale + shift),
+// scale = gamma * invstd, shift = beta, one explicit fma per value. The BN layers' prologue, their backward's
+// relu mask and the weight-gradient staging each recompute it from the pre-BN rows and must agree bit for bit.
+__device__ __forceinline__ floatx4 bn_relu4(floatx4 x, floatx4 mu, floatx4 scale, floatx4 shift) {
+  const floatx4 d = x - mu;
+  return floatx4{fmaxf(__builtin_fmaf(d.x, scale.x, shift.x), 0.f), fmaxf(__builtin_fmaf(d.y, scale.y, shift.y), 0.f),
+                 fmaxf(__builtin_fmaf(d.z, scale.z, shift.z), 0.f), fmaxf(__builtin_fmaf(d.w, scale.w, shift.w), 0.f)};
+}
+
 // ------------------------------------------------------------------ errors
 void set_error(const char* fmt, ...);
 int fail(int code, const char* fmt, ...);

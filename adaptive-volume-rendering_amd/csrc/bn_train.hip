@@ -10,7 +10,8 @@
 // fp16 hi/lo under one power-of-two scale per workgroup and staged in LDS in the fused kernels' B-fragment
 // order; the K loop is theirs (x3: three v_mfma_f32_16x16x32_f16 per product, fp32 accumulate, weights
 // streamed one chunk ahead); the epilogue adds bias / residual / lin_z rows (forward) or applies the relu mask
-// (backward), stores the rows and reduces this workgroup's column statistics. A finalize launch between
+// (backward, recomputed from the pre-BN rows: the relu'd operands are never stored), stores the rows and
+// reduces this workgroup's column statistics. A finalize launch between
 // layers (bn_stats_kernel / bn_grad_stats_kernel) combines the workgroups' partials in fp64.
 #include "x3_gemm.h"
 
@@ -29,8 +30,13 @@ struct BnArgs {
   int KC;
   const float* bias; const float* add1; const float* add2;
   float* out;
-  const float* mask_rows; const float* pre_rows; const float* out_mu; const float* out_invstd;
+  const float* pre_rows; const float* out_mu; const float* out_invstd; const float* out_scale; const float* out_shift;
   float* part;
+  // forward: the lin_z rows gathered in the epilogue (row m of scene m / zrows: the bilinear blend of
+  // ztab + scene * ztab_stride at zxyz[m] in zviews[scene]), or ztab = null
+  const float* ztab; int64_t ztab_stride, zrows;
+  const float* zxyz;
+  View zviews[AVR_MAX_SCENES];
 };
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
@@ -105,8 +111,7 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
       }
       if (k < a.kin) {
         if (a.prologue == AVR_BN_RELU) {
-          v = (v - ld4(a.in_mu + k)) * ld4(a.in_scale + k) + ld4(a.in_shift + k);
-          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+          v = bn_relu4(v, ld4(a.in_mu + k), ld4(a.in_scale + k), ld4(a.in_shift + k));
         } else if (a.prologue == AVR_BN_GRAD) {
           const floatx4 xh = (ld4(a.src_pre + row * a.ld_src + k) - ld4(a.in_mu + k)) * ld4(a.in_invstd + k);
           v = (v - ld4(a.in_m1 + k) - xh * ld4(a.in_m2 + k)) * ld4(a.in_scale + k);
@@ -167,17 +172,21 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   }
   __syncthreads();
   floatx4 yv[MAXQ];
+  Bilinear zbl{};                            // forward with ztab: the current row's lin_z corners
+  const float* ztab = a.ztab;
   floatx4 s1[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}}, s2[2] = {s1[0], s1[0]};
-  floatx4 cp0[2], cp1[2];                    // per-column parameters of the lane's two groups
+  floatx4 cp0[2], cp1[2], cp2[2], cp3[2];    // per-column parameters of the lane's two groups
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int f = 4 * (lane + 64 * h) < HID ? 4 * (lane + 64 * h) : 0;
     if constexpr (MODE == AVR_BN_FWD) {
       cp0[h] = a.bias ? ld4(a.bias + f) : floatx4{0.f, 0.f, 0.f, 0.f};
-      cp1[h] = cp0[h];
+      cp1[h] = cp2[h] = cp3[h] = cp0[h];
     } else {
       cp0[h] = ld4(a.out_mu + f);
       cp1[h] = ld4(a.out_invstd + f);
+      cp2[h] = ld4(a.out_scale + f);
+      cp3[h] = ld4(a.out_shift + f);
     }
   }
 #pragma unroll
@@ -193,22 +202,37 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
         v += cp0[i & 1];
         if (a.add1) v += ld4(a.add1 + row * HID + f);
         if (a.add2) v += ld4(a.add2 + row * HID + f);
+        if (a.ztab) {   // the row's lin_z features: avr_latent_features' lookup and blend order, bit for bit
+          if ((i & 1) == 0) {
+            const int64_t sc = row / a.zrows;
+            zbl = bilinear_at(a.zviews[sc], a.zxyz[3 * row], a.zxyz[3 * row + 1], a.zxyz[3 * row + 2]);
+            ztab = a.ztab + sc * a.ztab_stride;
+          }
+          const floatx4 c0 = ld4(ztab + (int64_t)zbl.tex[0] * HID + f), c1 = ld4(ztab + (int64_t)zbl.tex[1] * HID + f);
+          const floatx4 c2 = ld4(ztab + (int64_t)zbl.tex[2] * HID + f), c3 = ld4(ztab + (int64_t)zbl.tex[3] * HID + f);
+          floatx4 z;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            z[t] = fadd(fadd(fadd(fmul(c0[t], zbl.w[0]), fmul(c1[t], zbl.w[1])), fmul(c2[t], zbl.w[2])),
+                        fmul(c3[t], zbl.w[3]));
+          v += z;
+        }
         if (live) {
           *reinterpret_cast<floatx4*>(a.out + row * HID + f) = v;
           s1[i & 1] += v;
           yv[i] = v;
         }
-      } else {
-        const floatx4 z = ld4(a.mask_rows + row * HID + f);
+      } else if (live) {
+        // the relu mask of the forward operand, recomputed from the pre-BN row (bn_relu4, as the forward did)
+        const floatx4 p = ld4(a.pre_rows + row * HID + f);
+        const floatx4 z = bn_relu4(p, cp0[i & 1], cp2[i & 1], cp3[i & 1]);
         floatx4 gp;
         gp.x = z.x > 0.f ? v.x : 0.f; gp.y = z.y > 0.f ? v.y : 0.f;
         gp.z = z.z > 0.f ? v.z : 0.f; gp.w = z.w > 0.f ? v.w : 0.f;
-        if (live) {
-          *reinterpret_cast<floatx4*>(a.out + row * HID + f) = gp;
-          const floatx4 xh = (ld4(a.pre_rows + row * HID + f) - cp0[i & 1]) * cp1[i & 1];
-          s1[i & 1] += gp;
-          s2[i & 1] += gp * xh;
-        }
+        *reinterpret_cast<floatx4*>(a.out + row * HID + f) = gp;
+        const floatx4 xh = (p - cp0[i & 1]) * cp1[i & 1];
+        s1[i & 1] += gp;
+        s2[i & 1] += gp * xh;
       }
     }
   }
@@ -345,8 +369,9 @@ __global__ void __launch_bounds__(256) bn_grad_stats_kernel(const double* __rest
   dgamma[c] += (float)b;
 }
 
-// Grid (column groups of 4 x 64, rows / 4): thread (x, y) handles column group 64 blockIdx.x + (x & 63) of row
-// 4 blockIdx.y + (x >> 6): coalesced 1-KB row segments, the column parameters loaded once per thread.
+// Grid (column groups of 4 x 64, rows / 16): thread (x, y) handles column group 64 blockIdx.x + (x & 63) of rows
+// 16 blockIdx.y + (x >> 6) + 4 k, k < 4: coalesced 1-KB row segments, the column parameters loaded once per
+// thread, and all twelve row loads issued before the first store (out is __restrict__: nothing orders them).
 __global__ void __launch_bounds__(256) bn_grad_rows_kernel(int64_t n_rows, int N4, const floatx4* __restrict__ gr,
                                                            const floatx4* __restrict__ pre,
                                                            const floatx4* __restrict__ res,
@@ -354,20 +379,30 @@ __global__ void __launch_bounds__(256) bn_grad_rows_kernel(int64_t n_rows, int N
                                                            const floatx4* __restrict__ m1,
                                                            const floatx4* __restrict__ m2,
                                                            const floatx4* __restrict__ mu,
-                                                           const floatx4* __restrict__ invstd, floatx4* out,
-                                                           unsigned* out_max) {
+                                                           const floatx4* __restrict__ invstd,
+                                                           floatx4* __restrict__ out, unsigned* out_max) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int64_t r0 = (int64_t)blockIdx.y * 16 + (threadIdx.x >> 6);
   float mx = 0.f;
   if (c < N4) {
     const floatx4 cf = coef[c], a1 = m1[c], a2 = m2[c], u = mu[c], is = invstd[c];
-#pragma unroll 4
-    for (int64_t r = r0; r < n_rows && r < (int64_t)blockIdx.y * 16 + 16; r += 4) {
+    floatx4 g[4], p[4], q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t r = r0 + 4 * k < n_rows ? r0 + 4 * k : n_rows - 1;   // clamped rows are loaded, not stored
       const int64_t i = r * N4 + c;
-      floatx4 v = (gr[i] - a1 - (pre[i] - u) * is * a2) * cf;
-      if (res) v += res[i];
-      out[i] = v;
-      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      g[k] = gr[i];
+      p[k] = pre[i];
+      q[k] = res ? res[i] : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (r0 + 4 * k < n_rows) {
+        floatx4 v = (g[k] - a1 - (p[k] - u) * is * a2) * cf;
+        if (res) v += q[k];
+        out[(r0 + 4 * k) * N4 + c] = v;
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
     }
   }
   mx = wave_max(mx);
@@ -454,15 +489,28 @@ extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* 
     a.w = l->blob + (ly == 0 ? L.x3_in : (ly % 2 == 0 ? L.x3_fc0[(ly - 2) / 2] : L.x3_fc1[(ly - 2) / 2]));
     hdr = reinterpret_cast<const unsigned*>(l->blob + L.x3_hdr);
     a.bias = l->bias; a.add1 = l->add1; a.add2 = l->add2;
+    if (l->lin_z_table) {
+      AVR_REQUIRE(l->xyz && l->views && l->n_views >= 1 && l->n_views <= AVR_MAX_SCENES && l->rows_per_scene > 0 &&
+                      l->rows_per_scene * l->n_views == l->n_rows && l->lin_z_scene_stride >= 0 &&
+                      l->lin_z_scene_stride % 4 == 0 && reinterpret_cast<uintptr_t>(l->lin_z_table) % 16 == 0,
+                  "avr_bn_layer_run: lin_z_table needs xyz, 1..%d views of rows_per_scene rows each (n_rows in "
+                  "all), a 16-B aligned table", AVR_MAX_SCENES);
+      for (int v = 0; v < l->n_views; ++v) {
+        AVR_REQUIRE(l->views[v].latent_h > 0 && l->views[v].latent_w > 0, "avr_bn_layer_run: view %d latent size", v);
+        view_from_desc(&l->views[v], &a.zviews[v]);
+      }
+      a.ztab = l->lin_z_table; a.ztab_stride = l->lin_z_scene_stride; a.zrows = l->rows_per_scene; a.zxyz = l->xyz;
+    }
   } else {
     AVR_REQUIRE(ly >= 2 && l->in_dim == H, "avr_bn_layer_run: the backward runs fc_0 / fc_1 (d_hidden columns)");
-    AVR_REQUIRE(l->mask_rows && l->pre_rows && l->out_mu && l->out_invstd,
-                "avr_bn_layer_run: AVR_BN_BWD needs mask_rows, pre_rows, out_mu, out_invstd");
+    AVR_REQUIRE(l->pre_rows && l->out_mu && l->out_invstd && l->out_scale && l->out_shift,
+                "avr_bn_layer_run: AVR_BN_BWD needs pre_rows, out_mu, out_invstd, out_scale, out_shift");
     BwdLayout LB;
     if ((rc = field_bwd_layout(dims, &LB))) return rc;
     a.w = l->blob + (ly % 2 == 0 ? LB.fc0t[(ly - 2) / 2] : LB.fc1t[(ly - 2) / 2]);
     hdr = reinterpret_cast<const unsigned*>(l->blob);
-    a.mask_rows = l->mask_rows; a.pre_rows = l->pre_rows; a.out_mu = l->out_mu; a.out_invstd = l->out_invstd;
+    a.pre_rows = l->pre_rows; a.out_mu = l->out_mu; a.out_invstd = l->out_invstd;
+    a.out_scale = l->out_scale; a.out_shift = l->out_shift;
   }
   a.hdr = hdr;
   a.hdr_idx = ly;

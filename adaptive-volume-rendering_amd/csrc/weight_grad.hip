@@ -14,7 +14,9 @@
 // v_mfma_f32_16x16x32_f16 with gfx950's transposing ds_read_b64_tr_b16.
 // Products are W-split x3 (Gh.Xh + Gh.Xl + Gl.Xh, fp32 accumulate) under
 // per-layer power-of-two scales from the max |G| / |X| the producing kernels
-// tracked, the same arithmetic as the forward's GEMMs.
+// tracked, the same arithmetic as the forward's GEMMs. A layer may name a
+// per-column BatchNorm-relu transform of X (the training-mode BN path's
+// operands, rebuilt from the pre-BN rows in the staging instead of stored).
 //
 // Work split: workgroup = one 128 x 128 output tile of one layer over one
 // K-range; 4 waves of 64 x 64 (4 x 4 MFMA tiles). Consecutive workgroups on
@@ -30,6 +32,7 @@ constexpr int kDwRow = 256 + 32;             // bytes per row of a 128-column ha
 constexpr int kDwHalf = kDwK * kDwRow;       // one 128-column half image (32 rows)
 constexpr int kDwImg = 2 * kDwHalf;          // one fp16 image of 256 columns
 constexpr int kDwStage = 4 * kDwImg;         // G hi, G lo, X hi, X lo
+constexpr int kDwXf = 3 * kDwTile * 4;        // XF: the tile's BatchNorm column parameters (mu, scale, shift)
 
 struct DwLayerDev {
   const float* g;
@@ -40,6 +43,7 @@ struct DwLayerDev {
   const unsigned* xmax;
   float* part;
   float* bpart;
+  const float* xmu; const float* xscale; const float* xshift;   // NULL, or X = relu((x - mu) * scale + shift)
 };
 
 struct DwArgs {
@@ -52,6 +56,7 @@ typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
 typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) floatx4 lds_floatx4;
 
 // byte offset of column col of row r in a 256-column image (two 128-column
 // halves of padded 288-B rows: 8 consecutive rows start in 8 different 32-B
@@ -88,7 +93,9 @@ __device__ __forceinline__ half8 tr_frag(const lds_char* img_full, int col0_full
 // PIPE: the split of chunk c + 1 into its (free) stage and the loads of chunk
 // c + 2 are interleaved with chunk c's MFMAs instead of following them after
 // the barrier, so the two waves of a SIMD never both sit in a split phase.
-template <int NW, bool PIPE = false>
+// XF: some layer of the launch names a BatchNorm-relu transform of X (its own instantiation: the staging
+// registers of the default one are at the limit).
+template <int NW, bool PIPE = false, bool XF = false>
 __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
   constexpr int WI = NW / 2;                 // waves across the 256 input columns
   constexpr int TO = 8, TI = 16 / WI;        // 16 x 16 MFMA tiles per wave: output rows x input columns
@@ -156,7 +163,14 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
     split4(g, sG, hi, lo);
     *(lds_u32x2*)(st + off) = u32x2{hi.x, hi.y};
     *(lds_u32x2*)(st + kDwImg + off) = u32x2{lo.x, lo.y};
-    split4(xn[u], sX, hi, lo);
+    floatx4 xv = xn[u];
+    if constexpr (XF)
+      if (D.xmu) {   // block-uniform; the parameters from LDS (a global load here would make the wait for it
+                     // also wait for the chunk loads in flight behind it: the counter is in order)
+        const lds_floatx4* P = (const lds_floatx4*)(lds + 2 * kDwStage);
+        xv = bn_relu4(xv, P[cc], P[64 + cc], P[128 + cc]);
+      }
+    split4(xv, sX, hi, lo);
     *(lds_u32x2*)(st + 2 * kDwImg + off) = u32x2{hi.x, hi.y};
     *(lds_u32x2*)(st + 3 * kDwImg + off) = u32x2{lo.x, lo.y};
     if (bias) bsum += g;
@@ -255,6 +269,16 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
     lds_barrier();
   };
 
+  if constexpr (XF) {
+    if (D.xmu && nch > 0) {
+      if (threadIdx.x < 192) {
+        const int k = threadIdx.x >> 6;
+        const float* src = k == 0 ? D.xmu : (k == 1 ? D.xscale : D.xshift);
+        ((lds_floatx4*)(lds + 2 * kDwStage))[threadIdx.x] = *reinterpret_cast<const floatx4*>(src + xcol);
+      }
+      __syncthreads();
+    }
+  }
   if (nch > 0) {
 #pragma unroll
     for (int u = 0; u < NU; ++u) load_u(0, u);
@@ -379,6 +403,7 @@ extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int
   a.kper = ((per + kDwK - 1) / kDwK) * kDwK;
   if (a.kper == 0) a.kper = kDwK;
   int tiles = 0;
+  bool xf = false;
   for (int l = 0; l < n_layers; ++l) {
     const avr_wgrad_layer& s = layers[l];
     AVR_REQUIRE(s.grad && s.input && s.partial && s.grad_max && s.input_max, "avr_weight_grads: null pointer (layer %d)", l);
@@ -392,6 +417,13 @@ extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int
     D.tile0 = tiles;
     D.gmax = s.grad_max; D.xmax = s.input_max;
     D.part = s.partial; D.bpart = s.bias_partial;
+    AVR_REQUIRE((!s.in_mu && !s.in_scale && !s.in_shift) ||
+                    (s.in_mu && s.in_scale && s.in_shift &&
+                     ((reinterpret_cast<uintptr_t>(s.in_mu) | reinterpret_cast<uintptr_t>(s.in_scale) |
+                       reinterpret_cast<uintptr_t>(s.in_shift)) % 16) == 0),
+                "avr_weight_grads: layer %d: in_mu / in_scale / in_shift all NULL or all set (16-B aligned)", l);
+    D.xmu = s.in_mu; D.xscale = s.in_scale; D.xshift = s.in_shift;
+    xf = xf || s.in_mu;
     tiles += ((s.out_dim + kDwTile - 1) / kDwTile) * D.nIt;
   }
   a.tiles = tiles;
@@ -404,7 +436,9 @@ extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int
         hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel<8>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel<8, true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess)
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&weight_grad_kernel<8, true, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kDwStage + kDwXf) != hipSuccess)
       return fail(AVR_E_HIP, "weight_grad_kernel: cannot set dynamic LDS");
     attr = true;
   }
@@ -412,7 +446,9 @@ extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int
   // AVR_WGRAD_PIPE=0: the 8-wave kernel with the split after the MFMAs (the round-2 schedule, kept for A/B;
   // the pipelined one is 3-6 % faster, profiles/r03g_wgrad_pipe_ab.txt)
   const char* pe = getenv("AVR_WGRAD_PIPE");
-  if (e && atoi(e) == 4)
+  if (xf)   // BatchNorm-relu inputs: the pipelined 8-wave kernel with the transform (no A/B variants)
+    weight_grad_kernel<8, true, true><<<(unsigned)blocks, 512, 2 * kDwStage + kDwXf, as_stream(stream)>>>(a);
+  else if (e && atoi(e) == 4)
     weight_grad_kernel<4><<<(unsigned)blocks, 256, 2 * kDwStage, as_stream(stream)>>>(a);
   else if (pe && atoi(pe) == 0)
     weight_grad_kernel<8, false><<<(unsigned)blocks, 512, 2 * kDwStage, as_stream(stream)>>>(a);

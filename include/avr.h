@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 11
+#define AVR_ABI_VERSION 12
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -340,6 +340,10 @@ typedef struct {
   const uint32_t* input_max;
   float* partial;           /* (n_split, out_dim, in_dim) */
   float* bias_partial;      /* (n_split, out_dim) or NULL */
+  /* ABI 12: NULL, or the layer input is relu((input - in_mu) * in_scale + in_shift) per column (in_dim each,
+   * 16-B aligned) -- a training-mode BatchNorm's operand rebuilt from its pre-BN rows (avr_bn_layer's
+   * AVR_BN_RELU, bit for bit); input_max is then the max of the rebuilt values. */
+  const float* in_mu; const float* in_scale; const float* in_shift;
 } avr_wgrad_layer;
 int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int64_t n_rows, int n_split, void* stream);
 /* The caller's sum above, for the whole layer list in one launch (ABI 9): dw[l] (out_dim, in_dim) =
@@ -349,7 +353,7 @@ int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int64_t n_rows
 int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_split, float* const* dw,
                             float* const* db, void* stream);
 
-/* ------------------------------------------------ training-mode BatchNorm (ABI 11)
+/* ------------------------------------------------ training-mode BatchNorm (ABI 11, 12)
  * train.py --bn (train.py:210, :265) builds ResnetBlockFC(bn=True): relu(bn_0(x)) -> fc_0 -> relu(bn_0(net))
  * -> fc_1 (+ x), bn_0 twice per block with batch statistics over every row of the field call
  * (models.py:430-432, 454-461; bn_1 is unused). The statistics are a reduction over all rows between two
@@ -359,20 +363,23 @@ int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_s
  *   mode AVR_BN_FWD: out = W . op + bias (+ add1) (+ add2) with W = the forward blob's layer `layer` (header
  *     numbering: 0 lin_in, 2 + 2b fc_0[b], 3 + 2b fc_1[b]; pack with dims->bn = 0: no eval-BN folding);
  *     partial (n_wg, 2, out_dim) = per 64-row workgroup (mean, sum of squared deviations) of out's columns.
- *   mode AVR_BN_BWD: gp = (W^T . op) * [mask_rows > 0] with W^T from the backward blob (avr_field_pack_bwd);
- *     out = gp; partial = per workgroup (sum gp, sum gp * xhat), xhat = (pre_rows - out_mu) * out_invstd.
+ *   mode AVR_BN_BWD: gp = (W^T . op) * [(pre_rows - out_mu) * out_scale + out_shift > 0] with W^T from the
+ *     backward blob (avr_field_pack_bwd): the relu mask of the forward's AVR_BN_RELU operand, recomputed from
+ *     the pre-BN rows (ABI 12; the relu'd operands need not be stored); out = gp; partial = per workgroup
+ *     (sum gp, sum gp * xhat), xhat = (pre_rows - out_mu) * out_invstd.
  *   The operand op (n_rows, in_dim), read from src (columns >= in_valid are 0):
  *     AVR_BN_PLAIN op = src;
  *     AVR_BN_RELU  op = relu((src - in_mu) * in_scale + in_shift)                 (forward: relu(bn_0(x)));
  *     AVR_BN_GRAD  op = src_res + in_scale * (src - in_m1 - (src_pre - in_mu) * in_invstd * in_m2)
  *                  (src = d loss / d bn output, torch's batch_norm backward; src_res may be NULL).
  *   operand_out (ld in_dim) / operand_max (float bits, atomicMax): the operand as the GEMM used it, or NULL.
- * avr_bn_stats: the forward partials -> batch mean / invstd (fp64 Chan combine), scale = gamma * invstd, and
+ * avr_bn_stats: the forward partials -> batch mean / invstd (folded in fp64: sum n mean, sum M2 + n mean^2),
+ *   scale = gamma * invstd, and
  *   the running statistics updated as torch does (momentum; unbiased variance).
  * avr_bn_grad_stats: the backward partials -> m1 = mean gp, m2 = mean gp * xhat, coef = gamma * invstd, and
  *   dgamma += sum gp * xhat, dbeta += sum gp.
  * avr_bn_grad_rows: out = res + coef * (g - m1 - (pre - mu) * invstd * m2) (the last BN backward, no GEMM after
- *   it), out_max as operand_max.                                                                               */
+ *   it), out_max as operand_max; out must not overlap g, pre or res.                                                                               */
 #define AVR_BN_FWD 0
 #define AVR_BN_BWD 1
 #define AVR_BN_PLAIN 0
@@ -391,9 +398,15 @@ typedef struct {
   const float* blob; int layer;
   const float* bias; const float* add1; const float* add2;   /* AVR_BN_FWD (rows ld d_hidden) */
   float* out;                                                 /* (n_rows, d_hidden) */
-  const float* mask_rows; const float* pre_rows;              /* AVR_BN_BWD (ld d_hidden) */
-  const float* out_mu; const float* out_invstd;
+  const float* pre_rows;                                      /* AVR_BN_BWD (ld d_hidden) */
+  const float* out_mu; const float* out_invstd; const float* out_scale; const float* out_shift;
   float* partial;           /* (ceil(n_rows / 64), 2, d_hidden), within avr_bn_partial_floats floats */
+  /* AVR_BN_FWD (ABI 12): NULL, or lin_z rows added last, gathered in the epilogue: row m of scene
+   * s = m / rows_per_scene (n_views scenes, n_rows = n_views * rows_per_scene) adds the bilinear blend of the table
+   * lin_z_table + s * lin_z_scene_stride ((latent_h * latent_w, d_hidden), e.g. avr_field_latent_table's) at the
+   * world point xyz[m] (n_rows, 3) in views[s] -- avr_latent_features' lookup and blend, bit for bit. */
+  const float* lin_z_table; int64_t lin_z_scene_stride;
+  const float* xyz; const avr_view_desc* views; int n_views; int64_t rows_per_scene;
 } avr_bn_layer;
 int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* l, void* stream);
 /* Floats of an avr_bn_layer partial buffer for n_rows rows of n_cols columns: the per-workgroup partials

@@ -170,6 +170,9 @@ int main(void) {
     expect("wgrad reduce null db list", avr_weight_grads_reduce(&wl, 1, 1, dwp, NULL, NULL), AVR_E_INVALID);
     wl.in_dim = 6;
     expect("wgrad reduce odd dims", avr_weight_grads_reduce(&wl, 1, 1, dwp, dbp, NULL), AVR_E_INVALID);
+    wl.in_dim = 8; wl.grad = buf; wl.input = buf; wl.ld_grad = 8; wl.ld_input = 8;
+    wl.grad_max = (const uint32_t*)buf; wl.input_max = (const uint32_t*)buf; wl.in_mu = buf;
+    expect("wgrad half a BN transform", avr_weight_grads(&wl, 1, 64, 1, NULL), AVR_E_INVALID);
   }
   expect("latent_features null view", avr_latent_features(NULL, NULL, 4, NULL, 3, NULL, NULL), AVR_E_INVALID);
   expect("latent_features_batch too many scenes",
@@ -202,8 +205,13 @@ int main(void) {
     l.prologue = AVR_BN_PLAIN; l.layer = 2 + 2 * d.n_blocks;
     expect("bn_layer bad layer", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
     l.layer = 2; l.mode = AVR_BN_BWD;
-    expect("bn_layer bwd without mask rows", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
-    l.mode = AVR_BN_FWD; d.bn = 1;
+    expect("bn_layer bwd without pre rows", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    l.mode = AVR_BN_FWD; l.lin_z_table = buf; l.n_views = 1; l.rows_per_scene = 100;
+    expect("bn_layer lin_z without points", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    l.xyz = buf; l.views = &v; l.rows_per_scene = 50;
+    expect("bn_layer lin_z rows", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
+    l.lin_z_table = NULL; l.xyz = NULL; l.views = NULL; l.n_views = 0; l.rows_per_scene = 0;
+    d.bn = 1;
     expect("bn_layer folded blob", avr_bn_layer_run(&d, &l, NULL), AVR_E_INVALID);
     d.bn = 0; l.n_rows = 0;
     expect("bn_layer empty", avr_bn_layer_run(&d, &l, NULL), AVR_OK);
