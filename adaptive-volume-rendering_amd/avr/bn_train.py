@@ -152,8 +152,13 @@ class _FieldTrainBN(torch.autograd.Function):
             tables = fused.tables_batch(coarse, SB, fast=True, bn_fold=False)
             views = (ViewDesc * SB)(*[fused.view(s) for s in range(SB)])
             p = xyz.detach().to(F32).contiguous()
-            lin_z = lambda b: dict(lin_z_table=tables[0, b], lin_z_scene_stride=tables.stride(0), xyz=p,  # noqa: E731
-                                   views=ctypes.addressof(views), n_views=SB, rows_per_scene=B) if b < nz else {}
+
+            def lin_z(b):
+                """avr_bn_layer fields adding lin_z[b](latent features) rows (none past the last lin_z)."""
+                if b >= nz:
+                    return {}
+                return dict(lin_z_table=tables[0, b], lin_z_scene_stride=tables.stride(0), xyz=p,
+                            views=ctypes.addressof(views), n_views=SB, rows_per_scene=B)
             # biases with the lin_z biases folded where the tables (no bias) are added
             lz_b = [P[f"lin_z.{b}.bias"].detach() for b in range(nz)]
             b_in = P["lin_in.bias"].detach() + (lz_b[0] if nz > 0 else 0)

@@ -299,10 +299,13 @@ class NewPixelNeRFNet(nn.Module):
 
     def can_train_bn(self, xyz, viewdirs):
         """train.py --bn in training mode (batch statistics): the layer-by-layer HIP path (avr.bn_train), with
-        or without autograd; points must not need gradients through it (view directions never)."""
+        or without autograd, up to AVR_MAX_SCENES scenes per call (its layer epilogues gather the lin_z rows of
+        every scene); points must not need gradients through it (view directions never)."""
+        from . import _lib
         from .bn_train import bn_train_eligible
         return (self.use_fused and self.hip_backward and xyz.is_cuda and viewdirs is not None
-                and not viewdirs.requires_grad and xyz.shape[0] * xyz.shape[1] >= 2 and bn_train_eligible(self))
+                and not viewdirs.requires_grad and xyz.shape[0] * xyz.shape[1] >= 2
+                and xyz.shape[0] <= _lib.AVR_MAX_SCENES and bn_train_eligible(self))
 
     def mlp_inputs(self, xyz, viewdirs, latent=None):
         """(latent features (SB*B, d_latent), z_feature (SB*B, d_in)) at the
