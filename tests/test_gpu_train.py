@@ -264,6 +264,36 @@ def test_weight_grads_kernel_vs_fp64(M, O, I, ld, waves, pipe, monkeypatch):
         assert res[1][1] is None
 
 
+@pytest.mark.parametrize("M,O,I,ld", [(1000, 512, 512, 512), (333, 64, 128, 136), (4096, 4, 512, 512)])
+def test_weight_grads_bn_transform_vs_fp64(M, O, I, ld):
+    """avr_weight_grads with the BatchNorm-relu input transform (ABI 12: X = relu((x - mu) * scale + shift) per
+    column, the training-mode BN path's operand rebuilt from its pre-BN rows in the staging) against an fp64
+    G^T X of the same fp32 operand -- built with the kernels' own expression (one fma per value) -- in a batch
+    with an untransformed layer, ragged rows and a row stride wider than the layer."""
+    from avr import ops
+    g = torch.Generator(device="cpu").manual_seed(M + O + I)
+    pre = (torch.randn(M, ld, generator=g) * 3.0 + 0.5).to(DEV)
+    mu = (torch.randn(I, generator=g) * 0.3 + 0.5).to(DEV)
+    scale = (torch.rand(I, generator=g) + 0.2).to(DEV)
+    shift = (torch.randn(I, generator=g) * 0.2).to(DEV)
+    X = torch.relu(torch.addcmul(shift, pre[:, :I] - mu, scale))       # fma((x - mu), scale, shift), then relu
+    G = (torch.randn(M, O, generator=g) * 1e-3).to(DEV)
+    G2 = torch.randn(M, O, generator=g).to(DEV)
+    Xp = torch.relu(torch.randn(M, I, generator=g)).to(DEV)
+    mb = ops._max_bits
+    lay = [(G, pre[:, :I], mb(G), mb(X), True, (mu, scale, shift)), (G2, Xp, mb(G2), mb(Xp), True)]
+    res = ops.weight_grads(lay, M)
+    for (dW, db), GG, XX in zip(res, (G, G2), (X, Xp)):
+        ref = (GG.double().t() @ XX.double()).float().cpu().numpy()
+        got = dW.cpu().numpy()
+        scale_r = max(float(np.abs(ref).max()), 1e-30)
+        assert float(np.abs(got - ref).max()) <= 2e-6 * scale_r, float(np.abs(got - ref).max()) / scale_r
+        bref = GG.double().sum(0).float().cpu().numpy()
+        np.testing.assert_allclose(db.cpu().numpy(), bref, rtol=0, atol=2e-6 * float(np.abs(bref).max()))
+    with pytest.raises(Exception, match="BatchNorm transform"):
+        ops.weight_grads([(G, pre[:, :I], mb(G), mb(X), True, (mu, scale, shift[:-4]))], M)
+
+
 def test_latent_features_kernel_vs_grid_sample():
     """avr_latent_features (row-major pixel-aligned lookup) against the module's
     SpatialEncoder.index (torch grid_sample), two scenes, points inside and
