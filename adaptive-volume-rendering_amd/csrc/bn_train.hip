@@ -93,35 +93,68 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   const int G4 = a.K / 4;                    // column groups of a row
   const int rs = a.K + 4;                    // stage row stride (floats)
   float mx = 0.f;
-  // pair i of this lane: row wid + NW (i >> 1), column group lane + 64 (i & 1) (K <= 512: <= 2 per row);
-  // fully unrolled so every load of a pair is issued before the first one is used
+  // pair i of this lane: row wid + NW (i >> 1), column group lane + 64 (i & 1) (K <= 512: <= 2 per row). In
+  // batches of PB pairs, every load of a batch issued before the batch's first store: a load cannot move above a
+  // store that may alias it, and the in-order memory counter makes a wait on a load also wait on every store
+  // issued before it -- one round trip per pair otherwise. The lane's two column groups' parameters are loaded
+  // once (RELU: mu, scale, shift; GRAD: mu, invstd, m1, m2, scale).
+  floatx4 pp[5][2];
 #pragma unroll
-  for (int i = 0; i < MAXQ; ++i) {
-    const int r = wid + NW * (i >> 1), q = lane + 64 * (i & 1);
-    if (r < kX3Samples && q < G4) {
-      const bool live = r < nvalid;
-      const int64_t row = m0 + (live ? r : 0);
-      const int k = 4 * q;
-      floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (k + 4 <= a.kin) {
-        v = ld4(a.src + row * a.ld_src + k);
-      } else if (k < a.kin) {
+  for (int h = 0; h < 2; ++h) {
+    const int k = 4 * (lane + 64 * h) < a.kin ? 4 * (lane + 64 * h) : 0;
+    if (a.prologue == AVR_BN_RELU) {
+      pp[0][h] = ld4(a.in_mu + k); pp[1][h] = ld4(a.in_scale + k); pp[2][h] = ld4(a.in_shift + k);
+    } else if (a.prologue == AVR_BN_GRAD) {
+      pp[0][h] = ld4(a.in_mu + k); pp[1][h] = ld4(a.in_invstd + k); pp[2][h] = ld4(a.in_m1 + k);
+      pp[3][h] = ld4(a.in_m2 + k); pp[4][h] = ld4(a.in_scale + k);
+    }
+  }
+  // (the backward's GRAD prologue holds three rows per pair: smaller batches keep it within the registers)
+  constexpr int PB = MAXQ < 8 ? MAXQ : (MODE == AVR_BN_FWD ? 8 : 4);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = k + t < a.kin ? a.src[row * a.ld_src + k + t] : 0.f;
-      }
-      if (k < a.kin) {
-        if (a.prologue == AVR_BN_RELU) {
-          v = bn_relu4(v, ld4(a.in_mu + k), ld4(a.in_scale + k), ld4(a.in_shift + k));
-        } else if (a.prologue == AVR_BN_GRAD) {
-          const floatx4 xh = (ld4(a.src_pre + row * a.ld_src + k) - ld4(a.in_mu + k)) * ld4(a.in_invstd + k);
-          v = (v - ld4(a.in_m1 + k) - xh * ld4(a.in_m2 + k)) * ld4(a.in_scale + k);
-          if (a.src_res) v += ld4(a.src_res + row * a.ld_src + k);
+  for (int b0 = 0; b0 < MAXQ; b0 += PB) {
+    floatx4 sv[PB], pv[PB], rv[PB];
+#pragma unroll
+    for (int jb = 0; jb < PB; ++jb) {
+      const int i = b0 + jb, r = wid + NW * (i >> 1), q = lane + 64 * (i & 1);
+      sv[jb] = pv[jb] = rv[jb] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (r < kX3Samples && q < G4) {
+        const int64_t row = m0 + (r < nvalid ? r : 0);
+        const int k = 4 * q;
+        if (k + 4 <= a.kin) {
+          sv[jb] = ld4(a.src + row * a.ld_src + k);
+        } else if (k < a.kin) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) sv[jb][t] = k + t < a.kin ? a.src[row * a.ld_src + k + t] : 0.f;
+        }
+        if (a.prologue == AVR_BN_GRAD && k < a.kin) {
+          pv[jb] = ld4(a.src_pre + row * a.ld_src + k);
+          if (a.src_res) rv[jb] = ld4(a.src_res + row * a.ld_src + k);
         }
       }
-      if (!live) v = floatx4{0.f, 0.f, 0.f, 0.f};
-      else if (a.opnd_out) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a.opnd_out + row * a.K + k));
-      *reinterpret_cast<floatx4*>(lds + r * rs + k) = v;
-      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+#pragma unroll
+    for (int jb = 0; jb < PB; ++jb) {
+      const int i = b0 + jb, r = wid + NW * (i >> 1), q = lane + 64 * (i & 1), h = i & 1;
+      if (r < kX3Samples && q < G4) {
+        const bool live = r < nvalid;
+        const int64_t row = m0 + (live ? r : 0);
+        const int k = 4 * q;
+        floatx4 v = sv[jb];
+        if (k < a.kin) {
+          if (a.prologue == AVR_BN_RELU) {
+            v = bn_relu4(v, pp[0][h], pp[1][h], pp[2][h]);
+          } else if (a.prologue == AVR_BN_GRAD) {
+            const floatx4 xh = (pv[jb] - pp[0][h]) * pp[1][h];
+            v = (v - pp[2][h] - xh * pp[3][h]) * pp[4][h];
+            if (a.src_res) v += rv[jb];
+          }
+        }
+        if (!live) v = floatx4{0.f, 0.f, 0.f, 0.f};
+        else if (a.opnd_out) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a.opnd_out + row * a.K + k));
+        *reinterpret_cast<floatx4*>(lds + r * rs + k) = v;
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
     }
   }
   mx = wave_max(mx);
@@ -172,8 +205,6 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   }
   __syncthreads();
   floatx4 yv[MAXQ];
-  Bilinear zbl{};                            // forward with ztab: the current row's lin_z corners
-  const float* ztab = a.ztab;
   floatx4 s1[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}}, s2[2] = {s1[0], s1[0]};
   floatx4 cp0[2], cp1[2], cp2[2], cp3[2];    // per-column parameters of the lane's two groups
 #pragma unroll
@@ -189,48 +220,88 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
       cp3[h] = ld4(a.out_shift + f);
     }
   }
+  // pair i as in the prologue; every load of the epilogue is issued before its first store (see there)
+  const auto valid = [&](int i) { return wid + NW * (i >> 1) < kX3Samples && lane + 64 * (i & 1) < EQ; };
+  const auto live = [&](int i) { return wid + NW * (i >> 1) < nvalid; };
+  const auto row_of = [&](int i) -> int64_t { return m0 + (live(i) ? wid + NW * (i >> 1) : 0); };
+  const auto col_of = [&](int i) { return 4 * (lane + 64 * (i & 1)); };
+  const auto staged = [&](int i) {
+    return valid(i) ? *reinterpret_cast<const floatx4*>(lds + (wid + NW * (i >> 1)) * es + col_of(i))
+                    : floatx4{0.f, 0.f, 0.f, 0.f};
+  };
+  if constexpr (MODE == AVR_BN_FWD) {
 #pragma unroll
-  for (int i = 0; i < MAXQ; ++i) {
-    const int r = wid + NW * (i >> 1), q = lane + 64 * (i & 1);
-    yv[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-    if (r < kX3Samples && q < EQ) {
-      const bool live = r < nvalid;
-      const int64_t row = m0 + (live ? r : 0);
-      const int f = 4 * q;
-      floatx4 v = *reinterpret_cast<const floatx4*>(lds + r * es + f);
-      if constexpr (MODE == AVR_BN_FWD) {
-        v += cp0[i & 1];
-        if (a.add1) v += ld4(a.add1 + row * HID + f);
-        if (a.add2) v += ld4(a.add2 + row * HID + f);
-        if (a.ztab) {   // the row's lin_z features: avr_latent_features' lookup and blend order, bit for bit
-          if ((i & 1) == 0) {
-            const int64_t sc = row / a.zrows;
-            zbl = bilinear_at(a.zviews[sc], a.zxyz[3 * row], a.zxyz[3 * row + 1], a.zxyz[3 * row + 2]);
-            ztab = a.ztab + sc * a.ztab_stride;
+    for (int i = 0; i < MAXQ; ++i) yv[i] = staged(i);
+    // out = W . op + bias (+ add1) (+ add2) (+ lin_z rows), added in that order
+#pragma unroll
+    for (int i = 0; i < MAXQ; ++i)
+      if (valid(i)) yv[i] += cp0[i & 1];
+    if (a.add1) {
+#pragma unroll
+      for (int i = 0; i < MAXQ; ++i)
+        if (valid(i)) yv[i] += ld4(a.add1 + row_of(i) * HID + col_of(i));
+    }
+    if (a.add2) {
+#pragma unroll
+      for (int i = 0; i < MAXQ; ++i)
+        if (valid(i)) yv[i] += ld4(a.add2 + row_of(i) * HID + col_of(i));
+    }
+    if (a.ztab) {   // the rows' lin_z features: avr_latent_features' lookup and blend order, bit for bit
+      // the points of the wave's rows first (one load each, all in flight together), then per row its corners
+      float px[MAXQ / 2][3];
+#pragma unroll
+      for (int i = 0; i < MAXQ; i += 2)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) px[i >> 1][d] = a.zxyz[3 * row_of(i) + d];
+      const int64_t sc0 = m0 / a.zrows;      // the workgroup's first scene (rows are scene-major)
+#pragma unroll
+      for (int i = 0; i < MAXQ; i += 2) {
+        if (wid + NW * (i >> 1) < kX3Samples) {
+          int64_t sc = sc0;
+          while (row_of(i) >= (sc + 1) * a.zrows) ++sc;
+          const Bilinear bl = bilinear_at(a.zviews[sc], px[i >> 1][0], px[i >> 1][1], px[i >> 1][2]);
+          const float* tab = a.ztab + sc * a.ztab_stride;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            if (valid(i + h)) {
+              const int f = col_of(i + h);
+              const floatx4 c0 = ld4(tab + (int64_t)bl.tex[0] * HID + f), c1 = ld4(tab + (int64_t)bl.tex[1] * HID + f);
+              const floatx4 c2 = ld4(tab + (int64_t)bl.tex[2] * HID + f), c3 = ld4(tab + (int64_t)bl.tex[3] * HID + f);
+              floatx4 z;
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+                z[t] = fadd(fadd(fadd(fmul(c0[t], bl.w[0]), fmul(c1[t], bl.w[1])), fmul(c2[t], bl.w[2])),
+                            fmul(c3[t], bl.w[3]));
+              yv[i + h] += z;
+            }
           }
-          const floatx4 c0 = ld4(ztab + (int64_t)zbl.tex[0] * HID + f), c1 = ld4(ztab + (int64_t)zbl.tex[1] * HID + f);
-          const floatx4 c2 = ld4(ztab + (int64_t)zbl.tex[2] * HID + f), c3 = ld4(ztab + (int64_t)zbl.tex[3] * HID + f);
-          floatx4 z;
+        }
+      }
+    }
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
-            z[t] = fadd(fadd(fadd(fmul(c0[t], zbl.w[0]), fmul(c1[t], zbl.w[1])), fmul(c2[t], zbl.w[2])),
-                        fmul(c3[t], zbl.w[3]));
-          v += z;
-        }
-        if (live) {
-          *reinterpret_cast<floatx4*>(a.out + row * HID + f) = v;
-          s1[i & 1] += v;
-          yv[i] = v;
-        }
-      } else if (live) {
-        // the relu mask of the forward operand, recomputed from the pre-BN row (bn_relu4, as the forward did)
-        const floatx4 p = ld4(a.pre_rows + row * HID + f);
-        const floatx4 z = bn_relu4(p, cp0[i & 1], cp2[i & 1], cp3[i & 1]);
+    for (int i = 0; i < MAXQ; ++i) {
+      if (valid(i) && live(i)) {
+        *reinterpret_cast<floatx4*>(a.out + row_of(i) * HID + col_of(i)) = yv[i];
+        s1[i & 1] += yv[i];
+      }
+    }
+  } else {
+    // gp = (W^T . op) * relu mask of the forward operand, recomputed from the pre-BN row (bn_relu4, as the
+    // forward did); the pre-BN rows also give xhat for the statistics
+    floatx4 pv[MAXQ];
+#pragma unroll
+    for (int i = 0; i < MAXQ; ++i)
+      pv[i] = valid(i) ? ld4(a.pre_rows + row_of(i) * HID + col_of(i)) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < MAXQ; ++i) {
+      if (valid(i) && live(i)) {
+        const floatx4 z = bn_relu4(pv[i], cp0[i & 1], cp2[i & 1], cp3[i & 1]);
+        const floatx4 v = staged(i);
         floatx4 gp;
         gp.x = z.x > 0.f ? v.x : 0.f; gp.y = z.y > 0.f ? v.y : 0.f;
         gp.z = z.z > 0.f ? v.z : 0.f; gp.w = z.w > 0.f ? v.w : 0.f;
-        *reinterpret_cast<floatx4*>(a.out + row * HID + f) = gp;
-        const floatx4 xh = (p - cp0[i & 1]) * cp1[i & 1];
+        *reinterpret_cast<floatx4*>(a.out + row_of(i) * HID + col_of(i)) = gp;
+        const floatx4 xh = (pv[i] - cp0[i & 1]) * cp1[i & 1];
         s1[i & 1] += gp;
         s2[i & 1] += gp * xh;
       }
