@@ -18,6 +18,14 @@ __device__ __forceinline__ floatx4 bn_relu4(floatx4 x, floatx4 mu, floatx4 scale
                  fmaxf(__builtin_fmaf(d.z, scale.z, shift.z), 0.f), fmaxf(__builtin_fmaf(d.w, scale.w, shift.w), 0.f)};
 }
 
+// atomicMax on a max-|x| word (non-negative float bits) only where v would raise it: every workgroup of a
+// large grid publishing into one word (or one cache line) serialises at its L2 channel; after the first
+// workgroups almost all of them only read. A stale read only costs an atomic that changes nothing.
+__device__ __forceinline__ void publish_max(unsigned* p, float v) {
+  const unsigned b = __float_as_uint(v);
+  if (v > 0.f && b > __atomic_load_n(p, __ATOMIC_RELAXED)) atomicMax(p, b);
+}
+
 // ------------------------------------------------------------------ errors
 void set_error(const char* fmt, ...);
 int fail(int code, const char* fmt, ...);

@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   if (lane == 0) red[wid] = mx;
   lds_barrier();
   const float wgmax = red_max<NW>(red);
-  if (a.opnd_max && wid == 0 && lane == 0 && wgmax > 0.f) atomicMax(a.opnd_max, __float_as_uint(wgmax));
+  if (a.opnd_max && wid == 0 && lane == 0) publish_max(a.opnd_max, wgmax);
   const float s_x = pow2_scale_for(wgmax);
   const int qpw = a.K / 4 / NW;              // phase B: column groups of this wave
   floatx4 xv[MAXQ];
@@ -476,8 +476,15 @@ __global__ void __launch_bounds__(256) bn_grad_rows_kernel(int64_t n_rows, int N
       }
     }
   }
+  // one publish per block (publish_max: thousands of blocks' atomics on one word serialise at its L2 channel;
+  // one per wave took most of this kernel's time)
+  __shared__ float red[4];
   mx = wave_max(mx);
-  if (out_max && (threadIdx.x & 63) == 0 && mx > 0.f) atomicMax(out_max, __float_as_uint(mx));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0 && out_max) {
+    publish_max(out_max, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  }
 }
 
 // Two-stage finalize: stage 1 (grid column blocks x row groups of 16 partials, one wave each: lane = column,

@@ -191,8 +191,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   store_rows<FT, NW>(a.G + 2 * nb * a.g_stride + roff * HID, dx, base, a.M, wid, g, j);
   if (a.g_max) {
     const float mx_in = absmax<FT>(dx);
-    if (lane == 0) atomicMax(a.g_max + 2 * nb, __float_as_uint(mx_in));
-    if (wid == 0 && lane < 2 * nb) atomicMax(a.g_max + lane, __float_as_uint(lmax[lane]));
+    if (lane == 0) publish_max(a.g_max + 2 * nb, mx_in);
+    if (wid == 0 && lane < 2 * nb) publish_max(a.g_max + lane, lmax[lane]);
   }
 }
 

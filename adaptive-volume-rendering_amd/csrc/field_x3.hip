@@ -672,8 +672,8 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     // the layer maxima: one atomic per workgroup and layer, issued last (nothing waits on them here;
     // one per wave and layer in front of the weight loads cost ~1 ms per default_mv fine pass)
     const int nl = 2 * a.n_blocks + 1;
-    if (a.act_max && wid == 0 && lane < nl) atomicMax(a.act_max + lane, __float_as_uint(tail->lmax[lane]));
-    if (a.zf_max && threadIdx.x == 64) atomicMax(a.zf_max, __float_as_uint(tail->zmax));
+    if (a.act_max && wid == 0 && lane < nl) publish_max(a.act_max + lane, tail->lmax[lane]);
+    if (a.zf_max && threadIdx.x == 64) publish_max(a.zf_max, tail->zmax);
   }
 }
 

@@ -31,18 +31,26 @@ __global__ void __launch_bounds__(256) latent_features_kernel(LatBatch vb, const
   xyz += 3 * s * n_points;
   out += s * n_points * C;
   const Bilinear bl = bilinear_at(vb.v[s], xyz[3 * m], xyz[3 * m + 1], xyz[3 * m + 2]);
-  for (int c = 4 * lane; c < C; c += 256) {
-    float4 acc;
-    const float4 a = *reinterpret_cast<const float4*>(lat_hwc + (int64_t)bl.tex[0] * C + c);
-    const float4 b = *reinterpret_cast<const float4*>(lat_hwc + (int64_t)bl.tex[1] * C + c);
-    const float4 d = *reinterpret_cast<const float4*>(lat_hwc + (int64_t)bl.tex[2] * C + c);
-    const float4 e = *reinterpret_cast<const float4*>(lat_hwc + (int64_t)bl.tex[3] * C + c);
-    // grid_sample's order: nw, ne, sw, se
-    acc.x = fadd(fadd(fadd(fmul(a.x, bl.w[0]), fmul(b.x, bl.w[1])), fmul(d.x, bl.w[2])), fmul(e.x, bl.w[3]));
-    acc.y = fadd(fadd(fadd(fmul(a.y, bl.w[0]), fmul(b.y, bl.w[1])), fmul(d.y, bl.w[2])), fmul(e.y, bl.w[3]));
-    acc.z = fadd(fadd(fadd(fmul(a.z, bl.w[0]), fmul(b.z, bl.w[1])), fmul(d.z, bl.w[2])), fmul(e.z, bl.w[3]));
-    acc.w = fadd(fadd(fadd(fmul(a.w, bl.w[0]), fmul(b.w, bl.w[1])), fmul(d.w, bl.w[2])), fmul(e.w, bl.w[3]));
-    __builtin_nontemporal_store(floatx4{acc.x, acc.y, acc.z, acc.w}, reinterpret_cast<floatx4*>(out + m * C + c));
+  // two 256-channel groups per pass, both gathered before either is stored (a load behind a store waits for it)
+  for (int c0 = 4 * lane; c0 < C; c0 += 512) {
+    floatx4 acc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = c0 + 256 * u;
+      if (c < C) {
+        const floatx4 a = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[0] * C + c);
+        const floatx4 b = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[1] * C + c);
+        const floatx4 d = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[2] * C + c);
+        const floatx4 e = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[3] * C + c);
+        // grid_sample's order: nw, ne, sw, se
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[u][t] = fadd(fadd(fadd(fmul(a[t], bl.w[0]), fmul(b[t], bl.w[1])), fmul(d[t], bl.w[2])), fmul(e[t], bl.w[3]));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (c0 + 256 * u < C) __builtin_nontemporal_store(acc[u], reinterpret_cast<floatx4*>(out + m * C + c0 + 256 * u));
   }
 }
 
