@@ -136,6 +136,8 @@ _SIGS = {
                                 ctypes.POINTER(c_void_p), c_void_p],
     "avr_latent_features": [ctypes.POINTER(ViewDesc), c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
     "avr_latent_features_batch": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_int, c_void_p, i64, c_void_p, c_void_p],
+    "avr_latent_features_grad_points": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_int, c_void_p, i64, c_void_p,
+                                        c_void_p, c_void_p],
     "avr_bn_layer_run": [ctypes.POINTER(FieldDims), ctypes.POINTER(BnLayer), c_void_p],
     "avr_bn_partial_floats": [i64, c_int, ctypes.POINTER(i64)],
     "avr_bn_stats": [c_void_p, i64, c_int, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -91,3 +91,100 @@ extern "C" int avr_latent_features_batch(const avr_view_desc* views, int n_scene
       vb, latent_hwc, stride, channels, xyz, n_points, out);
   return check_launch("latent_features_kernel");
 }
+
+// ---- d loss / d xyz through the lookup (the adaptive renderer's band points carry a gradient): torch's
+// grid_sample grid gradient (bilinear, border padding, align_corners=True: a clipped coordinate passes none)
+// chained through grid = uv * scale - 1, uv = (-xc_xy / xc_z) * focal + c, xc = R x + t (models.py:753-810,
+// :260-273). One wave per point: lane l sums channels 4l, 4l + 256, ... of
+//   gix = sum_c g_c ((ne - nw) wy0 + (se - sw) wy1),  giy = sum_c g_c ((sw - nw) wx0 + (se - ne) wx1)
+// over the corner rows of latent_hwc (H*W, C) and the feature gradient row g (C), then lane 0 applies the
+// chain. The corners and weights are the forward's (bilinear_from_rot's operations); a corner past the edge
+// only occurs with a zero weight or a clipped (zero-gradient) coordinate, so its clamped texel changes nothing.
+namespace avr {
+
+__device__ __forceinline__ float lane_sum(float v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) latent_features_grad_points_kernel(LatBatch vb, const float* __restrict__ lat_hwc,
+                                                                          int64_t lat_stride, int C,
+                                                                          const float* __restrict__ xyz,
+                                                                          int64_t n_points,
+                                                                          const float* __restrict__ gfeat,
+                                                                          float* __restrict__ gxyz) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= n_points) return;
+  const int s = blockIdx.y;
+  const View& v = vb.v[s];
+  lat_hwc += s * lat_stride;
+  const int64_t row = s * n_points + m;
+  const float x0 = xyz[3 * row], x1 = xyz[3 * row + 1], x2 = xyz[3 * row + 2];
+  const float xr[3] = {dot3(v.R + 0, x0, x1, x2), dot3(v.R + 3, x0, x1, x2), dot3(v.R + 6, x0, x1, x2)};
+  const Bilinear bl = bilinear_from_rot(v, xr);
+  // the forward's coordinates again, for the weights and the clip masks
+  const float xc0 = fadd(xr[0], v.t[0]), xc1 = fadd(xr[1], v.t[1]), xc2 = fadd(xr[2], v.t[2]);
+  const float u = fadd(fmul(fdiv(-xc0, xc2), v.focal[0]), v.c[0]);
+  const float w = fadd(fmul(fdiv(-xc1, xc2), v.focal[1]), v.c[1]);
+  const float gx = fsub(fmul(u, v.scale[0]), 1.0f), gy = fsub(fmul(w, v.scale[1]), 1.0f);
+  const float ixr = fmul(fdiv(fadd(gx, 1.0f), 2.0f), (float)(v.W - 1));
+  const float iyr = fmul(fdiv(fadd(gy, 1.0f), 2.0f), (float)(v.H - 1));
+  const float ix = fminf(fmaxf(ixr, 0.f), (float)(v.W - 1)), iy = fminf(fmaxf(iyr, 0.f), (float)(v.H - 1));
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const float wx1 = fsub(ix, fx0), wy1 = fsub(iy, fy0);
+  const float wx0 = fsub(fadd(fx0, 1.0f), ix), wy0 = fsub(fadd(fy0, 1.0f), iy);
+  float sx = 0.f, sy = 0.f;
+  const float* g = gfeat + row * C;
+  for (int c = 4 * lane; c < C; c += 256) {
+    const floatx4 gv = *reinterpret_cast<const floatx4*>(g + c);
+    const floatx4 nw = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[0] * C + c);
+    const floatx4 ne = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[1] * C + c);
+    const floatx4 sw = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[2] * C + c);
+    const floatx4 se = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[3] * C + c);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sx += gv[t] * ((ne[t] - nw[t]) * wy0 + (se[t] - sw[t]) * wy1);
+      sy += gv[t] * ((sw[t] - nw[t]) * wx0 + (se[t] - ne[t]) * wx1);
+    }
+  }
+  sx = lane_sum(sx);
+  sy = lane_sum(sy);
+  if (lane == 0) {
+    // d grid -> d uv (the clip passes no gradient at or past either edge) -> d xc -> d x = R^T d xc
+    const float mxk = ixr > 0.f && ixr < (float)(v.W - 1) ? 1.f : 0.f;
+    const float myk = iyr > 0.f && iyr < (float)(v.H - 1) ? 1.f : 0.f;
+    const float gu = sx * (0.5f * (float)(v.W - 1)) * mxk * v.scale[0];
+    const float gw = sy * (0.5f * (float)(v.H - 1)) * myk * v.scale[1];
+    const float a0 = gu * v.focal[0], a1 = gw * v.focal[1];
+    const float inv_z = 1.0f / xc2;
+    const float d0 = -a0 * inv_z, d1 = -a1 * inv_z, d2 = (a0 * xc0 + a1 * xc1) * inv_z * inv_z;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) gxyz[3 * row + j] = v.R[j] * d0 + v.R[3 + j] * d1 + v.R[6 + j] * d2;
+  }
+}
+
+}  // namespace avr
+
+extern "C" int avr_latent_features_grad_points(const avr_view_desc* views, int n_scenes, const float* latent_hwc,
+                                               int channels, const float* xyz, int64_t n_points,
+                                               const float* grad_features, float* grad_xyz, void* stream) {
+  AVR_REQUIRE(n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES,
+              "avr_latent_features_grad_points: 1..%d scenes per call", AVR_MAX_SCENES);
+  AVR_REQUIRE(n_points >= 0 && channels > 0 && channels % 4 == 0, "avr_latent_features_grad_points: bad sizes");
+  if (n_points == 0) return AVR_OK;
+  AVR_REQUIRE(views && latent_hwc && xyz && grad_features && grad_xyz, "avr_latent_features_grad_points: null pointer");
+  LatBatch vb;
+  for (int s = 0; s < n_scenes; ++s) {
+    AVR_REQUIRE(views[s].latent_h == views[0].latent_h && views[s].latent_w == views[0].latent_w &&
+                    views[s].latent_h > 0 && views[s].latent_w > 0,
+                "avr_latent_features_grad_points: scenes need latent maps of one (positive) size");
+    view_from_desc(&views[s], &vb.v[s]);
+  }
+  const int64_t stride = (int64_t)views[0].latent_h * views[0].latent_w * channels;
+  latent_features_grad_points_kernel<<<dim3((unsigned)((n_points + 3) / 4), (unsigned)n_scenes), 256, 0,
+                                       as_stream(stream)>>>(vb, latent_hwc, stride, channels, xyz, n_points,
+                                                            grad_features, grad_xyz);
+  return check_launch("latent_features_grad_points_kernel");
+}

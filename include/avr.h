@@ -431,6 +431,14 @@ int avr_latent_features(const avr_view_desc* view, const float* latent_hwc, int 
  * (n_scenes, n_points, 3), out (n_scenes * n_points, channels).                                         */
 int avr_latent_features_batch(const avr_view_desc* views, int n_scenes, const float* latent_hwc, int channels,
                               const float* xyz, int64_t n_points, float* out, void* stream);
+/* ABI 12: the adjoint of that lookup with respect to the points -- grad_xyz (n_scenes * n_points, 3) = d loss /
+ * d xyz given grad_features (n_scenes * n_points, channels) = d loss / d features: grid_sample's grid gradient
+ * (bilinear, border padding -- a clipped coordinate passes no gradient --, align_corners=True) through the
+ * projection uv = (-xc_xy / xc_z) * focal + c, xc = R xyz + t (models.py:753-810, :260-273). Replaces the torch
+ * autograd of SpatialEncoder.index for the adaptive renderer's band points (renderers.py:492-508).           */
+int avr_latent_features_grad_points(const avr_view_desc* views, int n_scenes, const float* latent_hwc, int channels,
+                                    const float* xyz, int64_t n_points, const float* grad_features, float* grad_xyz,
+                                    void* stream);
 
 /* --------------------------------------------------------- LSTM ray marcher
  * Raymarcher / AdaptiveVolumeRenderer march (renderers.py:313-351, :380-432):

@@ -309,7 +309,45 @@ def test_latent_features_kernel_vs_grid_sample():
         np.testing.assert_allclose(got.cpu().numpy(), ref[sb * 333:(sb + 1) * 333].cpu().numpy(), atol=2e-6, rtol=1e-5)
 
 
-@pytest.mark.parametrize("d_hidden,latent_grad", [(64, False), (512, True)])
+def test_latent_features_grad_points_vs_autograd():
+    """avr_latent_features_grad_points (ABI 12: d loss / d xyz through the pixel-aligned lookup) against autograd
+    of the module's SpatialEncoder.index (torch grid_sample) in float64: two scenes, 512 channels, points inside
+    and outside the source image (border padding: a clipped coordinate passes no gradient), random feature
+    gradients; the fp32 autograd of the same lookup as the yardstick (2x its error + 1e-6 of max)."""
+    from avr import _lib
+    from avr._lib import ViewDesc
+    net = _net(128, 2, 512, (16, 16), sb=2)
+    xyz, vd, _ = _points(2, 700, seed=21)
+    xyz = xyz * torch.where(torch.arange(700, device=DEV) % 3 == 0, 3.0, 1.0).reshape(1, 700, 1)
+    g = torch.Generator().manual_seed(5)
+    gfeat = torch.randn(2 * 700, 512, generator=g).to(DEV)
+    fused = net.fused()
+    hwc = fused.latent_hwc_all(net.encoder.latent)
+    views = (ViewDesc * 2)(*[fused.view(sb) for sb in range(2)])
+    got = torch.empty(2 * 700, 3, device=DEV)
+    _lib.call("avr_latent_features_grad_points", views, 2, _lib.ptr(hwc), 512, _lib.ptr(xyz.contiguous()), 700,
+              _lib.ptr(gfeat), _lib.ptr(got), _lib.stream_of(got))
+
+    def autograd(dtype):
+        x = xyz.to(dtype).clone().requires_grad_(True)
+        feat, _ = net.mlp_inputs(x, vd.to(dtype))
+        return torch.autograd.grad(feat, x, gfeat.to(dtype))[0].reshape(-1, 3)
+
+    ref32 = autograd(torch.float32)
+    with torch.no_grad():
+        net.double()
+    try:
+        ref64 = autograd(torch.float64)
+    finally:
+        net.float()
+    s = float(ref64.abs().max())
+    eh = float((got.double() - ref64).abs().max())
+    et = float((ref32.double() - ref64).abs().max())
+    assert eh <= 2.0 * et + 1e-6 * s, (eh, et, s)
+    print(f"grad points: HIP err {eh / s:.2e}, torch fp32 err {et / s:.2e} of max {s:.3e}")
+
+
+@pytest.mark.parametrize("d_hidden,latent_grad", [(64, False), (512, False), (512, True)])
 def test_field_train_point_gradient(d_hidden, latent_grad):
     """Points that carry a gradient (the adaptive renderer's band samples,
     renderers.py:492-508): d loss / d xyz through PE, rotation, projection and
