@@ -180,6 +180,11 @@ int main(void) {
   expect("latent_features_batch null", avr_latent_features_batch(&v, 1, NULL, 4, buf, 3, buf, NULL), AVR_E_INVALID);
   expect("latent_features_batch odd channels", avr_latent_features_batch(&v, 1, buf, 6, buf, 3, buf, NULL),
          AVR_E_INVALID);
+  expect("latent_grad_points too many scenes",
+         avr_latent_features_grad_points(&v, AVR_MAX_SCENES + 1, buf, 4, buf, 3, buf, buf, NULL), AVR_E_INVALID);
+  expect("latent_grad_points null", avr_latent_features_grad_points(&v, 1, buf, 4, buf, 3, NULL, buf, NULL),
+         AVR_E_INVALID);
+  expect("latent_grad_points empty", avr_latent_features_grad_points(&v, 1, buf, 4, buf, 0, buf, buf, NULL), AVR_OK);
   expect("latent_table_batch null", avr_field_latent_table_batch(&d, NULL, NULL, 2, 8, 8, NULL, NULL), AVR_E_INVALID);
   expect("latent_table_batch no scenes", avr_field_latent_table_batch(&d, buf, buf, 0, 8, 8, buf, NULL),
          AVR_E_INVALID);
