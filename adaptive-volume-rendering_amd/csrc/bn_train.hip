@@ -114,22 +114,38 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
 #pragma unroll
   for (int b0 = 0; b0 < MAXQ; b0 += PB) {
     floatx4 sv[PB], pv[PB], rv[PB];
-#pragma unroll
-    for (int jb = 0; jb < PB; ++jb) {
+    // pair jb's source offset (rows past the end read row m0, columns past the row column 0: every load is
+    // unconditional, so none waits behind a branch); its values are dropped below where they do not belong
+    const auto src_off = [&](int jb) -> int64_t {
       const int i = b0 + jb, r = wid + NW * (i >> 1), q = lane + 64 * (i & 1);
-      sv[jb] = pv[jb] = rv[jb] = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (r < kX3Samples && q < G4) {
-        const int64_t row = m0 + (r < nvalid ? r : 0);
-        const int k = 4 * q;
-        if (k + 4 <= a.kin) {
-          sv[jb] = ld4(a.src + row * a.ld_src + k);
-        } else if (k < a.kin) {
+      const bool ok = r < kX3Samples && q < G4 && 4 * q + 4 <= a.kin;
+      return (m0 + (r < nvalid && ok ? r : 0)) * a.ld_src + (ok ? 4 * q : 0);
+    };
+    if (a.kin == a.K) {   // whole 16-B groups (every hidden layer): the batch's loads back to back
 #pragma unroll
-          for (int t = 0; t < 4; ++t) sv[jb][t] = k + t < a.kin ? a.src[row * a.ld_src + k + t] : 0.f;
+      for (int jb = 0; jb < PB; ++jb) sv[jb] = ld4(a.src + src_off(jb));
+      if (a.prologue == AVR_BN_GRAD) {
+#pragma unroll
+        for (int jb = 0; jb < PB; ++jb) pv[jb] = ld4(a.src_pre + src_off(jb));
+        if (a.src_res) {
+#pragma unroll
+          for (int jb = 0; jb < PB; ++jb) rv[jb] = ld4(a.src_res + src_off(jb));
         }
-        if (a.prologue == AVR_BN_GRAD && k < a.kin) {
-          pv[jb] = ld4(a.src_pre + row * a.ld_src + k);
-          if (a.src_res) rv[jb] = ld4(a.src_res + row * a.ld_src + k);
+      }
+    } else {              // lin_in's z_feature rows (in_valid < in_dim, PLAIN)
+#pragma unroll
+      for (int jb = 0; jb < PB; ++jb) {
+        const int i = b0 + jb, r = wid + NW * (i >> 1), q = lane + 64 * (i & 1);
+        sv[jb] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (r < kX3Samples && q < G4) {
+          const int64_t row = m0 + (r < nvalid ? r : 0);
+          const int k = 4 * q;
+          if (k + 4 <= a.kin) {
+            sv[jb] = ld4(a.src + row * a.ld_src + k);
+          } else if (k < a.kin) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) sv[jb][t] = k + t < a.kin ? a.src[row * a.ld_src + k + t] : 0.f;
+          }
         }
       }
     }
@@ -225,6 +241,8 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   const auto live = [&](int i) { return wid + NW * (i >> 1) < nvalid; };
   const auto row_of = [&](int i) -> int64_t { return m0 + (live(i) ? wid + NW * (i >> 1) : 0); };
   const auto col_of = [&](int i) { return 4 * (lane + 64 * (i & 1)); };
+  // an always-valid offset for pair i's row loads (past the row: column 0), so the loads need no branch
+  const auto off_of = [&](int i) -> int64_t { return row_of(i) * HID + (valid(i) ? col_of(i) : 0); };
   const auto staged = [&](int i) {
     return valid(i) ? *reinterpret_cast<const floatx4*>(lds + (wid + NW * (i >> 1)) * es + col_of(i))
                     : floatx4{0.f, 0.f, 0.f, 0.f};
@@ -236,15 +254,20 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
 #pragma unroll
     for (int i = 0; i < MAXQ; ++i)
       if (valid(i)) yv[i] += cp0[i & 1];
+    const floatx4 zero4 = floatx4{0.f, 0.f, 0.f, 0.f};
     if (a.add1) {
+      floatx4 t[MAXQ];
 #pragma unroll
-      for (int i = 0; i < MAXQ; ++i)
-        if (valid(i)) yv[i] += ld4(a.add1 + row_of(i) * HID + col_of(i));
+      for (int i = 0; i < MAXQ; ++i) t[i] = ld4(a.add1 + off_of(i));
+#pragma unroll
+      for (int i = 0; i < MAXQ; ++i) yv[i] += valid(i) ? t[i] : zero4;
     }
     if (a.add2) {
+      floatx4 t[MAXQ];
 #pragma unroll
-      for (int i = 0; i < MAXQ; ++i)
-        if (valid(i)) yv[i] += ld4(a.add2 + row_of(i) * HID + col_of(i));
+      for (int i = 0; i < MAXQ; ++i) t[i] = ld4(a.add2 + off_of(i));
+#pragma unroll
+      for (int i = 0; i < MAXQ; ++i) yv[i] += valid(i) ? t[i] : zero4;
     }
     if (a.ztab) {   // the rows' lin_z features: avr_latent_features' lookup and blend order, bit for bit
       // the points of the wave's rows first (one load each, all in flight together), then per row its corners
@@ -263,17 +286,15 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
           const float* tab = a.ztab + sc * a.ztab_stride;
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            if (valid(i + h)) {
-              const int f = col_of(i + h);
-              const floatx4 c0 = ld4(tab + (int64_t)bl.tex[0] * HID + f), c1 = ld4(tab + (int64_t)bl.tex[1] * HID + f);
-              const floatx4 c2 = ld4(tab + (int64_t)bl.tex[2] * HID + f), c3 = ld4(tab + (int64_t)bl.tex[3] * HID + f);
-              floatx4 z;
+            const int f = valid(i + h) ? col_of(i + h) : 0;
+            const floatx4 c0 = ld4(tab + (int64_t)bl.tex[0] * HID + f), c1 = ld4(tab + (int64_t)bl.tex[1] * HID + f);
+            const floatx4 c2 = ld4(tab + (int64_t)bl.tex[2] * HID + f), c3 = ld4(tab + (int64_t)bl.tex[3] * HID + f);
+            floatx4 z;
 #pragma unroll
-              for (int t = 0; t < 4; ++t)
-                z[t] = fadd(fadd(fadd(fmul(c0[t], bl.w[0]), fmul(c1[t], bl.w[1])), fmul(c2[t], bl.w[2])),
-                            fmul(c3[t], bl.w[3]));
-              yv[i + h] += z;
-            }
+            for (int t = 0; t < 4; ++t)
+              z[t] = fadd(fadd(fadd(fmul(c0[t], bl.w[0]), fmul(c1[t], bl.w[1])), fmul(c2[t], bl.w[2])),
+                          fmul(c3[t], bl.w[3]));
+            if (valid(i + h)) yv[i + h] += z;
           }
         }
       }
@@ -290,8 +311,7 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
     // forward did); the pre-BN rows also give xhat for the statistics
     floatx4 pv[MAXQ];
 #pragma unroll
-    for (int i = 0; i < MAXQ; ++i)
-      pv[i] = valid(i) ? ld4(a.pre_rows + row_of(i) * HID + col_of(i)) : floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < MAXQ; ++i) pv[i] = ld4(a.pre_rows + off_of(i));
 #pragma unroll
     for (int i = 0; i < MAXQ; ++i) {
       if (valid(i) && live(i)) {
