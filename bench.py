@@ -464,7 +464,7 @@ def run_train(args, device):
             loss = step()
         torch.cuda.synchronize()
         res[mode] = (time.perf_counter() - t0) / args.steps
-        assert bool(torch.isfinite(loss))
+        assert bool(torch.isfinite(loss)), f"{mode}: non-finite loss {float(loss)} after the timed steps"
     if args.renderer == "adaptive":
         spr = 1 + rend.n_coarse      # the marched point (coarse MLP) + the band (fine MLP); + steps latent lookups
         wl = (f"train.py defaults: {SB} scenes x {R} rays, AdaptiveVolumeRenderer (conf adaptive_renderer: "
