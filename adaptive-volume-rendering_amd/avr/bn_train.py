@@ -226,7 +226,8 @@ class _FieldTrainBN(torch.autograd.Function):
             go = grad_out.reshape(M, 4).to(F32)
             d4 = torch.cat([go[:, :3] * ((1.0 - y[:, :3]) * y[:, :3]), go[:, 3:] * (y[:, 3:] > 0)], -1).contiguous()
             Gx = torch.empty(nb + 1, M, H, device=dev, dtype=F32)      # d loss / d X[k]
-            Gx[nb] = (d4 @ P["lin_out.weight"].detach().to(F32)) * (X[nb] > 0)
+            # relu backward of lin_out's input in one pass (aten threshold_backward: g where X > 0, else 0)
+            Gx[nb] = torch.ops.aten.threshold_backward(d4 @ P["lin_out.weight"].detach().to(F32), X[nb], 0.0)
             gmax = torch.zeros(2 * nb + 2, device=dev, dtype=torch.int32)   # Gx[k] maxima (k = 0..nb), then DN's
             gmax[nb:nb + 1] = _max_bits(Gx[nb])
             DN = torch.empty(max(nb, 1), M, H, device=dev, dtype=F32)  # d loss / d fc_0 output (pre-BN)

@@ -359,8 +359,13 @@ def raymarch(view, gate_table, lstm, out_layer, ro, rd, init_dist, steps, trace=
 
 
 def _max_bits(t):
-    """max |t| as a one-element int32 device tensor of float bits (avr_weight_grads' scale input)."""
-    return t.detach().abs().amax().reshape(1).to(torch.float32).view(torch.int32)
+    """max |t| as a one-element int32 device tensor of float bits (avr_weight_grads' scale input): one
+    min / max pass over t, no |t| copy (max |t| = max(|max t|, |min t|) exactly)."""
+    t = t.detach()
+    if t.numel() == 0:
+        return torch.zeros(1, device=t.device, dtype=torch.int32)
+    mn, mx = torch.aminmax(t)
+    return torch.maximum(mx.abs(), mn.abs()).reshape(1).to(torch.float32).view(torch.int32)
 
 
 _DW_TILE = 256        # avr_weight_grads output tile (weight_grad.hip kDwTile), one workgroup per CU
