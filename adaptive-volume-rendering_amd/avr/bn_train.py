@@ -203,7 +203,7 @@ class _FieldTrainBN(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
-        from .ops import _max_bits, weight_grads
+        from .ops import _max_bits, sum_of_products, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         fused, entry, names = ctx.fused, ctx.entry, ctx.names
         X, N, amax, a_out, zfp, st1, st2, betas = ctx.keep
@@ -312,7 +312,7 @@ class _FieldTrainBN(torch.autograd.Function):
                 outs, grads_out = [], []
                 if nz > 0:
                     outs.append(feat)
-                    grads_out.append(sum(Gx[b] @ P[f"lin_z.{b}.weight"].detach() for b in range(nz)))
+                    grads_out.append(sum_of_products([(Gx[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)]))
                 if want_xyz:
                     outs.append(zft)
                     grads_out.append(Gx[0] @ P["lin_in.weight"].detach())

@@ -540,7 +540,7 @@ class _FieldTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
-        from .ops import _max_bits, latent_features, weight_grads
+        from .ops import _max_bits, latent_features, sum_of_products, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         fused, entry, names = ctx.fused, ctx.entry, ctx.names
         net = fused.net
@@ -624,7 +624,7 @@ class _FieldTrain(torch.autograd.Function):
             # the points alone (the adaptive renderer's band, fixed latent): the lookup's adjoint on HIP
             # (avr_latent_features_grad_points), the cheap z_feature path through torch autograd
             with torch.no_grad():
-                g_feat = sum(Gz[b] @ P[f"lin_z.{b}.weight"].detach() for b in range(nz)).contiguous()
+                g_feat = sum_of_products([(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)])
                 d_xyz = torch.empty(Mt, 3, device=dev, dtype=F32)
                 hwc = fused.latent_hwc_all(latent)
                 p = xyz.detach().to(F32).contiguous()
@@ -646,7 +646,7 @@ class _FieldTrain(torch.autograd.Function):
                 outs, grads_out = [], []
                 if nz > 0:
                     outs.append(feat)
-                    grads_out.append(sum(Gz[b] @ P[f"lin_z.{b}.weight"].detach() for b in range(nz)))
+                    grads_out.append(sum_of_products([(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)]))
                 if want_xyz:
                     outs.append(zft)
                     grads_out.append(G[2 * nb] @ P["lin_in.weight"].detach())

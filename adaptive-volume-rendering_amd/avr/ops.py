@@ -358,6 +358,16 @@ def raymarch(view, gate_table, lstm, out_layer, ro, rd, init_dist, steps, trace=
     return (world, fd, tr) if trace else (world, fd)
 
 
+def sum_of_products(pairs):
+    """sum_i A_i @ B_i with the accumulation inside the GEMMs (addmm_, beta = 1): no separate add passes over the
+    (rows, cols) partial products."""
+    (a0, b0), *rest = pairs
+    out = a0 @ b0
+    for a, b in rest:
+        out.addmm_(a, b)
+    return out
+
+
 def _max_bits(t):
     """max |t| as a one-element int32 device tensor of float bits (avr_weight_grads' scale input): one
     min / max pass over t, no |t| copy (max |t| = max(|max t|, |min t|) exactly)."""
