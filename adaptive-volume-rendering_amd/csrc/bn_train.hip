@@ -405,25 +405,41 @@ static int dispatch_bn_layer(int H, const BnArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ finalize
-// Stage 2: block = 4 waves over 64 columns, wave q folds rows q, q + 4, ... of the stage-1 sums, LDS meets them.
+// Stage 2: block = 16 waves over 64 columns, wave q folds rows q, q + 16, ... of the stage-1 sums (two rows in
+// flight per step), LDS meets the 16 wave sums in order (a 4-wave fold was a 40-step load-add chain, 15 µs).
+constexpr int kBnFoldWaves = 16;
+
 __device__ __forceinline__ void fold_rows(const double* __restrict__ fold, int nfold, int N, int c, double& a,
                                           double& b) {
-  __shared__ double sa[256], sb[256];
+  __shared__ double sa[64 * kBnFoldWaves], sb[64 * kBnFoldWaves];
   const int q = threadIdx.x >> 6;
-  a = 0.0; b = 0.0;
-  if (c < N)
-    for (int f = q; f < nfold; f += 4) {
-      a += fold[(int64_t)f * 2 * N + c];
-      b += fold[(int64_t)f * 2 * N + N + c];
+  double a0 = 0.0, b0 = 0.0, a1 = 0.0, b1 = 0.0;
+  if (c < N) {
+    int f = q;
+    for (; f + kBnFoldWaves < nfold; f += 2 * kBnFoldWaves) {
+      a0 += fold[(int64_t)f * 2 * N + c];
+      b0 += fold[(int64_t)f * 2 * N + N + c];
+      a1 += fold[(int64_t)(f + kBnFoldWaves) * 2 * N + c];
+      b1 += fold[(int64_t)(f + kBnFoldWaves) * 2 * N + N + c];
     }
-  sa[threadIdx.x] = a;
-  sb[threadIdx.x] = b;
+    if (f < nfold) {
+      a0 += fold[(int64_t)f * 2 * N + c];
+      b0 += fold[(int64_t)f * 2 * N + N + c];
+    }
+  }
+  sa[threadIdx.x] = a0 + a1;
+  sb[threadIdx.x] = b0 + b1;
   __syncthreads();
-  a = ((sa[threadIdx.x & 63] + sa[64 + (threadIdx.x & 63)]) + sa[128 + (threadIdx.x & 63)]) + sa[192 + (threadIdx.x & 63)];
-  b = ((sb[threadIdx.x & 63] + sb[64 + (threadIdx.x & 63)]) + sb[128 + (threadIdx.x & 63)]) + sb[192 + (threadIdx.x & 63)];
+  a = 0.0; b = 0.0;
+#pragma unroll
+  for (int w = 0; w < kBnFoldWaves; ++w) {
+    a += sa[64 * w + (threadIdx.x & 63)];
+    b += sb[64 * w + (threadIdx.x & 63)];
+  }
 }
 
-__global__ void __launch_bounds__(256) bn_stats_kernel(const double* __restrict__ fold, int nfold, int64_t M, int N,
+__global__ void __launch_bounds__(64 * kBnFoldWaves) bn_stats_kernel(const double* __restrict__ fold, int nfold,
+                                                                    int64_t M, int N,
                                                        const float* __restrict__ gamma, float eps, float momentum,
                                                        float* running_mean, float* running_var, float* mu_out,
                                                        float* invstd_out, float* scale_out) {
@@ -445,7 +461,8 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const double* __restrict_
   }
 }
 
-__global__ void __launch_bounds__(256) bn_grad_stats_kernel(const double* __restrict__ fold, int nfold, int64_t M,
+__global__ void __launch_bounds__(64 * kBnFoldWaves) bn_grad_stats_kernel(const double* __restrict__ fold, int nfold,
+                                                                         int64_t M,
                                                             int N, const float* __restrict__ gamma,
                                                             const float* __restrict__ invstd, float* coef, float* m1,
                                                             float* m2, float* dgamma, float* dbeta) {
@@ -653,7 +670,8 @@ extern "C" int avr_bn_stats(const float* partial, int64_t n_rows, int n_cols, co
   bn_fold(partial, n_rows, n_cols, true, &fold, s);
   int rc = check_launch("bn_fold_kernel");
   if (rc) return rc;
-  bn_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 256, 0, s>>>(fold, (int)bn_n_fold(n_rows), n_rows, n_cols, gamma,
+  bn_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 64 * kBnFoldWaves, 0, s>>>(fold, (int)bn_n_fold(n_rows), n_rows,
+                                                                             n_cols, gamma,
                                                                  eps, momentum, running_mean, running_var, mu, invstd,
                                                                  scale);
   return check_launch("bn_stats_kernel");
@@ -669,7 +687,8 @@ extern "C" int avr_bn_grad_stats(const float* partial, int64_t n_rows, int n_col
   bn_fold(partial, n_rows, n_cols, false, &fold, s);
   int rc = check_launch("bn_fold_kernel");
   if (rc) return rc;
-  bn_grad_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 256, 0, s>>>(fold, (int)bn_n_fold(n_rows), n_rows, n_cols,
+  bn_grad_stats_kernel<<<(unsigned)((n_cols + 63) / 64), 64 * kBnFoldWaves, 0, s>>>(fold, (int)bn_n_fold(n_rows),
+                                                                                  n_rows, n_cols,
                                                                       gamma, invstd, coef, m1, m2, dgamma, dbeta);
   return check_launch("bn_grad_stats_kernel");
 }
