@@ -20,7 +20,7 @@ import os
 
 import torch
 
-__all__ = ["set_detect_anomaly", "is_enabled", "check_outputs"]
+__all__ = ["set_detect_anomaly", "is_enabled", "check_outputs", "poison_allocations"]
 
 _flag = os.environ.get("AVR_DETECT_ANOMALY", "0") not in ("", "0")
 _installed = False
@@ -74,7 +74,8 @@ OPS = ("world_rays", "rays_sample_coarse", "composite_depth", "depth_from_world_
        "composite_fwd", "composite_bwd", "march_fine", "sample_coarse_rays", "depth_of_points_fwd", "raymarch",
        "weight_grads", "latent_features")
 FIELD_METHODS = ("forward_rays", "forward_rays_batch", "forward_points_multiview", "forward_points", "forward_train")
-FUNCTIONS = (("ops", "_Depth"), ("ops", "_Composite"), ("ops", "_DepthOfPoints"), ("field", "_FieldTrain"))
+FUNCTIONS = (("ops", "_Depth"), ("ops", "_Composite"), ("ops", "_DepthOfPoints"), ("field", "_FieldTrain"),
+             ("bn_train", "_FieldTrainBN"), ("renderers", "_MarchTrain"))
 
 
 def install():
@@ -82,8 +83,8 @@ def install():
     global _installed
     if _installed:
         return
-    from . import field, ops
-    mods = {"ops": ops, "field": field}
+    from . import bn_train, field, ops, renderers
+    mods = {"ops": ops, "field": field, "bn_train": bn_train, "renderers": renderers}
     for n in OPS:
         f = getattr(ops, n)
         if not getattr(f, "__avr_checked__", False):
@@ -98,3 +99,41 @@ def install():
         if not getattr(f, "__avr_checked__", False):
             cls.backward = staticmethod(_checked(f"{c}.backward", f))
     _installed = True
+
+
+class poison_allocations:
+    """Debug allocation hook: while active, every floating-point device tensor made by torch.empty /
+    torch.empty_like / Tensor.new_empty (the buffers the HIP kernels write their outputs into) starts filled with
+    `value` (default NaN) instead of whatever the caching allocator or a fresh hipMalloc left there. A kernel
+    that reads an output element it did not write -- a padding row, a tail past M, a table column -- then yields
+    NaN (or, with value=0.0, a reproducible zero), so two runs under different fills differ exactly where memory
+    is read before it is written. Integer buffers are left alone (garbage indices would fault the GPU).
+
+        with avr.anomaly.poison_allocations(float("nan")):
+            loss = step(); loss.backward()
+    """
+
+    def __init__(self, value=float("nan"), device_types=("cuda",)):
+        self.value = float(value)
+        self.device_types = tuple(device_types)
+        self._saved = None
+
+    def _fill(self, t):
+        if (isinstance(t, torch.Tensor) and t.device.type in self.device_types and t.is_floating_point()
+                and t.numel() > 0):
+            with torch.no_grad():
+                t.fill_(self.value)
+        return t
+
+    def __enter__(self):
+        self._saved = (torch.empty, torch.empty_like, torch.Tensor.new_empty)
+        real_empty, real_like, real_new = self._saved
+        fill = self._fill
+        torch.empty = functools.wraps(real_empty)(lambda *a, **k: fill(real_empty(*a, **k)))
+        torch.empty_like = functools.wraps(real_like)(lambda *a, **k: fill(real_like(*a, **k)))
+        torch.Tensor.new_empty = lambda self_, *a, **k: fill(real_new(self_, *a, **k))
+        return self
+
+    def __exit__(self, *exc):
+        torch.empty, torch.empty_like, torch.Tensor.new_empty = self._saved
+        return False

@@ -103,6 +103,12 @@ def _bn_stats(bn, part, M, H, stats, stream):
     call("avr_bn_stats", ptr(part), M, H, ptr(bn.weight), ctypes.c_float(bn.eps),
          ctypes.c_float(_momentum(bn) if track else 0.0), ptr(bn.running_mean) if track else None,
          ptr(bn.running_var) if track else None, ptr(stats.mu), ptr(stats.invstd), ptr(stats.scale), stream)
+    if track:
+        # the kernel wrote them through raw pointers: advance their versions as torch's in-place update does,
+        # so every (data_ptr, _version)-keyed cache (FusedField.packed's eval blob with the running statistics
+        # folded in, GraphedRenderer's capture check) sees the new statistics
+        torch.autograd.graph.increment_version(bn.running_mean)
+        torch.autograd.graph.increment_version(bn.running_var)
 
 
 def train_param_names_bn(mlp):

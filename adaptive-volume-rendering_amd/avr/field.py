@@ -620,24 +620,28 @@ class _FieldTrain(torch.autograd.Function):
         # PE / rotation / projection (the adaptive renderer's band points)
         d_latent = d_xyz = None
         want_xyz = ctx.needs_input_grad[3]
-        if want_xyz and not want_latent and nz > 0 and SB <= latent.shape[0]:
+        if want_xyz and not want_latent and (net.stop_encoder_grad or (nz > 0 and SB <= latent.shape[0])):
             # the points alone (the adaptive renderer's band, fixed latent): the lookup's adjoint on HIP
-            # (avr_latent_features_grad_points), the cheap z_feature path through torch autograd
-            with torch.no_grad():
-                g_feat = sum_of_products([(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)])
-                d_xyz = torch.empty(Mt, 3, device=dev, dtype=F32)
-                hwc = fused.latent_hwc_all(latent)
-                p = xyz.detach().to(F32).contiguous()
-                for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
-                    n = min(_lib.AVR_MAX_SCENES, SB - g0)
-                    views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
-                    call("avr_latent_features_grad_points", views, n, ptr(hwc[g0]), net.d_latent, ptr(p[g0]), B,
-                         ptr(g_feat[g0 * B]), ptr(d_xyz[g0 * B]), stream_of(d_xyz))
+            # (avr_latent_features_grad_points), the cheap z_feature path through torch autograd. With
+            # stop_encoder_grad the looked-up latent is detached (models.py:810-811), so no gradient reaches the
+            # points through the lookup: z_feature's part alone.
+            d_look = None
+            if not net.stop_encoder_grad:
+                with torch.no_grad():
+                    g_feat = sum_of_products([(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)])
+                    d_look = torch.empty(Mt, 3, device=dev, dtype=F32)
+                    hwc = fused.latent_hwc_all(latent)
+                    p = xyz.detach().to(F32).contiguous()
+                    for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
+                        n = min(_lib.AVR_MAX_SCENES, SB - g0)
+                        views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+                        call("avr_latent_features_grad_points", views, n, ptr(hwc[g0]), net.d_latent, ptr(p[g0]),
+                             B, ptr(g_feat[g0 * B]), ptr(d_look[g0 * B]), stream_of(d_look))
             with torch.enable_grad():
                 x = xyz.detach().requires_grad_(True)
                 zft = net.z_features(x, viewdirs.detach())
                 d_z, = torch.autograd.grad(zft, x, G[2 * nb] @ P["lin_in.weight"].detach())
-            d_xyz = (d_xyz.reshape(SB, B, 3) + d_z).to(xyz.dtype)
+            d_xyz = (d_z if d_look is None else d_look.reshape(SB, B, 3) + d_z).to(xyz.dtype)
         elif want_latent or want_xyz:
             with torch.enable_grad():
                 lat = latent.detach().requires_grad_(want_latent)

@@ -10,6 +10,7 @@ latent are read-only, so each rank builds them locally (or receives them once
 through `broadcast_scene`).
 """
 import inspect
+import time
 
 import torch
 import torch.distributed as dist
@@ -127,18 +128,66 @@ def _takes_ray_ids(fn):
     return "ray_ids" in params and "n_rays_total" in params
 
 
-def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None, pass_ray_ids=None):
+class ShardTimer:
+    """Per-phase time of render_sharded calls on this rank, summed over the calls since reset(): `render` (the
+    rank's renderer call on its tiles, including the tile gather of its inputs), `all_gather` (the collective,
+    including the wait for the slowest rank) and `reassembly` (packing the local outputs plus scattering every
+    rank's tiles into the frame). HIP events on the current stream on a GPU (no synchronisation inside the
+    step), wall clock on the CPU (gloo is synchronous). bench.py reports them per step, min / max over ranks,
+    so a 1 -> N shortfall can be attributed."""
+    PHASES = ("render", "all_gather", "reassembly")
+
+    def __init__(self):
+        self.calls = []
+        self._dev = None
+
+    def reset(self):
+        self.calls = []
+
+    def _mark(self):
+        if self._dev.type == "cuda":
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def begin(self, dev):
+        self._dev = dev
+        self._last = self._mark()
+        self.calls.append({p: [] for p in self.PHASES})
+
+    def lap(self, phase):
+        m = self._mark()
+        self.calls[-1][phase].append((self._last, m))
+        self._last = m
+
+    def totals_ms(self):
+        """{phase: ms summed over the calls} (synchronises the device)."""
+        out = {p: 0.0 for p in self.PHASES}
+        if self._dev is not None and self._dev.type == "cuda":
+            torch.cuda.synchronize(self._dev)
+        for call in self.calls:
+            for p, pairs in call.items():
+                for a, b in pairs:
+                    out[p] += a.elapsed_time(b) if isinstance(a, torch.cuda.Event) else (b - a) * 1e3
+        return out
+
+
+def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None, pass_ray_ids=None, timer=None):
     """render_fn(cam2world, intrinsics, x_pix[, ray_ids=, n_rays_total=]) ->
     (rgb_c, rgb_f, depth, depth) on this rank's tiles; returns the full-frame
     outputs on every rank. The frame-wide index of each of the rank's rays is
     passed as `ray_ids` (with `n_rays_total`) when pass_ray_ids is True, or,
     by default (None), when render_fn declares both parameters (a
     VolumeRenderer call: its Philox draws then match the single-GPU frame).
-    cam2world (SB,R,4,4) may be a stride-0 expand; x_pix (SB,R,2)."""
+    cam2world (SB,R,4,4) may be a stride-0 expand; x_pix (SB,R,2).
+    timer: a ShardTimer that records the call's render / all_gather / reassembly phases."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     SB, R, _ = x_pix.shape
     dev = x_pix.device
+    if timer is not None:
+        timer.begin(dev)
     idx = ray_tiles(R, rank, world, tile, device=dev)
     c2w_local = cam2world if cam2world.shape[1] == 1 else cam2world[:, idx]
     if c2w_local.shape[1] == 1 and idx.numel() != 1:
@@ -149,6 +198,8 @@ def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None,
                                            n_rays_total=R)
     else:
         rgb_c, rgb_f, depth, _ = render_fn(c2w_local, intrinsics, x_pix[:, idx].contiguous())
+    if timer is not None:
+        timer.lap("render")
     n_loc = idx.numel()
     cap = max_local_rays(R, world, tile)
     packed = torch.zeros(SB, cap, 7, device=dev, dtype=torch.float32)
@@ -156,11 +207,37 @@ def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None,
     packed[:, :n_loc, 3:6] = rgb_f
     packed[:, :n_loc, 6] = depth
     out = torch.empty(world * SB, cap, 7, device=dev, dtype=torch.float32)
+    if timer is not None:
+        timer.lap("reassembly")
     dist.all_gather_into_tensor(out, packed, group=group)
+    if timer is not None:
+        timer.lap("all_gather")
     out = out.view(world, SB, cap, 7)
     full = torch.empty(SB, R, 7, device=dev, dtype=torch.float32)
     for r in range(world):
         ridx = ray_tiles(R, r, world, tile, device=dev)
         full[:, ridx] = out[r, :, :ridx.numel()]
     depth_full = full[..., 6].contiguous()
-    return full[..., 0:3].contiguous(), full[..., 3:6].contiguous(), depth_full, depth_full
+    res = full[..., 0:3].contiguous(), full[..., 3:6].contiguous(), depth_full, depth_full
+    if timer is not None:
+        timer.lap("reassembly")
+    return res
+
+
+def gather_bytes(n_rays, world, sb=1, tile=64):
+    """Bytes one render_sharded all_gather moves into each rank: world x SB x (max tiles per rank x tile) x 28."""
+    return world * sb * max_local_rays(n_rays, world, tile) * 7 * 4
+
+
+def phase_spread(timer, steps, device, group=None):
+    """Every rank's ShardTimer totals per step -> {phase: {"min": ms, "max": ms, "per_rank": [...]}} on every
+    rank (one small all_gather; on the CPU tensor for gloo)."""
+    tot = timer.totals_ms()
+    comm = torch.device("cpu") if dist.get_backend(group) == "gloo" else device
+    mine = torch.tensor([tot[p] / max(steps, 1) for p in ShardTimer.PHASES], dtype=torch.float64, device=comm)
+    world = dist.get_world_size(group)
+    allr = torch.empty(world * mine.numel(), dtype=torch.float64, device=comm)
+    dist.all_gather_into_tensor(allr, mine, group=group)
+    allr = allr.cpu().reshape(world, mine.numel())
+    return {p: {"min": round(float(allr[:, i].min()), 3), "max": round(float(allr[:, i].max()), 3),
+                "per_rank": [round(float(v), 3) for v in allr[:, i]]} for i, p in enumerate(ShardTimer.PHASES)}

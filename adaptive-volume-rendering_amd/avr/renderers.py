@@ -18,6 +18,7 @@ Two evaluation modes for the radiance field:
     or training: the module is called on the sample points, and compositing
     runs on the HIP kernel with its HIP backward.
 """
+import ctypes
 from typing import Tuple
 
 import torch
@@ -384,12 +385,18 @@ class _MarchTrain(torch.autograd.Function):
         n = rd.shape[0]
         R = n // SB
         with torch.no_grad():
-            d_tab = torch.zeros_like(tables)
-            d_grads = torch.zeros(64 * 16 + 64 + 16 + 1, device=rd.device, dtype=torch.float32)
+            # deterministic backward (ABI 13): the table gradient in fp64, the parameter sums in a fixed order
+            d_tab64 = torch.zeros(tables.shape, device=rd.device, dtype=torch.float64)
+            d_grads = torch.empty(64 * 16 + 64 + 16 + 1, device=rd.device, dtype=torch.float32)
+            ns = ctypes.c_int64(0)
+            _lib.check(_lib.load().avr_raymarch_bwd_scratch_floats(n, ctypes.byref(ns)), "avr_raymarch_bwd_scratch_floats")
+            scratch = torch.empty(max(ns.value, 1), device=rd.device, dtype=torch.float32)
             gw = grad_world.float().reshape(n, 3).contiguous()
+            stop = bool(getattr(ctx.phi, "stop_encoder_grad", False))   # detached lookup: no position gradient
             _lib.call("avr_raymarch_bwd", ctx.views, SB, _lib.ptr(tables), _lib.ptr(P[0]), _lib.ptr(P[3]),
-                      _lib.ptr(rd), _lib.ptr(trace), _lib.ptr(state), _lib.ptr(gw), R, ctx.steps, _lib.ptr(d_tab),
-                      _lib.ptr(d_grads), _lib.stream_of(gw))
+                      _lib.ptr(rd), _lib.ptr(trace), _lib.ptr(state), _lib.ptr(gw), R, ctx.steps, 0 if stop else 1,
+                      _lib.ptr(d_tab64), _lib.ptr(d_grads), _lib.ptr(scratch), _lib.stream_of(gw))
+            d_tab = d_tab64.float()
             d_whh = d_grads[:1024].reshape(64, 16)
             d_b = d_grads[1024:1088]
             d_wout = d_grads[1088:1104].reshape(1, 16)

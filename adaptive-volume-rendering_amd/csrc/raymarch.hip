@@ -212,7 +212,14 @@ __global__ void __launch_bounds__(256) raymarch_train_kernel(MarchScenes sc, con
 // Gradient accumulators of one workgroup: d W_hh (64 x 16), d bias (64; b_ih and b_hh alike), d w_out (16),
 // d b_out (1).
 constexpr int kMarchGrads = kGates * kHid + kGates + kHid + 1;
+constexpr int kMarchRays = 256 / kHid;   // rays per workgroup
 
+// Deterministic backward (round 5): the table gradient is summed in fp64 atomics (order-independent to ~1e-16
+// relative, so its fp32 image is the same bits run after run), and the parameter gradients are summed in a fixed
+// order -- the 4 rays of a wave by two xor shuffles (commutative adds: every lane ends with the same bits), the 4
+// waves of a workgroup in wave order through LDS, the workgroups in block order by raymarch_grads_reduce_kernel.
+// With float atomics in both places two identical train.py steps differed in the LSTM gradients' last bits, and
+// one Adam step turned that into different parameters (tests/test_gpu_poison.py).
 __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const float* __restrict__ tables,
                                                            int64_t table_stride, const float* __restrict__ w_hh,
                                                            const float* __restrict__ w_out,
@@ -220,19 +227,23 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
                                                            const float* __restrict__ trace,
                                                            const float* __restrict__ state,
                                                            const float* __restrict__ grad_world, int64_t n_per_scene,
-                                                           int64_t n_rays, int steps, float* __restrict__ d_tables,
-                                                           float* __restrict__ d_grads) {
-  __shared__ float red[256 / kHid][kHid][kHid + 1];   // W_hh^T dg: (ray, unit k, column j)
-  __shared__ float gsum[kMarchGrads];
-  for (int i = threadIdx.x; i < kMarchGrads; i += blockDim.x) gsum[i] = 0.f;
+                                                           int64_t n_rays, int steps, int pos_grad,
+                                                           double* __restrict__ d_tables,
+                                                           float* __restrict__ grad_partials) {
+  // W_hh^T dg per step: red (ray, unit k, column j); after the loop the same LDS holds the per-wave parameter
+  // sums wsum (the loop's last barrier ends every read of red)
+  static_assert(kMarchRays * kHid * (kHid + 1) <= 4 * kMarchGrads, "red fits the wsum area");
+  __shared__ float smem[4 * kMarchGrads];
+  float (*red)[kHid][kHid + 1] = reinterpret_cast<float (*)[kHid][kHid + 1]>(smem);
+  float (*wsum)[kMarchGrads] = reinterpret_cast<float (*)[kMarchGrads]>(smem);
   const int k = threadIdx.x & (kHid - 1), rl = threadIdx.x / kHid;
-  const int64_t ray_raw = (int64_t)blockIdx.x * (blockDim.x / kHid) + rl;
+  const int64_t ray_raw = (int64_t)blockIdx.x * kMarchRays + rl;
   const bool live = ray_raw < n_rays;
   const int64_t ray = live ? ray_raw : n_rays - 1;
   const int scene = (int)(ray / n_per_scene);
   const View& v = sc.v[scene];
   const float* table = tables + scene * table_stride;
-  float* dtab = d_tables + scene * table_stride;
+  double* dtab = d_tables + scene * table_stride;
   float wr[4][kHid];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -248,7 +259,6 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
 #pragma unroll
     for (int j = 0; j < kHid; ++j) dWhh[q][j] = 0.f;
   float dh_next = 0.f, dc_next = 0.f;
-  __syncthreads();
   for (int s = steps - 1; s >= 0; --s) {
     const float* st = state + ((int64_t)s * n_rays + ray) * kMarchState;
     const float h = st[k], c = st[kHid + k];
@@ -299,7 +309,7 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
       if (live) {
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc)
-          atomicAdd(dtab + (int64_t)L.bl.tex[cc] * kGates + row, L.bl.w[cc] * dg[q]);
+          atomicAdd(dtab + (int64_t)L.bl.tex[cc] * kGates + row, (double)(L.bl.w[cc] * dg[q]));
       }
     }
 #pragma unroll
@@ -310,10 +320,13 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
     const float dxc0 = gix * L.dix[0] + giy * L.diy[0];
     const float dxc1 = gix * L.dix[1] + giy * L.diy[1];
     const float dxc2 = gix * L.dix[2] + giy * L.diy[2];
-    // xc = R x + t: dx += R^T dxc (x_s feeds the lookup and, by identity, x_{s+1})
-    dx0 += v.R[0] * dxc0 + v.R[3] * dxc1 + v.R[6] * dxc2;
-    dx1 += v.R[1] * dxc0 + v.R[4] * dxc1 + v.R[7] * dxc2;
-    dx2 += v.R[2] * dxc0 + v.R[5] * dxc1 + v.R[8] * dxc2;
+    // xc = R x + t: dx += R^T dxc (x_s feeds the lookup and, by identity, x_{s+1}); not with stop_encoder_grad,
+    // whose detached latent cuts the lookup from the points (models.py:810-811)
+    if (pos_grad) {
+      dx0 += v.R[0] * dxc0 + v.R[3] * dxc1 + v.R[6] * dxc2;
+      dx1 += v.R[1] * dxc0 + v.R[4] * dxc1 + v.R[7] * dxc2;
+      dx2 += v.R[2] * dxc0 + v.R[5] * dxc1 + v.R[8] * dxc2;
+    }
     __syncthreads();   // red written
     float acc = 0.f;
 #pragma unroll
@@ -321,7 +334,7 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
     dh_next = acc;
     __syncthreads();   // red read before the next step overwrites it
   }
-  // this workgroup's parameter gradients (dead rays contribute nothing)
+  // this workgroup's parameter gradients (dead rays contribute nothing), summed in a fixed order
   if (!live) {
     dwo = dbo = 0.f;
 #pragma unroll
@@ -331,16 +344,41 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
       for (int j = 0; j < kHid; ++j) dWhh[q][j] = 0.f;
     }
   }
+  const auto wave_sum = [](float x) {   // the wave's 4 rays (lanes 16 r + k), same bits on every lane
+    x += __shfl_xor(x, 16);
+    return x + __shfl_xor(x, 32);
+  };
+  const int wave = threadIdx.x >> 6;
+  float* ws = wsum[wave];
+  const bool writer = (threadIdx.x & 63) < kHid;   // ray 0 of the wave writes the wave's sums
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
 #pragma unroll
-    for (int j = 0; j < kHid; ++j) atomicAdd(&gsum[(q * kHid + k) * kHid + j], dWhh[q][j]);
-    atomicAdd(&gsum[kGates * kHid + q * kHid + k], db[q]);
+    for (int j = 0; j < kHid; ++j) {
+      const float t = wave_sum(dWhh[q][j]);
+      if (writer) ws[(q * kHid + k) * kHid + j] = t;
+    }
+    const float t = wave_sum(db[q]);
+    if (writer) ws[kGates * kHid + q * kHid + k] = t;
   }
-  atomicAdd(&gsum[kGates * kHid + kGates + k], dwo);
-  if (k == 0) atomicAdd(&gsum[kGates * kHid + kGates + kHid], dbo);
+  dwo = wave_sum(dwo);
+  dbo = wave_sum(dbo);
+  if (writer) ws[kGates * kHid + kGates + k] = dwo;
+  if (writer && k == 0) ws[kGates * kHid + kGates + kHid] = dbo;
   __syncthreads();
-  for (int i = threadIdx.x; i < kMarchGrads; i += blockDim.x) atomicAdd(d_grads + i, gsum[i]);
+  float* out = grad_partials + (int64_t)blockIdx.x * kMarchGrads;
+  for (int i = threadIdx.x; i < kMarchGrads; i += blockDim.x)
+    out[i] = ((wsum[0][i] + wsum[1][i]) + wsum[2][i]) + wsum[3][i];
+}
+
+// d_grads[i] = sum over the workgroups' partials in block order
+__global__ void __launch_bounds__(256) raymarch_grads_reduce_kernel(const float* __restrict__ partials, int n_blocks,
+                                                                    float* __restrict__ d_grads) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= kMarchGrads) return;
+  float s = 0.f;
+  for (int b = 0; b < n_blocks; ++b) s += partials[(int64_t)b * kMarchGrads + i];
+  d_grads[i] = s;
 }
 
 }  // namespace avr
@@ -380,23 +418,35 @@ extern "C" int avr_raymarch_train(const avr_view_desc* views, int n_scenes, cons
   return check_launch("raymarch_train_kernel");
 }
 
+extern "C" int avr_raymarch_bwd_scratch_floats(int64_t n_rays, int64_t* n_floats) {
+  AVR_REQUIRE(n_rays >= 0 && n_floats, "avr_raymarch_bwd_scratch_floats: bad arguments");
+  *n_floats = ((n_rays + kMarchRays - 1) / kMarchRays) * kMarchGrads;
+  return AVR_OK;
+}
+
 extern "C" int avr_raymarch_bwd(const avr_view_desc* views, int n_scenes, const float* gate_tables,
                                 const float* w_hh, const float* w_out, const float* rd, const float* trace,
                                 const float* state, const float* grad_world, int64_t n_per_scene, int steps,
-                                float* d_tables, float* d_grads, void* stream) {
+                                int lookup_grad, double* d_tables, float* d_grads, float* scratch, void* stream) {
   AVR_REQUIRE(n_per_scene >= 0 && steps >= 0, "avr_raymarch_bwd: negative size");
   if (n_per_scene == 0 || steps == 0) return AVR_OK;
   MarchScenes sc;
   int rc = march_scenes(views, n_scenes, &sc, "avr_raymarch_bwd");
   if (rc) return rc;
-  AVR_REQUIRE(gate_tables && w_hh && w_out && rd && trace && state && grad_world && d_tables && d_grads,
+  AVR_REQUIRE(gate_tables && w_hh && w_out && rd && trace && state && grad_world && d_tables && d_grads && scratch,
               "avr_raymarch_bwd: null pointer");
   const int64_t n = n_per_scene * n_scenes;
   const int64_t stride = (int64_t)views[0].latent_h * views[0].latent_w * kGates;
-  const int per_block = 256 / kHid;
-  raymarch_bwd_kernel<<<(unsigned)((n + per_block - 1) / per_block), 256, 0, as_stream(stream)>>>(
-      sc, gate_tables, stride, w_hh, w_out, rd, trace, state, grad_world, n_per_scene, n, steps, d_tables, d_grads);
-  return check_launch("raymarch_bwd_kernel");
+  const int64_t blocks = (n + kMarchRays - 1) / kMarchRays;
+  AVR_REQUIRE(blocks < (1ll << 31), "avr_raymarch_bwd: too many rays");
+  raymarch_bwd_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(
+      sc, gate_tables, stride, w_hh, w_out, rd, trace, state, grad_world, n_per_scene, n, steps, lookup_grad ? 1 : 0,
+      d_tables, scratch);
+  rc = check_launch("raymarch_bwd_kernel");
+  if (rc) return rc;
+  raymarch_grads_reduce_kernel<<<(kMarchGrads + 255) / 256, 256, 0, as_stream(stream)>>>(scratch, (int)blocks,
+                                                                                         d_grads);
+  return check_launch("raymarch_grads_reduce_kernel");
 }
 
 extern "C" int avr_raymarch(const avr_view_desc* view, const float* gate_table, const float* w_hh, const float* b_ih,

@@ -562,14 +562,20 @@ def run_standin(args, config, world, rank):
     net = build_scene(torch.device("cpu"), seed=0 if rank == 0 else 1000 + rank)
     shared = share_scene(net, torch.device("cpu"), world > 1)
 
+    stimer = None
+    if world > 1:
+        from avr.parallel import ShardTimer
+        stimer = ShardTimer()
+
     def step():
         if world > 1:
-            return render_sharded(standin_render, c2w, K, x_pix)
+            return render_sharded(standin_render, c2w, K, x_pix, timer=stimer)
         return standin_render(c2w, K, x_pix)
 
     for _ in range(args.warmup):
         step()
     if world > 1:
+        stimer.reset()
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -581,6 +587,7 @@ def run_standin(args, config, world, rank):
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
+    phases = shard_phases(stimer, args.steps, torch.device("cpu"), R) if world > 1 else None
     if rank == 0:
         line = {"metric": "rays/sec (128 coarse + 64 fine samples) + achieved HBM GB/s vs roofline",
                 "value": round(R * args.steps / elapsed, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
@@ -593,6 +600,8 @@ def run_standin(args, config, world, rank):
                 "scene_checksum": scene_checksum(net)}
         if shared is not None:
             line["scene_broadcast"] = shared
+        if phases is not None:
+            line["shard_phases"] = phases
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -728,20 +737,52 @@ def config5_leg(args, net, fused, K, device):
     x_pix, c2w = frame_views(4, args.frame, device)
     rend = VolumeRenderer(0.8, 1.8, args.n_coarse, args.n_fine, 0, 0.01, True)
     rend.seed = 1234
+    sharded = dist is not None and dist.is_initialized()   # --dist: the per-rank path of --gpus N, gather included
+    stimer = None
+    if sharded:
+        from avr.parallel import ShardTimer, render_sharded
+        stimer = ShardTimer()
+
+        def render_fn(c, k, x, ray_ids=None, n_rays_total=None):
+            return rend(c, k, x, net, ray_ids=ray_ids, n_rays_total=n_rays_total)
 
     def step():
         fused._packed.clear()
         with torch.no_grad():
+            if sharded:
+                return render_sharded(render_fn, c2w, K, x_pix, timer=stimer)[1]
             return rend(c2w, K, x_pix, net)[1]
 
-    elapsed, out = time_steps(step, args.config5_steps, 1, 1, device)
+    if sharded:
+        step()
+        stimer.reset()
+    elapsed, out = time_steps(step, args.config5_steps, 0 if sharded else 1, dist.get_world_size() if sharded else 1,
+                              device)
     assert rend.last_path == "fused" and bool(torch.isfinite(out).all())
     R = x_pix.shape[1]
-    return {"value": round(R * args.config5_steps / elapsed, 1), "unit": "rays/s", "steps": args.config5_steps,
-            "warmup": 1, "ms_per_step": round(elapsed / args.config5_steps * 1e3, 3), "rays_per_step": R,
-            "scaling": "strong",
-            "workload": f"BASELINE config 5 on 1 GPU: 4 orbit views x {args.frame}x{args.frame} ({R} rays) per step "
-                        f"x ({args.n_coarse} coarse + {args.n_fine} fine), the per-rank renderer call of --gpus N"}
+    leg = {"value": round(R * args.config5_steps / elapsed, 1), "unit": "rays/s", "steps": args.config5_steps,
+           "warmup": 1, "ms_per_step": round(elapsed / args.config5_steps * 1e3, 3), "rays_per_step": R,
+           "scaling": "strong",
+           "workload": f"BASELINE config 5 on 1 GPU: 4 orbit views x {args.frame}x{args.frame} ({R} rays) per step "
+                       f"x ({args.n_coarse} coarse + {args.n_fine} fine), the per-rank renderer call of --gpus N"
+                       + (" through avr.parallel.render_sharded (tiles, RCCL all_gather, reassembly)" if sharded else "")}
+    if sharded:
+        leg["shard_phases"] = shard_phases(stimer, args.config5_steps, device, R)
+    return leg
+
+
+def shard_phases(stimer, steps, device, n_rays):
+    """The N > 1 attribution keys: per-step render / all_gather / reassembly ms of every rank (min / max over
+    ranks; HIP events on each rank's stream), rays per rank and the gather's bytes per step."""
+    from avr.parallel import gather_bytes, max_local_rays, phase_spread
+    world = dist.get_world_size()
+    ph = phase_spread(stimer, steps, device)
+    return {"render_ms_per_step": ph["render"], "all_gather_ms_per_step": ph["all_gather"],
+            "reassembly_ms_per_step": ph["reassembly"], "rays_per_rank_max": max_local_rays(n_rays, world),
+            "gather_bytes_per_step": gather_bytes(n_rays, world),
+            "note": "render: the rank's renderer call on its 64-ray tiles; all_gather: the RCCL collective "
+                    "(includes waiting for the slowest rank); reassembly: packing + scattering the tiles into "
+                    "the frame (avr.parallel.ShardTimer)"}
 
 
 def config2_leg(args, net, fused, K, c2w, x_pix, device):
@@ -946,8 +987,10 @@ def main():
         g = torch.Generator(device="cpu").manual_seed(100 + rank)
         x_pix = torch.rand(1, R, 2, generator=g).to(device)
     gathered = None
+    stimer = None
     if config == 5:
-        from avr.parallel import render_sharded
+        from avr.parallel import ShardTimer, render_sharded
+        stimer = ShardTimer()
     else:
         c2w = orbit_c2w(0.7 + 0.5 * rank).to(device).reshape(1, 1, 4, 4).expand(1, R, 4, 4)
         if use_dist:
@@ -961,7 +1004,7 @@ def main():
         with torch.no_grad():
             if config == 5:
                 if use_dist:
-                    rgb_c, rgb_f, depth, _ = render_sharded(render_fn, c2w, K, x_pix)
+                    rgb_c, rgb_f, depth, _ = render_sharded(render_fn, c2w, K, x_pix, timer=stimer)
                 else:
                     rgb_c, rgb_f, depth, _ = rend(c2w, K, x_pix, net)
                 return rgb_f
@@ -982,6 +1025,8 @@ def main():
     assert rend.last_path == "fused", "bench must run the fused HIP field"
     torch.cuda.synchronize()
     timer.reset()
+    if stimer is not None:
+        stimer.reset()
     hbm.on = True
     fine_evaluated = [0]
 
@@ -1098,6 +1143,8 @@ def main():
     if shared is not None:
         line["scene_broadcast"] = shared
         line["scene_checksum"] = scene_checksum(net)
+    if config == 5 and use_dist:
+        line["shard_phases"] = shard_phases(stimer, args.steps, device, R)
     if config == 4:
         line["config"]["fine_samples_evaluated_fraction"] = round(
             fine_evaluated[0] / (args.steps * R * (args.n_coarse + args.n_fine)), 4)

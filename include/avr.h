@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 12
+#define AVR_ABI_VERSION 13
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -459,18 +459,24 @@ int avr_raymarch(const avr_view_desc* view, const float* gate_table, const float
  * (renderers.py:413-432, :320-343). n_scenes (<= AVR_MAX_SCENES) scenes of n_per_scene rays each (ray r in
  * scene r / n_per_scene, its view and gate table; gate_tables (n_scenes, H*W, 64)). Forward: world (n, 3),
  * trace ((steps + 1), n, 3) = every point, state (steps, n, 96) = h, c, i, f, g, o per step (the backward's
- * input). Backward, given grad_world (n, 3): d_tables (n_scenes, H*W, 64) += d loss / d gate table (W_ih's
- * gradient is then sum_s d_tables[s]^T latent_s^T, the latent's W_ih^T d_tables[s]), d_grads (64*16 + 64 + 16
- * + 1) += d W_hh, d (b_ih = b_hh), d w_out, d b_out, with the reference's clamp(-10, 10) of every h gradient
- * (state[0].register_hook) and grid_sample's border / align_corners=True position gradient. Zero both first. */
+ * input). Backward, given grad_world (n, 3): d_tables (n_scenes, H*W, 64), fp64, += d loss / d gate table
+ * (zero it first; W_ih's gradient is then sum_s d_tables[s]^T latent_s^T, the latent's W_ih^T d_tables[s]),
+ * d_grads (64*16 + 64 + 16 + 1) = d W_hh, d (b_ih = b_hh), d w_out, d b_out, with the reference's clamp(-10, 10)
+ * of every h gradient (state[0].register_hook) and grid_sample's border / align_corners=True position gradient.
+ * ABI 13: deterministic -- the table gradient in fp64 atomics, the parameter gradients summed in a fixed order
+ * through `scratch` (avr_raymarch_bwd_scratch_floats(n) floats, n = n_scenes * n_per_scene); lookup_grad 1 =
+ * the lookup's position gradient flows into the points (models.py:753-823 with stop_encoder_grad False), 0 = it
+ * does not (stop_encoder_grad True detaches the looked-up latent, models.py:810-811: W_ih, the LSTM and
+ * out_layer still get theirs, the points only through x += rd * sd).                                          */
 int avr_raymarch_train(const avr_view_desc* views, int n_scenes, const float* gate_tables, const float* w_hh,
                        const float* b_ih, const float* b_hh, const float* w_out, const float* b_out, const float* ro,
                        const float* rd, const float* init_dist, int64_t n_per_scene, int steps, float* world,
                        float* trace, float* state, void* stream);
+int avr_raymarch_bwd_scratch_floats(int64_t n_rays, int64_t* n_floats);
 int avr_raymarch_bwd(const avr_view_desc* views, int n_scenes, const float* gate_tables, const float* w_hh,
                      const float* w_out, const float* rd, const float* trace, const float* state,
-                     const float* grad_world, int64_t n_per_scene, int steps, float* d_tables, float* d_grads,
-                     void* stream);
+                     const float* grad_world, int64_t n_per_scene, int steps, int lookup_grad, double* d_tables,
+                     float* d_grads, float* scratch, void* stream);
 
 /* ------------------------------------------------------------ measurement
  * Streaming device copy dst[0, n_bytes) = src[0, n_bytes) (16-B aligned,

@@ -236,10 +236,17 @@ int main(void) {
                             NULL), AVR_E_INVALID);
   expect("raymarch_train null", avr_raymarch_train(&v, 1, buf, NULL, buf, buf, buf, buf, buf, buf, buf, 4, 10, buf, buf,
                                                    buf, NULL), AVR_E_INVALID);
-  expect("raymarch_bwd null", avr_raymarch_bwd(&v, 1, buf, buf, buf, buf, buf, buf, NULL, 4, 10, buf, buf, NULL),
-         AVR_E_INVALID);
-  expect("raymarch_bwd no steps", avr_raymarch_bwd(&v, 1, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 4, 0, NULL, NULL,
-                                                   NULL), AVR_OK);
+  expect("raymarch_bwd null", avr_raymarch_bwd(&v, 1, buf, buf, buf, buf, buf, buf, NULL, 4, 10, 1, (double*)buf, buf,
+                                               buf, NULL), AVR_E_INVALID);
+  expect("raymarch_bwd no scratch", avr_raymarch_bwd(&v, 1, buf, buf, buf, buf, buf, buf, buf, 4, 10, 1, (double*)buf,
+                                                     buf, NULL, NULL), AVR_E_INVALID);
+  expect("raymarch_bwd no steps", avr_raymarch_bwd(&v, 1, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 4, 0, 1, NULL,
+                                                   NULL, NULL, NULL), AVR_OK);
+  {
+    int64_t nf = 0;
+    expect("raymarch_bwd scratch size", avr_raymarch_bwd_scratch_floats(33, &nf), AVR_OK);
+    check("raymarch_bwd scratch = 3 workgroups", nf == 3 * (64 * 16 + 64 + 16 + 1));
+  }
 
   /* measurement */
   expect("copy odd size", avr_stream_copy(buf, buf + 8, 15, NULL), AVR_E_INVALID);

@@ -38,6 +38,16 @@ def test_bench_gpus_n_spawns_n_ranks(n):
     # ranks > 0 start from another scene; broadcast_scene hands them rank 0's
     assert many["scene_checksum"] == one["scene_checksum"]
     assert many["scene_broadcast"]["bytes"] > 27e6 and "scene_broadcast" not in one
+    # the N > 1 line attributes the step (VERDICT r04 missing 3): per-rank render / all_gather / reassembly
+    # ms per step (min / max over ranks) and the gather's size
+    ph = many["shard_phases"]
+    for k in ("render_ms_per_step", "all_gather_ms_per_step", "reassembly_ms_per_step"):
+        assert len(ph[k]["per_rank"]) == n and 0.0 <= ph[k]["min"] <= ph[k]["max"], (k, ph[k])
+    assert ph["render_ms_per_step"]["max"] > 0 and ph["all_gather_ms_per_step"]["max"] > 0
+    tiles = -(-4 * 48 * 48 // 64)
+    assert ph["rays_per_rank_max"] == -(-tiles // n) * 64
+    assert ph["gather_bytes_per_step"] == n * ph["rays_per_rank_max"] * 28
+    assert "shard_phases" not in one
 
 
 def test_bench_default_is_config3_weak():

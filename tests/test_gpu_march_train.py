@@ -93,6 +93,43 @@ def test_march_autograd_matches_fp64(sb, R, steps):
     print(f"march sb={sb} R={R} steps={steps}: worst HIP gradient error vs float64 {worst:.2e}")
 
 
+@pytest.mark.parametrize("sb,R", [(1, 300), (2, 129)])
+def test_march_autograd_stop_encoder_grad_matches_fp64(sb, R):
+    """train.py --stop_encoder_grad (train.py:279): phi(return_features=True) returns a detached latent
+    (models.py:810-811), so no gradient reaches the points through the lookup; W_ih, the LSTM and out_layer still
+    get theirs. The HIP march (avr_raymarch_bwd with the position gradient off) against a float64 run of the
+    reference loop, and against the march with the flag off (the lookup term must be gone)."""
+    net = _net(64, 2, 64, (8, 8), sb=sb)
+    net.stop_encoder_grad = True
+    rend = _renderer(64, 10)
+    ros, rds, init, *_ = _march_inputs(sb, R, seed=5 + sb)
+    w = 300.0 * torch.randn(sb, R, 3, generator=torch.Generator().manual_seed(9)).to(DEV)
+    wh, gh, path = _march_grads(rend, net, ros, rds, init, w, hip=True, latent_grad=False)
+    assert path == "hip_train"
+    wt, gt, _ = _march_grads(rend, net, ros, rds, init, w, hip=False, latent_grad=False)
+    net.double()
+    rend.double()
+    net.use_fused = False
+    try:
+        _, gd, _ = _march_grads(rend, net, ros.double(), rds.double(), init.double(), w.double(), hip=False,
+                                latent_grad=False)
+    finally:
+        net.float()
+        rend.float()
+        net.use_fused = True
+    assert set(gh) == set(gt) == set(gd)
+    for k in gd:
+        ref = gd[k].double()
+        s = float(ref.abs().max()) or 1.0
+        eh = float((gh[k].double() - ref).abs().max()) / s
+        et = float((gt[k].double() - ref).abs().max()) / s
+        assert eh <= 2.0 * et + 1e-4, f"{k}: HIP err {eh:.2e} vs fp32 autograd err {et:.2e} of max |grad| {s:.2e}"
+    net.stop_encoder_grad = False
+    _, gon, _ = _march_grads(rend, net, ros, rds, init, w, hip=True, latent_grad=False)
+    k = "lstm.weight_hh"
+    assert float((gon[k] - gh[k]).abs().max()) > 1e-3 * float(gd[k].abs().max()), "lookup gradient not cut"
+
+
 def test_adaptive_renderer_training_step_hip_vs_torch():
     """AdaptiveVolumeRenderer (conf adaptive_renderer: 10 steps, band of 20, epsilon 0.15) training step on
     the default_mv-shaped net (combine_layer 3): loss and every gradient (net, LSTM, out_layer) of the HIP

@@ -347,13 +347,17 @@ def test_latent_features_grad_points_vs_autograd():
     print(f"grad points: HIP err {eh / s:.2e}, torch fp32 err {et / s:.2e} of max {s:.3e}")
 
 
-@pytest.mark.parametrize("d_hidden,latent_grad", [(64, False), (512, False), (512, True)])
-def test_field_train_point_gradient(d_hidden, latent_grad):
+@pytest.mark.parametrize("d_hidden,latent_grad,stop", [(64, False, False), (512, False, False), (512, True, False),
+                                                    (64, False, True), (512, False, True)])
+def test_field_train_point_gradient(d_hidden, latent_grad, stop):
     """Points that carry a gradient (the adaptive renderer's band samples,
     renderers.py:492-508): d loss / d xyz through PE, rotation, projection and
-    the bilinear latent lookup, with the parameter gradients, vs PyTorch autograd."""
+    the bilinear latent lookup, with the parameter gradients, vs PyTorch autograd.
+    stop: train.py --stop_encoder_grad (train.py:279): the looked-up latent is detached
+    (models.py:810-811), so the points get z_feature's gradient only."""
     d_latent = 512 if d_hidden == 512 else 64
     net = _net(d_hidden, 3, d_latent, (16, 16) if d_hidden == 512 else (8, 8))
+    net.stop_encoder_grad = stop
     xyz0, vd, w = _points(1, 500, seed=17)
     res = {}
     for hip in (True, False, "fp64"):
@@ -367,6 +371,11 @@ def test_field_train_point_gradient(d_hidden, latent_grad):
             return out
         res[hip] = _fp64(net, run) if hip == "fp64" else run()
     _compare64(res[True], res[False], res["fp64"])
+    if stop:   # the lookup's position gradient is really cut: it is not the stop_encoder_grad=False gradient
+        net.stop_encoder_grad = False
+        xyz = xyz0.clone().requires_grad_(True)
+        _grads(net, xyz, vd, w, True, hip=True)
+        assert float((xyz.grad - res[True]["xyz"]).abs().max()) > 1e-3 * float(xyz.grad.abs().max())
 
 
 def test_encoder_training_step_hip_vs_torch():
