@@ -159,7 +159,12 @@ __global__ void __launch_bounds__(256) latent_features_grad_points_kernel(LatBat
     const float gw = sy * (0.5f * (float)(v.H - 1)) * myk * v.scale[1];
     const float a0 = gu * v.focal[0], a1 = gw * v.focal[1];
     const float inv_z = 1.0f / xc2;
-    const float d0 = -a0 * inv_z, d1 = -a1 * inv_z, d2 = (a0 * xc0 + a1 * xc1) * inv_z * inv_z;
+    // a clipped coordinate passes exactly zero: at a point on the source camera's plane (xc2 = 0: the lookup
+    // is clipped, 1 / xc2 = inf) the chain would otherwise give 0 * inf = NaN (torch's autograd does: the
+    // r04q adaptive train step hit a band point at world z = -1.3f, camera z 0, profiles/r05d_*)
+    const float num = a0 * xc0 + a1 * xc1;
+    const float d0 = a0 != 0.f ? -a0 * inv_z : 0.f, d1 = a1 != 0.f ? -a1 * inv_z : 0.f;
+    const float d2 = num != 0.f ? num * inv_z * inv_z : 0.f;
 #pragma unroll
     for (int j = 0; j < 3; ++j) gxyz[3 * row + j] = v.R[j] * d0 + v.R[3 + j] * d1 + v.R[6 + j] * d2;
   }

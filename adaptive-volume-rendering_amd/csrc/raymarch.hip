@@ -133,9 +133,11 @@ __device__ __forceinline__ LookupGrad lookup_grad(const View& v, float x0, float
   const bool cx = ixr > 0.f && ixr < (float)(v.W - 1), cy = iyr > 0.f && iyr < (float)(v.H - 1);
   const float ax = cx ? 0.5f * (float)(v.W - 1) * v.scale[0] * v.focal[0] : 0.f;
   const float ay = cy ? 0.5f * (float)(v.H - 1) * v.scale[1] * v.focal[1] : 0.f;
+  // a clipped coordinate (ax / ay = 0) passes exactly zero, also where 1 / xc2 is infinite (a point on the
+  // source camera's plane: 0 * inf would be NaN)
   const float iz = 1.0f / xc2;
-  L.dix[0] = -ax * iz; L.dix[1] = 0.f; L.dix[2] = ax * xc0 * iz * iz;
-  L.diy[0] = 0.f; L.diy[1] = -ay * iz; L.diy[2] = ay * xc1 * iz * iz;
+  L.dix[0] = ax != 0.f ? -ax * iz : 0.f; L.dix[1] = 0.f; L.dix[2] = ax != 0.f ? ax * xc0 * iz * iz : 0.f;
+  L.diy[0] = 0.f; L.diy[1] = ay != 0.f ? -ay * iz : 0.f; L.diy[2] = ay != 0.f ? ay * xc1 * iz * iz : 0.f;
   return L;
 }
 
@@ -270,7 +272,9 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
     dwo += dsd * h;
     dbo += dsd;
     float dh = wo * dsd + dh_next;
-    dh = fminf(fmaxf(dh, -10.f), 10.f);               // state[0].register_hook(clamp(-10, 10))
+    // state[0].register_hook(clamp(-10, 10)); a NaN stays NaN, as torch.clamp keeps it (fminf / fmaxf alone
+    // would turn it into -10 and hide it from the LSTM's gradients)
+    dh = dh != dh ? dh : fminf(fmaxf(dh, -10.f), 10.f);
     const float tc = tanhf(c);
     const float dc = dh * og * (1.f - tc * tc) + dc_next;
     float dg[4];

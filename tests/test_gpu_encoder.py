@@ -7,9 +7,10 @@ tensors to the reference's utils (g8_batching.npz).
 
 The encoder's bar is MIOpen against the CPU's convolutions, not a fixed number: a float64 encode on the CPU
 (same weights) is the exact result; the reference's fp32 CPU output (g7) sits some distance e_cpu from it, and
-the device output must sit within 8 e_cpu of it (convolution algorithms -- implicit GEMM, Winograd, direct --
-order a 4 608-term dot product differently; 8x leaves room for a Winograd transform's extra rounding), with the
-test run under train.py's defaults (no TF32 switches touched)."""
+the device output must sit within 2 e_cpu of it (convolution algorithms order a 4 608-term dot product
+differently; measured on the MI355X: 4.16e-5 vs the CPU's 3.97e-5 at nl4, 5.34e-6 vs 4.98e-6 at nl3,
+profiles/r05a_pytest_poison_encoder_train.log), with the test run under train.py's defaults (no TF32 switches
+touched)."""
 import numpy as np
 import pytest
 import torch
@@ -53,7 +54,7 @@ def test_encode_on_device_matches_reference(golden, tag):
     e_g7 = float(np.abs(sub - ref32).max())
     print(f"encode {tag}: device vs fp64 {e_dev:.2e}, reference CPU fp32 vs fp64 {e_cpu:.2e}, device vs g7 {e_g7:.2e} "
           f"(max |latent| {scale:.3f})")
-    assert e_dev <= 8.0 * e_cpu + 1e-7 * scale, (e_dev, e_cpu)
+    assert e_dev <= 2.0 * e_cpu + 1e-7 * scale, (e_dev, e_cpu)
     full = lat.double().sum().item()
     assert abs(full - float(g[f"{tag}_latent_sum"])) <= 1e-5 * float(lat.abs().sum())
     # the scene-side outputs of encode() are exact copies / fp32 arithmetic on a few values

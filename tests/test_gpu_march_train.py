@@ -130,6 +130,30 @@ def test_march_autograd_stop_encoder_grad_matches_fp64(sb, R):
     assert float((gon[k] - gh[k]).abs().max()) > 1e-3 * float(gd[k].abs().max()), "lookup gradient not cut"
 
 
+def test_march_backward_on_source_camera_plane_is_finite():
+    """Rays that run inside the source camera's plane (every march point at camera z = 0: the lookup is clipped,
+    1 / z infinite) get finite gradients: the clipped lookup passes exactly zero (avr_raymarch_bwd's lookup_grad),
+    as avr_latent_features_grad_points does (test_gpu_train.py); a NaN would reach out_layer and the LSTM."""
+    sb, R = 1, 64
+    net = _net(64, 2, 64, (8, 8), sb=sb)
+    rend = _renderer(64, 4)
+    tz = float(net.poses[0, 2, 3])
+    g = torch.Generator().manual_seed(3)
+    ros = torch.zeros(sb, R, 3)
+    ros[..., 0] = torch.rand(sb, R, generator=g) - 0.5
+    ros[..., 1] = torch.rand(sb, R, generator=g) - 0.5
+    ros[..., 2] = -tz                                                    # world z = -t_z: camera z = 0 (R = I)
+    ang = torch.rand(sb, R, generator=g) * 6.28
+    rds = torch.stack([torch.cos(ang), torch.sin(ang), torch.zeros_like(ang)], -1)   # inside the plane
+    init = 0.8 + 0.05 * torch.randn(sb, R, 1, generator=g)
+    w = torch.randn(sb, R, 3, generator=g).to(DEV)
+    world, grads, path = _march_grads(rend, net, ros.to(DEV), rds.to(DEV), init.to(DEV), w, hip=True)
+    assert path == "hip_train"
+    assert bool(torch.isfinite(world).all())
+    bad = [k for k, v in grads.items() if not bool(torch.isfinite(v).all())]
+    assert not bad, bad
+
+
 def test_adaptive_renderer_training_step_hip_vs_torch():
     """AdaptiveVolumeRenderer (conf adaptive_renderer: 10 steps, band of 20, epsilon 0.15) training step on
     the default_mv-shaped net (combine_layer 3): loss and every gradient (net, LSTM, out_layer) of the HIP

@@ -347,6 +347,37 @@ def test_latent_features_grad_points_vs_autograd():
     print(f"grad points: HIP err {eh / s:.2e}, torch fp32 err {et / s:.2e} of max {s:.3e}")
 
 
+def test_latent_features_grad_points_on_source_camera_plane():
+    """A point on the source camera's plane (camera z = 0: the projection is infinite, the lookup clipped to the
+    border) gets exactly the clip's zero position gradient from the lookup, not 0 * inf = NaN. The r04q adaptive
+    train.py bench run failed on one such band point (world z = -1.3f with the source camera at z = -1.3;
+    profiles/r05d_adaptive_nan_probe.log); torch's autograd of the reference lookup gives NaN there."""
+    from avr import _lib
+    from avr._lib import ViewDesc
+    net = _net(64, 2, 64, (8, 8), sb=2)
+    xyz, vd, _ = _points(2, 256, seed=23)
+    plane = torch.arange(256, device=DEV) % 2 == 0                       # every other point on the plane
+    tz = net.poses[:, 2, 3].reshape(2, 1)                                # R = I: camera z = world z + t_z
+    xyz[..., 2] = torch.where(plane, -tz, xyz[..., 2])
+    assert bool((xyz[..., 2][:, plane] + tz == 0).all())
+    gfeat = torch.randn(2 * 256, 64, generator=torch.Generator().manual_seed(6)).to(DEV)
+    fused = net.fused()
+    hwc = fused.latent_hwc_all(net.encoder.latent)
+    views = (ViewDesc * 2)(*[fused.view(sb) for sb in range(2)])
+    got = torch.empty(2 * 256, 3, device=DEV)
+    _lib.call("avr_latent_features_grad_points", views, 2, _lib.ptr(hwc), 64, _lib.ptr(xyz.contiguous()), 256,
+              _lib.ptr(gfeat), _lib.ptr(got), _lib.stream_of(got))
+    got = got.reshape(2, 256, 3)
+    assert bool(torch.isfinite(got).all())
+    assert bool((got[:, plane] == 0).all())
+    x = xyz.clone().requires_grad_(True)
+    feat, _ = net.mlp_inputs(x, vd)
+    ref = torch.autograd.grad(feat, x, gfeat)[0]
+    assert not bool(torch.isfinite(ref[:, plane]).all())                 # the reference's autograd: 0 * inf
+    np.testing.assert_allclose(got[:, ~plane].cpu().numpy(), ref[:, ~plane].cpu().numpy(), rtol=1e-4,
+                               atol=1e-5 * float(ref[:, ~plane].abs().max()))
+
+
 @pytest.mark.parametrize("d_hidden,latent_grad,stop", [(64, False, False), (512, False, False), (512, True, False),
                                                     (64, False, True), (512, False, True)])
 def test_field_train_point_gradient(d_hidden, latent_grad, stop):

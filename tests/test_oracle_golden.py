@@ -165,3 +165,18 @@ def test_torch_port_matches_oracle(golden):
     np.testing.assert_allclose(rgb_c.numpy(), o_c, atol=1e-4, rtol=0)
     ok = (np.abs(rgb_f.numpy() - o_f).max(-1) <= 1e-4) & (np.abs(depth.numpy() - o_d) <= 1e-4)
     assert ok.mean() >= 0.98, ok.mean()      # a fine bin may flip at an exact cdf tie between fp paths
+
+
+@pytest.mark.parametrize("tag", ["small", "full", "mv512", "d256"])
+def test_field64_against_reference(golden, tag):
+    """oracle/field64.py (the float64 restatement the C3 field error is attributed against) agrees with the
+    reference's own fp32 forward (g4) to within that forward's fp32 rounding, and with the fp32 oracle."""
+    from oracle.field64 import field64
+    g = golden(f"g4_field_{tag}.npz")
+    pc, pf, latent = synth.field_from_meta(g)
+    for p, key in ((pc, "out_coarse"), (pf, "out_fine")):
+        out = field64(p, latent.reshape(latent.shape[-3:]), g["poses"].reshape(3, 4), g["focal"], g["c"],
+                      g["image_shape"], g["latent_scaling"], g["xyz"].reshape(-1, 3), g["viewdirs"].reshape(-1, 3),
+                      n_blocks=int(g["n_blocks"]), combine_layer=int(g["combine_layer"]))
+        ref = g[key].reshape(-1, 4).astype(np.float64)
+        np.testing.assert_allclose(out, ref, atol=1e-4, rtol=1e-4)
