@@ -295,7 +295,17 @@ class NewPixelNeRFNet(nn.Module):
         if not return_features and self.can_train_bn(xyz, viewdirs):
             from .bn_train import forward_train_bn
             return forward_train_bn(self.fused(), xyz, viewdirs, coarse)
+        if not return_features and self.can_train_layers(xyz, viewdirs):
+            from .layer_train import forward_train_layers
+            return forward_train_layers(self.fused(), xyz, viewdirs, coarse)
         return self.forward_torch(xyz, coarse, viewdirs, far, return_features)
+
+    def can_train_layers(self, xyz, viewdirs):
+        """use_spade and / or NS > 1 source views with autograd: the layer-by-layer HIP path (avr.layer_train);
+        view directions must not need gradients."""
+        from .layer_train import layer_train_eligible
+        return (self.use_fused and self.hip_backward and xyz.is_cuda and torch.is_grad_enabled()
+                and viewdirs is not None and not viewdirs.requires_grad and layer_train_eligible(self))
 
     def can_train_bn(self, xyz, viewdirs):
         """train.py --bn in training mode (batch statistics): the layer-by-layer HIP path (avr.bn_train), with

@@ -565,8 +565,10 @@ extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* 
   int rc = field_layout(dims, &L);
   if (rc) return rc;
   AVR_REQUIRE(l, "avr_bn_layer_run: null layer");
-  AVR_REQUIRE(dims->precision == AVR_FIELD_X3 && !dims->bn && !dims->spade && !(dims->beta > 0.f),
-              "avr_bn_layer_run: an x3 blob packed without eval-BN folding (dims->bn = 0), ReLU, no use_spade");
+  // use_spade blobs too (ABI 13: avr.layer_train runs spade / NS > 1 nets layer by layer; the layer reads only
+  // lin_in / fc_0 / fc_1 fragments and the header, whose offsets the layout computes for either)
+  AVR_REQUIRE(dims->precision == AVR_FIELD_X3 && !dims->bn && !(dims->beta > 0.f),
+              "avr_bn_layer_run: an x3 blob packed without eval-BN folding (dims->bn = 0), ReLU");
   AVR_REQUIRE(l->mode == AVR_BN_FWD || l->mode == AVR_BN_BWD, "avr_bn_layer_run: bad mode %d", l->mode);
   AVR_REQUIRE(l->prologue >= AVR_BN_PLAIN && l->prologue <= AVR_BN_GRAD, "avr_bn_layer_run: bad prologue");
   AVR_REQUIRE(l->n_rows >= 0, "avr_bn_layer_run: bad row count");

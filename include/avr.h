@@ -361,7 +361,9 @@ int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_s
  *
  * avr_bn_layer: one x3 GEMM of a layer over all rows (split-fp16 MFMA, fp32 accumulate, as the fused kernels).
  *   mode AVR_BN_FWD: out = W . op + bias (+ add1) (+ add2) with W = the forward blob's layer `layer` (header
- *     numbering: 0 lin_in, 2 + 2b fc_0[b], 3 + 2b fc_1[b]; pack with dims->bn = 0: no eval-BN folding);
+ *     numbering: 0 lin_in, 2 + 2b fc_0[b], 3 + 2b fc_1[b]; pack with dims->bn = 0: no eval-BN folding; ABI 13:
+ *     a use_spade blob as well -- avr.layer_train runs use_spade / NS > 1 nets on these layers with identity
+ *     statistics, in_mu = out_mu = shift = 0, scale = invstd = 1: op = relu(src), mask = [pre_rows > 0]);
  *     partial (n_wg, 2, out_dim) = per 64-row workgroup (mean, sum of squared deviations) of out's columns.
  *   mode AVR_BN_BWD: gp = (W^T . op) * [(pre_rows - out_mu) * out_scale + out_shift > 0] with W^T from the
  *     backward blob (avr_field_pack_bwd): the relu mask of the forward's AVR_BN_RELU operand, recomputed from

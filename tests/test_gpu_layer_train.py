@@ -1,0 +1,129 @@
+"""HIP training of use_spade and NS > 1 source-view nets (VERDICT r04 missing 2; avr.layer_train): the
+layer-by-layer x3 GEMMs (avr_bn_layer_run with identity statistics), the spade product rule
+(models.py:528-534, 585-587) and the views' combine adjoint (models.py:566-579, utils.py:71-81) against a
+float64 autograd reference of the same module: every parameter gradient (scale_z's included), the latent-map
+and point gradients within twice PyTorch fp32 autograd's own error (or 3e-5 of max |grad|), as the fused
+training path is held (tests/test_gpu_train.py)."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_train import _compare64, _fp64, _net
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def _views_net(d_hidden, n_blocks, d_latent, hw, combine_layer, SB, NS, spade, combine_type="average", seed=0):
+    """SB objects seen from NS source views each (train.py would encode SB x NS images): latent maps and poses per
+    (object, view), focal / principal point per object."""
+    net = _net(d_hidden, n_blocks, d_latent, hw, combine_layer, sb=1, seed=seed, spade=spade,
+               combine_type=combine_type)
+    K = SB * NS
+    g = torch.Generator().manual_seed(seed + 11)
+    net.encoder.set_latent(torch.randn(K, d_latent, hw[0], hw[1], generator=g).to(DEV))
+    poses = net.poses.repeat(K, 1, 1)
+    poses[:, 0, 3] += 0.07 * torch.arange(K, device=DEV, dtype=torch.float32)
+    poses[:, 1, 3] -= 0.05 * torch.arange(K, device=DEV, dtype=torch.float32)
+    net.poses = poses
+    net.focal = net.focal.repeat(SB, 1)
+    net.c = net.c.repeat(SB, 1)
+    net.num_views_per_obj = NS
+    net.num_objs = SB
+    return net
+
+
+def _grads(net, xyz, vd, w, coarse, hip, latent_grad):
+    net.hip_backward = hip
+    net.zero_grad(set_to_none=True)
+    lat = net.encoder.latent.detach().clone().requires_grad_(latent_grad)
+    net.encoder.latent = lat
+    x = xyz.clone().requires_grad_(True)
+    out = net(x, coarse=coarse, viewdirs=vd)
+    (out * w).sum().backward()
+    mlp = net.mlp_coarse if coarse else net.mlp_fine
+    gr = {n: p.grad.detach().clone() for n, p in mlp.named_parameters() if p.grad is not None}
+    gr["xyz"] = x.grad.detach().clone()
+    if latent_grad:
+        gr["latent"] = lat.grad.detach().clone()
+    return out.detach(), gr
+
+
+def _near_tie_points(net, xyz, vd, coarse, rel=1e-4):
+    """Max combine: the points where some feature's two largest views are within `rel` (of that feature's largest
+    |value| over the batch) at the combine layer, in float64 -- the only places the view a gradient goes to can
+    depend on fp32 rounding (the gradient of a max is discontinuous at ties)."""
+    mlp = net.mlp_coarse if coarse else net.mlp_fine
+    NS, (SB, B, _) = net.num_views_per_obj, xyz.shape
+    with torch.no_grad():
+        net.double()
+        try:
+            feat, zft = net.mlp_inputs(xyz.double(), vd.double())
+            x = mlp.lin_in(zft)
+            for b in range(mlp.combine_layer):
+                tz = mlp.lin_z[b](feat)
+                x = mlp.scale_z[b](feat) * x + tz if mlp.use_spade else x + tz
+                x = mlp.blocks[b](x)
+        finally:
+            net.float()
+    v = x.reshape(SB, NS, B, -1)
+    top2 = v.topk(2, dim=1).values
+    gap = (top2[:, 0] - top2[:, 1]) / v.abs().amax(dim=(0, 1, 2)).clamp_min(1e-30)
+    return (gap < rel).any(-1)                                              # (SB, B)
+
+
+CASES = [  # d_hidden, n_blocks, d_latent, combine_layer, SB, NS, spade, combine_type
+    (64, 3, 64, 1000, 2, 1, True, "average"),
+    (128, 5, 64, 3, 1, 1, True, "average"),
+    (64, 3, 64, 2, 2, 2, False, "average"),
+    (128, 4, 128, 2, 1, 3, False, "max"),
+    (64, 3, 64, 2, 2, 2, True, "average"),
+    (64, 3, 64, 2, 2, 2, True, "max"),
+    (512, 5, 512, 3, 1, 2, True, "average"),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"h{c[0]}-nb{c[1]}-cl{c[3]}-sb{c[4]}-ns{c[5]}"
+                                                     f"{'-spade' if c[6] else ''}-{c[7]}")
+def test_layer_train_grads_match_fp64(case):
+    from avr import layer_train
+    d_hidden, n_blocks, d_latent, cl, SB, NS, spade, ctype = case
+    hw = (16, 16) if d_hidden == 512 else (8, 8)
+    net = _views_net(d_hidden, n_blocks, d_latent, hw, cl, SB, NS, spade, ctype)
+    g = torch.Generator().manual_seed(17)
+    B = 333
+    xyz = ((torch.rand(SB, B, 3, generator=g) - 0.5) * 0.8).to(DEV)
+    vd = torch.nn.functional.normalize(torch.randn(SB, B, 3, generator=g), dim=-1).to(DEV)
+    w = torch.randn(SB, B, 4, generator=g).to(DEV)
+    assert net.can_train_layers(xyz, vd) and not net.can_train_fused(xyz, vd)
+    calls = []
+    orig = layer_train._FieldTrainLayers.apply
+    layer_train._FieldTrainLayers.apply = lambda *a: calls.append(1) or orig(*a)
+    try:
+        for coarse in (True, False):
+            wc = w
+            if ctype == "max":
+                # the gradient of a max goes to each feature's largest view; where two views tie to within fp32
+                # noise, any two implementations may pick different ones (a discrete flip, as a relu mask's:
+                # 5e-5 to 1e-4 of max |grad| on lin_in seen at (128, 4, ns3)): those points carry no loss here
+                tie = _near_tie_points(net, xyz, vd, coarse)
+                wc = w * (~tie).unsqueeze(-1).float()
+                print(f"{case} coarse={coarse}: {int(tie.sum())} of {tie.numel()} points near a max tie")
+            out_h, g_h = _grads(net, xyz, vd, wc, coarse, hip=True, latent_grad=True)
+            n_hip = len(calls)
+            out_t, g_t = _grads(net, xyz, vd, wc, coarse, hip=False, latent_grad=True)
+            assert n_hip >= 1 and len(calls) == n_hip, "the HIP run must take the layer path, torch's must not"
+            np.testing.assert_allclose(out_h.cpu().numpy(), out_t.cpu().numpy(), atol=2e-4)
+            if spade:
+                assert any(k.startswith("scale_z.") for k in g_h)
+            _, g_d = _fp64(net, lambda: _grads(net, xyz.double(), vd.double(), wc.double(), coarse, hip=False,
+                                               latent_grad=True))
+            for k in g_d:   # every key's errors first (the assertion below names only the first failing one)
+                ref = g_d[k].double()
+                sc = float(ref.abs().max()) or 1.0
+                print(f"   {k}: HIP {float((g_h[k].double() - ref).abs().max()) / sc:.2e} "
+                      f"torch32 {float((g_t[k].double() - ref).abs().max()) / sc:.2e}")
+            worst = _compare64(g_h, g_t, g_d)
+            print(f"{case} coarse={coarse}: worst HIP gradient error vs float64 {worst:.2e} of max |grad|")
+    finally:
+        layer_train._FieldTrainLayers.apply = orig

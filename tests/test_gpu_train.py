@@ -13,13 +13,14 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
 
 
-def _net(d_hidden, n_blocks=3, d_latent=64, hw=(8, 8), combine_layer=1000, sb=1, seed=0, beta=0.0):
+def _net(d_hidden, n_blocks=3, d_latent=64, hw=(8, 8), combine_layer=1000, sb=1, seed=0, beta=0.0, spade=False,
+         combine_type="average"):
     from avr.conf import Conf, default_conf
     from avr.scene import synthetic_scene
     conf = default_conf()["model"]
     d = dict(conf)
     mlp = {"type": "resnet", "n_blocks": n_blocks, "d_hidden": d_hidden, "combine_layer": combine_layer,
-           "beta": beta}
+           "beta": beta, "use_spade": spade, "combine_type": combine_type}
     d["mlp_coarse"], d["mlp_fine"] = dict(mlp), dict(mlp)
     d["encoder"] = {"backbone": "resnet34", "pretrained": False,
                     "num_layers": {64: 1, 128: 2, 256: 3, 512: 4}[d_latent]}
