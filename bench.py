@@ -330,7 +330,7 @@ def _median_rate(fn, units, runs=3):
     return float(np.median(rates)), rates
 
 
-def cpu_baseline(c3_rays=384, c1_rays=2048):
+def cpu_baseline(c3_rays=384, c1_rays=4096):
     """The reference's CPU path on this host's cores, SURVEY §8d protocol:
     every thread this process may use, 1 warm-up, median of 3. Two ports are
     timed and the faster one is the baseline (which one wins depends on the
