@@ -132,8 +132,8 @@ class _FieldTrainLayers(torch.autograd.Function):
             Xin, N = [], []
             for b in range(nb):
                 x = Xpre[b]
-                if b < nz:
-                    x = S[b] * x + T[b] if spade else x + T[b]             # models.py:583-588
+                if b < nz:                                                  # models.py:583-588
+                    x = torch.addcmul(T[b], S[b], x) if spade else x + T[b]
                 if b == cl and NS > 1:
                     x = combine_interleaved(x, (NS, B), mlp.combine_type).reshape(M2, H)
                 x = x.contiguous()
@@ -188,22 +188,27 @@ class _FieldTrainLayers(torch.autograd.Function):
             d4 = torch.cat([go[:, :3] * ((1.0 - y[:, :3]) * y[:, :3]), go[:, 3:] * (y[:, 3:] > 0)], -1).contiguous()
             g = torch.ops.aten.threshold_backward(d4 @ P["lin_out.weight"].detach().to(F32), Xpre[nb], 0.0)
             wl1, wl2 = [], []           # weight-gradient layers over M1 / M2 rows
-            Gz, Gs = [None] * nz, [None] * nz
+            Gz, Gs, Gz_max = [None] * nz, [None] * nz, [None] * nz
             blk = [None] * nb
+            # max |operand| of every backward layer call, published by the layer kernels (the weight gradients'
+            # scales for gp2 and g without a reduction pass over the rows): [2b] fc_0^T's, [2b + 1] fc_1^T's
+            omax = torch.zeros(2 * nb, device=dev, dtype=torch.int32)
             for b in range(nb - 1, -1, -1):
                 m = M1 if b < cl else M2
                 # fc_1^T: gradient at N[b]; fc_0^T: the fc_0 path's gradient at X'[b]
                 gp2 = torch.empty(m, H, device=dev, dtype=F32)
                 _run(dims, _layer(n_rows=m, mode=_lib.BN_BWD, prologue=_lib.BN_PLAIN, in_dim=H, in_valid=H, src=g,
-                                  ld_src=H, blob=bwd, layer=3 + 2 * b, out=gp2, pre_rows=N[b], out_mu=idt.zero,
-                                  out_invstd=idt.one, out_scale=idt.one, out_shift=idt.zero, partial=part), stream)
+                                  ld_src=H, operand_max=omax[2 * b + 1:], blob=bwd, layer=3 + 2 * b, out=gp2,
+                                  pre_rows=N[b], out_mu=idt.zero, out_invstd=idt.one, out_scale=idt.one,
+                                  out_shift=idt.zero, partial=part), stream)
                 gp1 = torch.empty(m, H, device=dev, dtype=F32)
                 _run(dims, _layer(n_rows=m, mode=_lib.BN_BWD, prologue=_lib.BN_PLAIN, in_dim=H, in_valid=H, src=gp2,
-                                  ld_src=H, blob=bwd, layer=2 + 2 * b, out=gp1, pre_rows=Xin[b], out_mu=idt.zero,
-                                  out_invstd=idt.one, out_scale=idt.one, out_shift=idt.zero, partial=part), stream)
+                                  ld_src=H, operand_max=omax[2 * b:], blob=bwd, layer=2 + 2 * b, out=gp1,
+                                  pre_rows=Xin[b], out_mu=idt.zero, out_invstd=idt.one, out_scale=idt.one,
+                                  out_shift=idt.zero, partial=part), stream)
                 relu_x = (idt.zero, idt.one, idt.zero)     # X = relu(rows), rebuilt in the staging
-                blk[b] = [(gp2, Xin[b], _max_bits(gp2), amax[2 * b:2 * b + 1], True, relu_x),
-                          (g, N[b], _max_bits(g), amax[2 * b + 1:2 * b + 2], True, relu_x)]
+                blk[b] = [(gp2, Xin[b], omax[2 * b:2 * b + 1], amax[2 * b:2 * b + 1], True, relu_x),
+                          (g, N[b], omax[2 * b + 1:2 * b + 2], amax[2 * b + 1:2 * b + 2], True, relu_x)]
                 gin = g + gp1                                  # d loss / d X'[b] (residual + fc_0 path)
                 if b == cl and NS > 1:                         # torch's adjoint of the views' combine
                     with torch.enable_grad():
@@ -215,6 +220,8 @@ class _FieldTrainLayers(torch.autograd.Function):
                     if spade:                                  # X' = S * X + T (models.py:585-587)
                         Gs[b] = (gin * Xpre[b]).contiguous()
                         gin = S[b] * gin
+                    elif b > 0:                                # gin is the next fc_1^T's operand: its max comes free
+                        Gz_max[b] = omax[2 * b - 1:2 * b]
                 g = gin.contiguous()
             g_in0 = g                                          # d loss / d lin_in output
             for b in range(nb):
@@ -227,7 +234,8 @@ class _FieldTrainLayers(torch.autograd.Function):
                 lat_feat = _gather(fused, hwc, K, NS, p, B, net.d_latent)
                 lat_max = fused.latent_max_bits(latent)
                 for b in range(nz):
-                    wl1.append((Gz[b], lat_feat, _max_bits(Gz[b]), lat_max, True))
+                    wl1.append((Gz[b], lat_feat, Gz_max[b] if Gz_max[b] is not None else _max_bits(Gz[b]), lat_max,
+                                True))
                 for b in range(nz if spade else 0):
                     wl1.append((Gs[b], lat_feat, _max_bits(Gs[b]), lat_max, True))
             wl1.append((g_in0, zfp, _max_bits(g_in0), _max_bits(zfp), True))

@@ -334,7 +334,7 @@ class NewPixelNeRFNet(nn.Module):
         rot = self.poses[:, :3, :3]
 
         def rotate(v):   # R v per point: the reference's per-point (3x3)(3x1) matmul, or one bmm per scene
-            if batched_rot and NS == 1 and rot.shape[0] == v.shape[0]:
+            if batched_rot and rot.shape[0] == v.shape[0] and v.dim() == 3:
                 return torch.bmm(v, rot.transpose(1, 2))
             return torch.matmul(rot[:, None], v.unsqueeze(-1))[..., 0]
 

@@ -50,12 +50,15 @@ def reference_flops_per_sample(d_in=42, d_latent=512, d_hidden=512, n_blocks=3, 
                 + d_hidden * d_out)
 
 
-def build_scene(device, seed=0, sigma_bias=0.0, conf="default", bn=False):
+def build_scene(device, seed=0, sigma_bias=0.0, conf="default", bn=False, spade=False):
     """avr.scene.synthetic_scene: the default.conf field (or default_mv.conf's: 5 blocks, combine_layer 3)
-    with fc_1 ~ N(0, 0.02), random 512x64x64 latent."""
+    with fc_1 ~ N(0, 0.02), random 512x64x64 latent. spade: ResnetFC(use_spade=True) in both MLPs."""
     from avr.conf import default_conf
     from avr.scene import synthetic_scene
     model = default_conf(multiview=conf == "default_mv")["model"]
+    if spade:
+        model["mlp_coarse"] = dict(model["mlp_coarse"], use_spade=True)
+        model["mlp_fine"] = dict(model["mlp_fine"], use_spade=True)
     return synthetic_scene(device, seed, model, sigma_bias=sigma_bias, bn=bn)
 
 
@@ -417,12 +420,14 @@ def run_train(args, device):
     from avr.conf import default_conf
     from avr.renderers import AdaptiveVolumeRenderer, VolumeRenderer
     SB, R = 4, 512
-    net = build_scene(device, conf=args.conf, bn=args.bn)
+    NS = args.views                  # source views per object (train.py:56 fixes 1; models.py:566-579 combines them)
+    net = build_scene(device, conf=args.conf, bn=args.bn, spade=args.spade)
     g = torch.Generator(device="cpu").manual_seed(7)
-    net.encoder.set_latent(torch.randn(SB, net.d_latent, 64, 64, generator=g).to(device))
+    net.encoder.set_latent(torch.randn(SB * NS, net.d_latent, 64, 64, generator=g).to(device))
     net.num_objs = SB
-    net.poses = net.poses.repeat(SB, 1, 1)
-    net.poses[:, 0, 3] += 0.05 * torch.arange(SB, device=device, dtype=torch.float32)
+    net.num_views_per_obj = NS
+    net.poses = net.poses.repeat(SB * NS, 1, 1)
+    net.poses[:, 0, 3] += 0.05 * torch.arange(SB * NS, device=device, dtype=torch.float32)
     net.focal, net.c = net.focal.repeat(SB, 1), net.c.repeat(SB, 1)
     net.train()
     for p in net.parameters():
@@ -486,11 +491,13 @@ def run_train(args, device):
         "value": round(SB * R / res["hip"], 1), "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(res["hip"] * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (field products as 3 fp16 MFMA terms)",
-        "data": f"synthetic: random-init {args.conf}.conf field{' with --bn (training-mode BatchNorm)' if args.bn else ''}, "
-                "4 random 512x64x64 latents, random pixels/targets",
+        "data": f"synthetic: random-init {args.conf}.conf field{' with --bn (training-mode BatchNorm)' if args.bn else ''}"
+                f"{' with use_spade' if args.spade else ''}, {SB * NS} random 512x64x64 latents"
+                f"{f' ({NS} source views per object)' if NS > 1 else ''}, random pixels/targets",
         "config": {"workload": wl + f", field of conf/{args.conf}.conf ({net.mlp_coarse.n_blocks} x "
                                f"{net.mlp_coarse.d_hidden} ResnetFC, combine_layer {net.mlp_coarse.combine_layer}"
-                               + (", bn=True: training-mode BatchNorm, avr.bn_train)" if args.bn else ")"),
+                               + (", bn=True: training-mode BatchNorm, avr.bn_train)" if args.bn else
+                                  ", layer by layer: avr.layer_train)" if (args.spade or NS > 1) else ")"),
                    "field_samples_per_step": SB * R * spr},
     }
     if "torch" in res:
@@ -922,6 +929,9 @@ def main():
     ap.add_argument("--bn", action="store_true",
                     help="--mode train: train.py --bn (ResnetBlockFC(bn=True), training-mode BatchNorm: the "
                          "layer-by-layer HIP path avr.bn_train)")
+    ap.add_argument("--spade", action="store_true", help="--mode train: ResnetFC(use_spade=True) (avr.layer_train)")
+    ap.add_argument("--views", type=int, default=1,
+                    help="--mode train: source views per object, NS (> 1: the views' combine, avr.layer_train)")
     ap.add_argument("--renderer", choices=["volume", "adaptive"], default="volume",
                     help="--mode train: VolumeRenderer (train.py 'VR*' runs) or AdaptiveVolumeRenderer (train.py's "
                          "default for other run names, train.py:268-273)")

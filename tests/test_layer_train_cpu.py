@@ -88,19 +88,22 @@ def _install(monkeypatch, net):
             for k in ("add1", "add2"):
                 if kw.get(k) is not None:
                     out = out + kw[k]
-            if kw.get("operand_max") is not None:
-                m = torch.maximum(op.abs().max().reshape(1), kw["operand_max"][:1].view(torch.float32))
-                kw["operand_max"][:1].copy_(m.view(torch.int32))
         else:
             assert kw["prologue"] == _lib.BN_PLAIN
+            op = src
             mask = torch.relu((kw["pre_rows"] - kw["out_mu"]) * kw["out_scale"] + kw["out_shift"]) > 0
             out = (src @ W) * mask
+        if kw.get("operand_max") is not None:     # publish max |operand| (float bits, max with what is there)
+            m = torch.maximum(op.abs().max().reshape(1), kw["operand_max"][:1].view(torch.float32))
+            kw["operand_max"][:1].copy_(m.view(torch.int32))
         kw["out"].copy_(out)
 
     def weight_grads(layers, n_rows, n_split=None):
         res = []
         for g, x, gmax, xmax, want_bias, *bn in layers:
             assert g.shape[0] == x.shape[0] == n_rows
+            # the scales' inputs: max |G| exactly (the operand maxima the layer kernels publish, or a reduction)
+            assert float(gmax.view(torch.float32)[0]) == float(g.abs().max()), "wrong max |G|"
             if bn:
                 mu, sc, sh = bn[0]
                 x = torch.relu((x - mu) * sc + sh)
