@@ -6,11 +6,12 @@
 // The fused field kernels carry a 64-sample tile through every layer in one workgroup; batch statistics are a
 // reduction over all rows between two GEMMs, so this net runs layer by layer. One launch per GEMM over
 // row-major fp32 rows (bn_layer_kernel): the operand -- the layer input normalised and relu'd (forward), or
-// the BatchNorm backward of the gradient (backward) -- is built in the prologue from the rows, split into
-// fp16 hi/lo under one power-of-two scale per workgroup and staged in LDS in the fused kernels' B-fragment
-// order; the K loop is theirs (x3: three v_mfma_f32_16x16x32_f16 per product, fp32 accumulate, weights
-// streamed one chunk ahead); the epilogue adds bias / residual / lin_z rows (forward) or applies the relu mask
-// (backward, recomputed from the pre-BN rows: the relu'd operands are never stored), stores the rows and
+// the BatchNorm backward of the gradient (backward) -- is built in the prologue straight from the rows in the
+// fused kernels' B-fragment order (each lane loads exactly its fragment columns), split into fp16 hi/lo under
+// one power-of-two scale per workgroup and written to LDS; the K loop is theirs (x3: three
+// v_mfma_f32_16x16x32_f16 per product, fp32 accumulate, weights streamed one chunk ahead); the epilogue works in
+// the accumulator layout -- adds bias / residual / lin_z rows (forward) or applies the relu mask (backward,
+// recomputed from the pre-BN rows: the relu'd operands are never stored), stores the rows and
 // reduces this workgroup's column statistics. A finalize launch between
 // layers (bn_stats_kernel / bn_grad_stats_kernel) combines the workgroups' partials in fp64.
 #include "x3_gemm.h"
@@ -41,16 +42,37 @@ struct BnArgs {
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 
-// 16 lanes of one lane group g (lanes 16g .. 16g + 15): sum over j
+// 16 lanes of one lane group g (lanes 16g .. 16g + 15): sum over j, the same bits in every lane (xor butterfly on
+// DPP / row shifts: no LDS round trip, unlike __shfl_xor's ds_bpermute)
 __device__ __forceinline__ floatx4 sum16(floatx4 v) {
 #pragma unroll
   for (int d = 1; d < 16; d <<= 1) {
-    v.x += __shfl_xor(v.x, d, 64);
-    v.y += __shfl_xor(v.y, d, 64);
-    v.z += __shfl_xor(v.z, d, 64);
-    v.w += __shfl_xor(v.w, d, 64);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] += lane_xor(v[t], d, 0);
   }
   return v;
+}
+
+// Row lines <-> fragment pairs. Lane (g, j) of a 16-row group works on the 16-B groups x0 (columns c + 4g .. +3)
+// and x1 (c + 16 + 4g .. +3) of row j: each row's 128-B line is split over lanes g and both halves. In memory it
+// is moved as two instructions of 8 rows x 128 B -- lane j takes row j & 7 (A) and row 8 + (j & 7) (B), columns
+// c + 16 (j >> 3) + 4g .. +3 -- so that every instruction covers whole lines, and lanes j and j ^ 8 swap one
+// value through one DPP row rotation (row_ror:8).
+__device__ __forceinline__ floatx4 ror8(floatx4 v) {
+  floatx4 r;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) r[t] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[t]), 0x128, 0xf, 0xf, false));
+  return r;
+}
+__device__ __forceinline__ void lines_to_pair(floatx4 A, floatx4 B, bool lo, floatx4& x0, floatx4& x1) {
+  const floatx4 r = ror8(lo ? B : A);
+  x0 = lo ? A : r;
+  x1 = lo ? r : B;
+}
+__device__ __forceinline__ void pair_to_lines(floatx4 x0, floatx4 x1, bool lo, floatx4& A, floatx4& B) {
+  const floatx4 r = ror8(lo ? x1 : x0);
+  A = lo ? x0 : r;
+  B = lo ? r : x1;
 }
 
 template <int FT, int NW, bool TWO>
@@ -62,20 +84,32 @@ __device__ __forceinline__ void bn_gemm(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT],
     gemm_x3<FT, true, false>(acc, A0, W, KC, cstride, X16, lane);
 }
 
-// MODE 0 forward, 1 backward. Workgroup = 64 rows; lane = row in the prologue (wave w builds the operand
-// columns [K/NW * w, K/NW * (w + 1)) of all 64 rows: one 16-B load per row and column group, written into
-// the slots of its sample -- conflict-free LDS stores), then the fused kernels' GEMM and register layout:
-// lane (g, j) of wave w holds features 16 (FT w + ft) + 4 g .. +3 of rows 16 sg + j.
-template <int FT, int NW, int MODE>
-__global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
-  constexpr int HID = 16 * FT * NW, NTT = FT * NW;
+// MODE 0 forward, 1 backward; KK = K (64: lin_in, or d_hidden). Workgroup = 64 rows, NW waves, no fp32 stage and
+// no epilogue barrier:
+// * operand: the K columns are 4 KK / 32 items (32-column chunk c, sample group sg of 16 rows); wave w takes IPW
+//   consecutive items; lane (g, j) needs, for each, exactly its B-fragment columns 32c + 4g .. +3 and
+//   32c + 16 + 4g .. +3 of row 16 sg + j, loaded as whole 128-B row lines and exchanged (lines_to_pair); it
+//   applies the prologue's transform and keeps the values in registers until the workgroup's max |operand| is
+//   met in LDS; then one 16-B hi and one 16-B lo LDS write per item put them in the fused kernels' X slots
+//   (conflict-free: consecutive j, consecutive slots).
+// * GEMM: the fused kernels' K loop; lane (g, j) of wave w ends with features 16 (FT w + ft) + 4g .. +3 of rows
+//   16 sg + j.
+// * epilogue straight from the accumulators: the addend / pre-BN loads and the row stores move whole lines
+//   (pair_to_lines), and since a wave owns its columns for all 64 rows, a column's statistics are in-lane sums
+//   over the four sample groups and a 16-lane DPP reduction over j -- no LDS, no barrier, so each wave starts its
+//   epilogue as soon as its own GEMM ends.
+template <int FT, int NW, int MODE, int KK>
+// (4-wave layouts: two workgroups per CU, so at most 256 registers a lane)
+__global__ void __launch_bounds__(64 * NW, NW > 4 ? 1 : 2) bn_layer_kernel(BnArgs a) {
+  constexpr int HID = 16 * FT * NW;
   constexpr bool TWO = NW > 4;
-  constexpr int MAXQ = 512 / 4 / NW;        // operand column groups per wave (K <= 512)
+  constexpr int IPW = 4 * (KK / 32) / NW;    // operand items per wave
+  constexpr int IPC = IPW < 4 ? IPW : 4;     // items per chunk of this wave
+  constexpr int NCH = IPW / IPC;             // chunks of this wave
+  static_assert(IPW >= 1 && IPW * NW == 4 * (KK / 32) && NCH * IPC == IPW, "operand items per wave");
   extern __shared__ float lds[];
   uint4* X16 = reinterpret_cast<uint4*>(lds);
-  // the stages (prologue K + 4, epilogue HID + 4 floats a row; X aliases them), the column sums, then red
-  const int stage_f = kX3Samples * ((a.K > HID ? a.K : HID) + 4);
-  float* red = lds + stage_f + NW * HID;
+  float* red = lds + 64 * KK;                // past X (64 samples x KK x (hi + lo) fp16)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, j = lane & 15;
   const int64_t m0 = (int64_t)blockIdx.x * kX3Samples;
@@ -85,92 +119,114 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   prefetch_a<FT, TWO ? FT : kPrefetch>(A0, W, lane);
 
   // ---------------------------------------------------------------- operand
-  // Phase A, coalesced: wave w takes rows w, w + NW, ...; lane l column groups l, l + 64, ... of the row (one
-  // 1-KB row segment per load), applies the prologue's transform with its columns' parameters and writes the
-  // fp32 values into an LDS stage, row stride 4 K + 16 B. Phase B: lane = row reads its operand columns back
-  // (the +16 B row pad spreads the 64 rows over the banks) and splits them into X, which aliases the stage
-  // (the values wait in registers across the barrier).
-  const int G4 = a.K / 4;                    // column groups of a row
-  const int rs = a.K + 4;                    // stage row stride (floats)
-  float mx = 0.f;
-  // pair i of this lane: row wid + NW (i >> 1), column group lane + 64 (i & 1) (K <= 512: <= 2 per row). In
-  // batches of PB pairs, every load of a batch issued before the batch's first store: a load cannot move above a
-  // store that may alias it, and the in-order memory counter makes a wait on a load also wait on every store
-  // issued before it -- one round trip per pair otherwise. The lane's two column groups' parameters are loaded
-  // once (RELU: mu, scale, shift; GRAD: mu, invstd, m1, m2, scale).
-  floatx4 pp[5][2];
+  // item i of this wave: chunk (IPW w + i) / 4, sample group (IPW w + i) % 4; its row r = 16 sg + j (rows past
+  // the end load row m0 and become zeros); half h: columns 32 c + 16 h + 4 g .. +3
+  const int i0 = IPW * wid;
+  const auto chunk = [&](int i) { return (i0 + i) >> 2; };
+  const auto row_r = [&](int i) { return 16 * ((i0 + i) & 3) + j; };
+  const auto col_k = [&](int i, int h) { return 32 * chunk(i) + 16 * h + 4 * g; };
+  // the item's rows as lines (see lines_to_pair): line row lr(i, half), columns 32 c + 16 (j >> 3) + 4 g
+  const bool lo = j < 8;
+  const auto lr = [&](int i, int half) { return 16 * ((i0 + i) & 3) + 8 * half + (j & 7); };
+  const auto lrow = [&](int i, int half) -> int64_t { return m0 + (lr(i, half) < nvalid ? lr(i, half) : 0); };
+  const auto lcol = [&](int i) { return 32 * chunk(i) + 16 * (j >> 3) + 4 * g; };
+  const auto srow = [&](int i) -> int64_t { return m0 + (row_r(i) < nvalid ? row_r(i) : 0); };
+  floatx4 xv[IPW][2];
+  if (KK != 64 || a.kin == KK) {   // whole 16-B groups (every hidden layer): a batch's loads back to back, branch-free
+    if (a.prologue == AVR_BN_GRAD) {
+      // three rows per value (gradient, pre-BN, residual): one chunk's parameters and two items per batch, the
+      // residual's presence decided once (a null check per load would keep each load behind its own branch)
+      const auto grad = [&](auto res_t) {
+        constexpr bool RES = decltype(res_t)::value;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int k = 4 * (lane + 64 * h) < a.kin ? 4 * (lane + 64 * h) : 0;
-    if (a.prologue == AVR_BN_RELU) {
-      pp[0][h] = ld4(a.in_mu + k); pp[1][h] = ld4(a.in_scale + k); pp[2][h] = ld4(a.in_shift + k);
-    } else if (a.prologue == AVR_BN_GRAD) {
-      pp[0][h] = ld4(a.in_mu + k); pp[1][h] = ld4(a.in_invstd + k); pp[2][h] = ld4(a.in_m1 + k);
-      pp[3][h] = ld4(a.in_m2 + k); pp[4][h] = ld4(a.in_scale + k);
+        for (int cc = 0; cc < NCH; ++cc) {
+          floatx4 pp[5][2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = col_k(cc * IPC, h);
+            pp[0][h] = ld4(a.in_mu + k); pp[1][h] = ld4(a.in_invstd + k); pp[2][h] = ld4(a.in_m1 + k);
+            pp[3][h] = ld4(a.in_m2 + k); pp[4][h] = ld4(a.in_scale + k);
+          }
+          constexpr int GB = IPC < 2 ? IPC : 2;   // items per batch
+#pragma unroll
+          for (int q0 = 0; q0 < IPC; q0 += GB) {
+            floatx4 sv[GB][2], pv[GB][2], rv[GB][2];
+#pragma unroll
+            for (int q = 0; q < GB; ++q)
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {   // line e (A / B)
+                const int i = cc * IPC + q0 + q;
+                const int64_t o = lrow(i, e) * a.ld_src + lcol(i);
+                sv[q][e] = ld4(a.src + o);
+                pv[q][e] = ld4(a.src_pre + o);
+                if constexpr (RES) rv[q][e] = ld4(a.src_res + o);
+              }
+#pragma unroll
+            for (int q = 0; q < GB; ++q) {
+              lines_to_pair(sv[q][0], sv[q][1], lo, sv[q][0], sv[q][1]);
+              lines_to_pair(pv[q][0], pv[q][1], lo, pv[q][0], pv[q][1]);
+              if constexpr (RES) lines_to_pair(rv[q][0], rv[q][1], lo, rv[q][0], rv[q][1]);
+            }
+#pragma unroll
+            for (int q = 0; q < GB; ++q)
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const floatx4 xh = (pv[q][h] - pp[0][h]) * pp[1][h];
+                floatx4 v = (sv[q][h] - pp[2][h] - xh * pp[3][h]) * pp[4][h];
+                if constexpr (RES) v += rv[q][h];
+                xv[cc * IPC + q0 + q][h] = v;
+              }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      };
+      if (a.src_res) grad(std::true_type{});
+      else grad(std::false_type{});
+    } else {
+#pragma unroll
+      for (int i = 0; i < IPW; ++i)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) xv[i][e] = ld4(a.src + lrow(i, e) * a.ld_src + lcol(i));
+#pragma unroll
+      for (int i = 0; i < IPW; ++i) lines_to_pair(xv[i][0], xv[i][1], lo, xv[i][0], xv[i][1]);
+      if (a.prologue == AVR_BN_RELU) {
+#pragma unroll
+        for (int cc = 0; cc < NCH; ++cc)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = col_k(cc * IPC, h);
+            const floatx4 mu = ld4(a.in_mu + k), sc = ld4(a.in_scale + k), sh = ld4(a.in_shift + k);
+#pragma unroll
+            for (int q = 0; q < IPC; ++q) xv[cc * IPC + q][h] = bn_relu4(xv[cc * IPC + q][h], mu, sc, sh);
+          }
+      }
     }
+  } else {             // lin_in's z_feature rows (in_valid < in_dim, PLAIN): columns past in_valid are zeros
+#pragma unroll
+    for (int i = 0; i < IPW; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = col_k(i, h);
+        const float* p = a.src + srow(i) * a.ld_src + k;
+        floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (k + 4 <= a.kin) {
+          v = ld4(p);
+        } else if (k < a.kin) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = k + t < a.kin ? p[t] : 0.f;
+        }
+        xv[i][h] = v;
+      }
   }
-  // (the backward's GRAD prologue holds three rows per pair: smaller batches keep it within the registers)
-  constexpr int PB = MAXQ < 8 ? MAXQ : (MODE == AVR_BN_FWD ? 8 : 4);
+  float mx = 0.f;
 #pragma unroll
-  for (int b0 = 0; b0 < MAXQ; b0 += PB) {
-    floatx4 sv[PB], pv[PB], rv[PB];
-    // pair jb's source offset (rows past the end read row m0, columns past the row column 0: every load is
-    // unconditional, so none waits behind a branch); its values are dropped below where they do not belong
-    const auto src_off = [&](int jb) -> int64_t {
-      const int i = b0 + jb, r = wid + NW * (i >> 1), q = lane + 64 * (i & 1);
-      const bool ok = r < kX3Samples && q < G4 && 4 * q + 4 <= a.kin;
-      return (m0 + (r < nvalid && ok ? r : 0)) * a.ld_src + (ok ? 4 * q : 0);
-    };
-    if (a.kin == a.K) {   // whole 16-B groups (every hidden layer): the batch's loads back to back
+  for (int i = 0; i < IPW; ++i) {
+    const bool live = row_r(i) < nvalid;
 #pragma unroll
-      for (int jb = 0; jb < PB; ++jb) sv[jb] = ld4(a.src + src_off(jb));
-      if (a.prologue == AVR_BN_GRAD) {
-#pragma unroll
-        for (int jb = 0; jb < PB; ++jb) pv[jb] = ld4(a.src_pre + src_off(jb));
-        if (a.src_res) {
-#pragma unroll
-          for (int jb = 0; jb < PB; ++jb) rv[jb] = ld4(a.src_res + src_off(jb));
-        }
-      }
-    } else {              // lin_in's z_feature rows (in_valid < in_dim, PLAIN)
-#pragma unroll
-      for (int jb = 0; jb < PB; ++jb) {
-        const int i = b0 + jb, r = wid + NW * (i >> 1), q = lane + 64 * (i & 1);
-        sv[jb] = floatx4{0.f, 0.f, 0.f, 0.f};
-        if (r < kX3Samples && q < G4) {
-          const int64_t row = m0 + (r < nvalid ? r : 0);
-          const int k = 4 * q;
-          if (k + 4 <= a.kin) {
-            sv[jb] = ld4(a.src + row * a.ld_src + k);
-          } else if (k < a.kin) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) sv[jb][t] = k + t < a.kin ? a.src[row * a.ld_src + k + t] : 0.f;
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int jb = 0; jb < PB; ++jb) {
-      const int i = b0 + jb, r = wid + NW * (i >> 1), q = lane + 64 * (i & 1), h = i & 1;
-      if (r < kX3Samples && q < G4) {
-        const bool live = r < nvalid;
-        const int64_t row = m0 + (live ? r : 0);
-        const int k = 4 * q;
-        floatx4 v = sv[jb];
-        if (k < a.kin) {
-          if (a.prologue == AVR_BN_RELU) {
-            v = bn_relu4(v, pp[0][h], pp[1][h], pp[2][h]);
-          } else if (a.prologue == AVR_BN_GRAD) {
-            const floatx4 xh = (pv[jb] - pp[0][h]) * pp[1][h];
-            v = (v - pp[2][h] - xh * pp[3][h]) * pp[4][h];
-            if (a.src_res) v += rv[jb];
-          }
-        }
-        if (!live) v = floatx4{0.f, 0.f, 0.f, 0.f};
-        else if (a.opnd_out) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a.opnd_out + row * a.K + k));
-        *reinterpret_cast<floatx4*>(lds + r * rs + k) = v;
-        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-      }
+    for (int h = 0; h < 2; ++h) {
+      if (!live) xv[i][h] = floatx4{0.f, 0.f, 0.f, 0.f};
+      const floatx4 v = xv[i][h];
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
   }
   mx = wave_max(mx);
@@ -179,227 +235,244 @@ __global__ void __launch_bounds__(64 * NW, 1) bn_layer_kernel(BnArgs a) {
   const float wgmax = red_max<NW>(red);
   if (a.opnd_max && wid == 0 && lane == 0) publish_max(a.opnd_max, wgmax);
   const float s_x = pow2_scale_for(wgmax);
-  const int qpw = a.K / 4 / NW;              // phase B: column groups of this wave
-  floatx4 xv[MAXQ];
 #pragma unroll
-  for (int i = 0; i < MAXQ; ++i)
-    if (i < qpw) xv[i] = *reinterpret_cast<const floatx4*>(lds + lane * rs + 4 * (qpw * wid + i));
-  lds_barrier();
-  char* xb = reinterpret_cast<char*>(X16);
+  for (int i = 0; i < IPW; ++i) {
+    uint2 hi0, lo0, hi1, lo1;
+    split4(xv[i][0], s_x, hi0, lo0);
+    split4(xv[i][1], s_x, hi1, lo1);
+    X16[xidx(chunk(i), 0, g, row_r(i))] = make_uint4(hi0.x, hi0.y, hi1.x, hi1.y);
+    X16[xidx(chunk(i), 1, g, row_r(i))] = make_uint4(lo0.x, lo0.y, lo1.x, lo1.y);
+  }
+  if (a.opnd_out) {    // after every prologue load: a store ahead of a load would hold its wait
 #pragma unroll
-  for (int i = 0; i < MAXQ; ++i) {
-    if (i < qpw) {
-      const int k = 4 * (qpw * wid + i);
-      uint2 hi, lo;
-      split4(xv[i], s_x, hi, lo);
-      const int c = k >> 5, gq = (k >> 2) & 3, half = (k >> 4) & 1;
-      *reinterpret_cast<uint2*>(xb + xidx(c, 0, gq, lane) * 16 + 8 * half) = hi;
-      *reinterpret_cast<uint2*>(xb + xidx(c, 1, gq, lane) * 16 + 8 * half) = lo;
+    for (int i = 0; i < IPW; ++i) {
+      floatx4 L[2];
+      pair_to_lines(xv[i][0], xv[i][1], lo, L[0], L[1]);
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        if (lr(i, e) < nvalid)
+          __builtin_nontemporal_store(L[e], reinterpret_cast<floatx4*>(a.opnd_out + (m0 + lr(i, e)) * KK + lcol(i)));
     }
   }
   lds_barrier();
 
   // ---------------------------------------------------------------- GEMM
   floatx4 acc[FT][4];
-  bn_gemm<FT, NW, TWO>(acc, A0, W, a.KC, 64 * NTT, X16, lane);
+  bn_gemm<FT, NW, TWO>(acc, A0, W, KK / 32, 64 * FT * NW, X16, lane);
   const float inv = 1.0f / (pow2_scale_for(__uint_as_float(a.hdr[a.hdr_idx])) * s_x);
 
   // ---------------------------------------------------------------- epilogue
-  // The accumulators (feature-major in the registers) go to an fp32 stage in LDS (row-major, aliasing X), and
-  // the rows are finished like the prologue's: wave = rows, lane = column groups, so the addend / mask / pre-BN
-  // row loads and the row stores are coalesced 1-KB segments. The workgroup's column statistics are per-lane
-  // sums over the wave's rows, met across the waves in LDS.
-  constexpr int EQ = HID / 4;                // column groups of an output row
-  constexpr int es = HID + 4;                // stage row stride (floats)
-  float* colred = lds + stage_f;             // (NW, HID) per-wave column sums, past the stages
-  __syncthreads();                           // every wave has left the GEMM (the stage overwrites X)
-#pragma unroll
-  for (int ft = 0; ft < FT; ++ft) {
-    const int f0 = 16 * (FT * wid + ft) + 4 * g;
-#pragma unroll
-    for (int sg = 0; sg < 4; ++sg) *reinterpret_cast<floatx4*>(lds + (16 * sg + j) * es + f0) = acc[ft][sg] * inv;
-  }
-  __syncthreads();
-  floatx4 yv[MAXQ];
-  floatx4 s1[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}}, s2[2] = {s1[0], s1[0]};
-  floatx4 cp0[2], cp1[2], cp2[2], cp3[2];    // per-column parameters of the lane's two groups
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int f = 4 * (lane + 64 * h) < HID ? 4 * (lane + 64 * h) : 0;
-    if constexpr (MODE == AVR_BN_FWD) {
-      cp0[h] = a.bias ? ld4(a.bias + f) : floatx4{0.f, 0.f, 0.f, 0.f};
-      cp1[h] = cp2[h] = cp3[h] = cp0[h];
-    } else {
-      cp0[h] = ld4(a.out_mu + f);
-      cp1[h] = ld4(a.out_invstd + f);
-      cp2[h] = ld4(a.out_scale + f);
-      cp3[h] = ld4(a.out_shift + f);
-    }
-  }
-  // pair i as in the prologue; every load of the epilogue is issued before its first store (see there)
-  const auto valid = [&](int i) { return wid + NW * (i >> 1) < kX3Samples && lane + 64 * (i & 1) < EQ; };
-  const auto live = [&](int i) { return wid + NW * (i >> 1) < nvalid; };
-  const auto row_of = [&](int i) -> int64_t { return m0 + (live(i) ? wid + NW * (i >> 1) : 0); };
-  const auto col_of = [&](int i) { return 4 * (lane + 64 * (i & 1)); };
-  // an always-valid offset for pair i's row loads (past the row: column 0), so the loads need no branch
-  const auto off_of = [&](int i) -> int64_t { return row_of(i) * HID + (valid(i) ? col_of(i) : 0); };
-  const auto staged = [&](int i) {
-    return valid(i) ? *reinterpret_cast<const floatx4*>(lds + (wid + NW * (i >> 1)) * es + col_of(i))
-                    : floatx4{0.f, 0.f, 0.f, 0.f};
+  const auto feat = [&](int ft) { return 16 * (FT * wid + ft) + 4 * g; };
+  const auto live = [&](int sg) { return 16 * sg + j < nvalid; };
+  const auto orow = [&](int sg) -> int64_t { return (m0 + (live(sg) ? 16 * sg + j : 0)) * HID; };
+  // the rows' lines (FT even: tiles 2p, 2p + 1 are one 128-B line of a row; lines_to_pair): line row
+  // 16 sg + 8 e + (j & 7), columns 16 (FT w + 2p) + 16 (j >> 3) + 4g
+  const auto er = [&](int sg, int e) { return 16 * sg + 8 * e + (j & 7); };
+  const auto eoff = [&](int sg, int e, int p) -> int64_t {
+    return (m0 + (er(sg, e) < nvalid ? er(sg, e) : 0)) * HID + 16 * (FT * wid + 2 * p) + 16 * (j >> 3) + 4 * g;
   };
+  // t = this lane's tiles of the rows at base (all loads issued, then the exchanges)
+  const auto load_rows = [&](const float* base, floatx4 (&t)[FT][4]) {
+    if constexpr (FT % 2 == 0) {
+#pragma unroll
+      for (int p = 0; p < FT / 2; ++p)
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg) {
+          t[2 * p][sg] = ld4(base + eoff(sg, 0, p));
+          t[2 * p + 1][sg] = ld4(base + eoff(sg, 1, p));
+        }
+#pragma unroll
+      for (int p = 0; p < FT / 2; ++p)
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg) lines_to_pair(t[2 * p][sg], t[2 * p + 1][sg], lo, t[2 * p][sg], t[2 * p + 1][sg]);
+    } else {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg) t[ft][sg] = ld4(base + orow(sg) + feat(ft));
+    }
+  };
+  const auto store_rows = [&](float* base, const floatx4 (&t)[FT][4]) {
+    if constexpr (FT % 2 == 0) {
+#pragma unroll
+      for (int p = 0; p < FT / 2; ++p)
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg) {
+          floatx4 L[2];
+          pair_to_lines(t[2 * p][sg], t[2 * p + 1][sg], lo, L[0], L[1]);
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            if (er(sg, e) < nvalid) *reinterpret_cast<floatx4*>(base + eoff(sg, e, p)) = L[e];
+        }
+    } else {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg)
+          if (live(sg)) *reinterpret_cast<floatx4*>(base + orow(sg) + feat(ft)) = t[ft][sg];
+    }
+  };
+  const floatx4 zero4 = floatx4{0.f, 0.f, 0.f, 0.f};
+  floatx4 s1[FT], s2[FT];
   if constexpr (MODE == AVR_BN_FWD) {
+    // out = W . op + bias (+ add1) (+ add2) (+ lin_z rows), added in that order (acc * inv is exact: a power of 2)
 #pragma unroll
-    for (int i = 0; i < MAXQ; ++i) yv[i] = staged(i);
-    // out = W . op + bias (+ add1) (+ add2) (+ lin_z rows), added in that order
+    for (int ft = 0; ft < FT; ++ft) {
+      const floatx4 b = a.bias ? ld4(a.bias + feat(ft)) : zero4;
 #pragma unroll
-    for (int i = 0; i < MAXQ; ++i)
-      if (valid(i)) yv[i] += cp0[i & 1];
-    const floatx4 zero4 = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int sg = 0; sg < 4; ++sg) acc[ft][sg] = acc[ft][sg] * inv + b;
+    }
     if (a.add1) {
-      floatx4 t[MAXQ];
+      floatx4 t[FT][4];
+      load_rows(a.add1, t);
 #pragma unroll
-      for (int i = 0; i < MAXQ; ++i) t[i] = ld4(a.add1 + off_of(i));
+      for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
-      for (int i = 0; i < MAXQ; ++i) yv[i] += valid(i) ? t[i] : zero4;
+        for (int sg = 0; sg < 4; ++sg) acc[ft][sg] += t[ft][sg];
     }
     if (a.add2) {
-      floatx4 t[MAXQ];
+      floatx4 t[FT][4];
+      load_rows(a.add2, t);
 #pragma unroll
-      for (int i = 0; i < MAXQ; ++i) t[i] = ld4(a.add2 + off_of(i));
+      for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
-      for (int i = 0; i < MAXQ; ++i) yv[i] += valid(i) ? t[i] : zero4;
+        for (int sg = 0; sg < 4; ++sg) acc[ft][sg] += t[ft][sg];
     }
     if (a.ztab) {   // the rows' lin_z features: avr_latent_features' lookup and blend order, bit for bit
-      // the points of the wave's rows first (one load each, all in flight together), then per row its corners
-      float px[MAXQ / 2][3];
+      float px[4][3];
 #pragma unroll
-      for (int i = 0; i < MAXQ; i += 2)
+      for (int sg = 0; sg < 4; ++sg)
 #pragma unroll
-        for (int d = 0; d < 3; ++d) px[i >> 1][d] = a.zxyz[3 * row_of(i) + d];
+        for (int d = 0; d < 3; ++d) px[sg][d] = a.zxyz[3 * (orow(sg) / HID) + d];
       const int64_t sc0 = m0 / a.zrows;      // the workgroup's first scene (rows are scene-major)
+      Bilinear bl[4];
+      int64_t sc[4];
 #pragma unroll
-      for (int i = 0; i < MAXQ; i += 2) {
-        if (wid + NW * (i >> 1) < kX3Samples) {
-          int64_t sc = sc0;
-          while (row_of(i) >= (sc + 1) * a.zrows) ++sc;
-          const Bilinear bl = bilinear_at(a.zviews[sc], px[i >> 1][0], px[i >> 1][1], px[i >> 1][2]);
-          const float* tab = a.ztab + sc * a.ztab_stride;
+      for (int sg = 0; sg < 4; ++sg) {
+        const int64_t row = orow(sg) / HID;
+        sc[sg] = sc0;
+        while (row >= (sc[sg] + 1) * a.zrows) ++sc[sg];
+        bl[sg] = bilinear_at(a.zviews[sc[sg]], px[sg][0], px[sg][1], px[sg][2]);
+      }
+      // one sample group's corners in flight at a time (all four would not fit beside the accumulators)
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int f = valid(i + h) ? col_of(i + h) : 0;
-            const floatx4 c0 = ld4(tab + (int64_t)bl.tex[0] * HID + f), c1 = ld4(tab + (int64_t)bl.tex[1] * HID + f);
-            const floatx4 c2 = ld4(tab + (int64_t)bl.tex[2] * HID + f), c3 = ld4(tab + (int64_t)bl.tex[3] * HID + f);
-            floatx4 z;
+      for (int sg = 0; sg < 4; ++sg) {
+        const float* tab = a.ztab + sc[sg] * a.ztab_stride;
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
-              z[t] = fadd(fadd(fadd(fmul(c0[t], bl.w[0]), fmul(c1[t], bl.w[1])), fmul(c2[t], bl.w[2])),
-                          fmul(c3[t], bl.w[3]));
-            if (valid(i + h)) yv[i + h] += z;
-          }
+        for (int ft = 0; ft < FT; ++ft) {
+          const int f = feat(ft);
+          const floatx4 c0 = ld4(tab + (int64_t)bl[sg].tex[0] * HID + f);
+          const floatx4 c1 = ld4(tab + (int64_t)bl[sg].tex[1] * HID + f);
+          const floatx4 c2 = ld4(tab + (int64_t)bl[sg].tex[2] * HID + f);
+          const floatx4 c3 = ld4(tab + (int64_t)bl[sg].tex[3] * HID + f);
+          floatx4 z;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            z[t] = fadd(fadd(fadd(fmul(c0[t], bl[sg].w[0]), fmul(c1[t], bl[sg].w[1])), fmul(c2[t], bl[sg].w[2])),
+                        fmul(c3[t], bl[sg].w[3]));
+          acc[ft][sg] += z;
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
+    store_rows(a.out, acc);
 #pragma unroll
-    for (int i = 0; i < MAXQ; ++i) {
-      if (valid(i) && live(i)) {
-        *reinterpret_cast<floatx4*>(a.out + row_of(i) * HID + col_of(i)) = yv[i];
-        s1[i & 1] += yv[i];
+    for (int ft = 0; ft < FT; ++ft) {
+      s1[ft] = zero4;
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg)
+        if (live(sg)) s1[ft] += acc[ft][sg];
+    }
+    // this workgroup's column means, then M2 about them (two-pass)
+    const float rn = 1.0f / (float)nvalid;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      s1[ft] = sum16(s1[ft]) * rn;
+      s2[ft] = zero4;
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        if (live(sg)) {
+          const floatx4 d = acc[ft][sg] - s1[ft];
+          s2[ft] += d * d;
+        }
       }
+      s2[ft] = sum16(s2[ft]);
     }
   } else {
     // gp = (W^T . op) * relu mask of the forward operand, recomputed from the pre-BN row (bn_relu4, as the
-    // forward did); the pre-BN rows also give xhat for the statistics
-    floatx4 pv[MAXQ];
+    // forward did); the pre-BN rows also give xhat for the statistics (sums of gp and of gp * xhat)
+    floatx4 pv[FT][4];
+    load_rows(a.pre_rows, pv);
 #pragma unroll
-    for (int i = 0; i < MAXQ; ++i) pv[i] = ld4(a.pre_rows + off_of(i));
+    for (int ft = 0; ft < FT; ++ft) {
+      const int f = feat(ft);
+      const floatx4 mu = ld4(a.out_mu + f), is = ld4(a.out_invstd + f);
+      const floatx4 sc = ld4(a.out_scale + f), sh = ld4(a.out_shift + f);
+      s1[ft] = zero4;
+      s2[ft] = zero4;
 #pragma unroll
-    for (int i = 0; i < MAXQ; ++i) {
-      if (valid(i) && live(i)) {
-        const floatx4 z = bn_relu4(pv[i], cp0[i & 1], cp2[i & 1], cp3[i & 1]);
-        const floatx4 v = staged(i);
+      for (int sg = 0; sg < 4; ++sg) {
+        const floatx4 z = bn_relu4(pv[ft][sg], mu, sc, sh);
+        const floatx4 v = acc[ft][sg] * inv;
         floatx4 gp;
         gp.x = z.x > 0.f ? v.x : 0.f; gp.y = z.y > 0.f ? v.y : 0.f;
         gp.z = z.z > 0.f ? v.z : 0.f; gp.w = z.w > 0.f ? v.w : 0.f;
-        *reinterpret_cast<floatx4*>(a.out + row_of(i) * HID + col_of(i)) = gp;
-        const floatx4 xh = (pv[i] - cp0[i & 1]) * cp1[i & 1];
-        s1[i & 1] += gp;
-        s2[i & 1] += gp * xh;
+        acc[ft][sg] = gp;
+        if (live(sg)) {
+          const floatx4 xh = (pv[ft][sg] - mu) * is;
+          s1[ft] += gp;
+          s2[ft] += gp * xh;
+        }
       }
+      s1[ft] = sum16(s1[ft]);
+      s2[ft] = sum16(s2[ft]);
     }
+    store_rows(a.out, acc);
   }
-  float* part = a.part + (int64_t)blockIdx.x * 2 * HID;
-  // the waves' column sums meet in one LDS slot (NW x HID), used twice: sums of y (-> the means, needed by
-  // every lane for the squared deviations) or of gp, then M2 or the sums of gp * xhat
-  const auto put = [&](const floatx4 (&v)[2]) {
+  if (j == 0) {
+    float* part = a.part + (int64_t)blockIdx.x * 2 * HID;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      if (lane + 64 * h < EQ) *reinterpret_cast<floatx4*>(colred + wid * HID + 4 * (lane + 64 * h)) = v[h];
-  };
-  const auto total = [&](int h) {
-    floatx4 t = floatx4{0.f, 0.f, 0.f, 0.f};
-    if (lane + 64 * h < EQ)
-      for (int w = 0; w < NW; ++w) t += *reinterpret_cast<const floatx4*>(colred + w * HID + 4 * (lane + 64 * h));
-    return t;
-  };
-  put(s1);
-  __syncthreads();
-  floatx4 t1[2] = {total(0), total(1)};
-  __syncthreads();
-  if constexpr (MODE == AVR_BN_FWD) {
-    const float rn = 1.0f / (float)nvalid;
-    t1[0] *= rn;                             // this workgroup's column means
-    t1[1] *= rn;
-#pragma unroll
-    for (int i = 0; i < MAXQ; ++i) {
-      const int r = wid + NW * (i >> 1);
-      if (r < nvalid) {
-        const floatx4 d = yv[i] - t1[i & 1];
-        s2[i & 1] += d * d;
-      }
-    }
-  }
-  put(s2);
-  __syncthreads();
-  if (wid == 0) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const floatx4 t2 = total(h);
-      const int f = 4 * (lane + 64 * h);
-      if (f < HID) {
-        *reinterpret_cast<floatx4*>(part + f) = t1[h];
-        *reinterpret_cast<floatx4*>(part + HID + f) = t2;
-      }
+    for (int ft = 0; ft < FT; ++ft) {
+      *reinterpret_cast<floatx4*>(part + feat(ft)) = s1[ft];
+      *reinterpret_cast<floatx4*>(part + HID + feat(ft)) = s2[ft];
     }
   }
 }
 
-template <int FT, int NW, int MODE>
+template <int FT, int NW, int MODE, int KK>
 static int launch_bn_layer(const BnArgs& a, hipStream_t s) {
-  // the larger of the prologue's and the epilogue's fp32 stage (X aliases them) + the column sums + red
-  constexpr int HID = 16 * FT * NW;
-  const size_t stage = (size_t)kX3Samples * ((a.K > HID ? a.K : HID) + 4) * 4;
-  const size_t shm = stage + (size_t)NW * HID * 4 + 64;
+  const size_t shm = (size_t)64 * KK * 4 + 64;   // X (64 samples x KK x hi + lo fp16) + the wave maxima
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&bn_layer_kernel<FT, NW, MODE>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kX3Samples * (512 + 4) * 4 + NW * HID * 4 + 64) != hipSuccess)
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&bn_layer_kernel<FT, NW, MODE, KK>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
       return fail(AVR_E_HIP, "bn_layer_kernel: cannot set dynamic LDS");
     attr = true;
   }
   const int64_t blocks = (a.M + kX3Samples - 1) / kX3Samples;
   AVR_REQUIRE(blocks < (1ll << 31), "avr_bn_layer_run: too many rows");
-  bn_layer_kernel<FT, NW, MODE><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
+  bn_layer_kernel<FT, NW, MODE, KK><<<(unsigned)blocks, 64 * NW, shm, s>>>(a);
   return check_launch("bn_layer_kernel");
+}
+
+// K is lin_in's 64 (forward) or d_hidden
+template <int FT, int NW, int MODE>
+static int launch_bn_layer_k(const BnArgs& a, hipStream_t s) {
+  constexpr int HID = 16 * FT * NW;
+  if (a.K == HID) return launch_bn_layer<FT, NW, MODE, HID>(a, s);
+  if constexpr (MODE == AVR_BN_FWD && HID != 64) {
+    if (a.K == 64) return launch_bn_layer<FT, NW, MODE, 64>(a, s);
+  }
+  return fail(AVR_E_UNSUPPORTED, "avr_bn_layer_run: in_dim %d with d_hidden %d", a.K, HID);
 }
 
 template <int MODE>
 static int dispatch_bn_layer(int H, const BnArgs& a, hipStream_t s) {
   switch (H) {
-    case 64: return launch_bn_layer<1, 4, MODE>(a, s);
-    case 128: return launch_bn_layer<2, 4, MODE>(a, s);
-    case 256: return launch_bn_layer<4, 4, MODE>(a, s);
-    case 512: return launch_bn_layer<4, 8, MODE>(a, s);
+    case 64: return launch_bn_layer_k<1, 4, MODE>(a, s);
+    case 128: return launch_bn_layer_k<2, 4, MODE>(a, s);
+    case 256: return launch_bn_layer_k<4, 4, MODE>(a, s);
+    case 512: return launch_bn_layer_k<4, 8, MODE>(a, s);
   }
   return fail(AVR_E_UNSUPPORTED, "avr_bn_layer_run: d_hidden %d", H);
 }
@@ -582,7 +655,8 @@ extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* 
   a.KC = l->in_dim / 32;
   AVR_REQUIRE(l->in_dim % 64 == 0 && l->in_dim >= 64 && l->in_dim <= 512 && l->in_dim / 4 % (H == 512 ? 8 : 4) == 0,
               "avr_bn_layer_run: in_dim %d", l->in_dim);
-  AVR_REQUIRE(l->in_valid > 0 && l->in_valid <= l->in_dim, "avr_bn_layer_run: in_valid %d", l->in_valid);
+  AVR_REQUIRE(l->in_valid > 0 && l->in_valid <= l->in_dim && (l->in_valid == l->in_dim || l->in_dim == 64),
+              "avr_bn_layer_run: in_valid %d (< in_dim only for lin_in's 64 columns)", l->in_valid);
   AVR_REQUIRE(l->src && l->out && l->partial && l->blob, "avr_bn_layer_run: null pointer");
   AVR_REQUIRE(l->ld_src >= l->in_valid && l->ld_src % 4 == 0,
               "avr_bn_layer_run: ld_src %lld (>= in_valid, a multiple of 4: 16-B rows)", (long long)l->ld_src);
