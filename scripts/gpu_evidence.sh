@@ -8,13 +8,14 @@
 #   train  bench.py --mode train for each conf in CONFS (+ TRAIN_ARGS)      -> $OUT/bench_train_<conf>.log
 #   tprof  rocprofv3 kernel stats of the HIP train step (CONFS' last conf)  -> $OUT/train_kernel_stats.csv
 #   trainx the --bn and the AdaptiveVolumeRenderer train steps (default_mv) -> $OUT/bench_train_{bn,adaptive}_mv.log
+#   bprof  rocprofv3 kernel stats of the --bn HIP train step (default_mv)   -> $OUT/train_bn_kernel_stats.csv
 # env: TAG (default r04), STEPS (default all), PYTEST_ARGS (extra pytest args, e.g. "-k philox"), CONFS.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r04}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
-STEPS=${STEPS:-tests smoke bench prof train tprof trainx}
+STEPS=${STEPS:-tests smoke bench prof train tprof trainx bprof}
 CONFS=${CONFS:-default default_mv}
 export AVR_TEST_REPORT=$OUT/philox_c3_flip_rates.jsonl
 has() { [[ " $STEPS " == *" $1 "* ]]; }
@@ -58,4 +59,13 @@ if has trainx; then
     rc=$?; tail -1 $OUT/bench_train_${x%%:*}_mv.log | cut -c1-300; echo; [ $rc -eq 0 ] || { echo "train ${x%%:*} rc=$rc"; exit $rc; }
   done
 fi
+if has bprof; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/bprof -o train -- python bench.py --mode train \
+    --conf default_mv --bn --train-modes hip --steps 10 --warmup 3 > $OUT/bprof.log 2>&1
+  rc=$?; [ $rc -eq 0 ] || { echo "bn train rocprof rc=$rc"; tail -5 $OUT/bprof.log; exit $rc; }
+  cp "$(find $OUT/bprof -name '*kernel_stats.csv' | head -1)" $OUT/train_bn_kernel_stats.csv
+  head -4 $OUT/train_bn_kernel_stats.csv | cut -c1-160
+fi
+# the traces stay on the box (gpurun copies back at most 64 MiB)
+find $OUT -name '*kernel_trace.csv' -delete; find $OUT -name '*_results.db' -delete
 exit 0
