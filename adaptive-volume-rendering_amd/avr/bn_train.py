@@ -234,8 +234,11 @@ class _FieldTrainBN(torch.autograd.Function):
             Gx = torch.empty(nb + 1, M, H, device=dev, dtype=F32)      # d loss / d X[k]
             # relu backward of lin_out's input in one pass (aten threshold_backward: g where X > 0, else 0)
             Gx[nb] = torch.ops.aten.threshold_backward(d4 @ P["lin_out.weight"].detach().to(F32), X[nb], 0.0)
-            gmax = torch.zeros(2 * nb + 2, device=dev, dtype=torch.int32)   # Gx[k] maxima (k = 0..nb), then DN's
-            gmax[nb:nb + 1] = _max_bits(Gx[nb])
+            # Gx[k] maxima (k = 0..nb): Gx[nb]'s published by fc_1[nb-1]^T's operand pass, the others by the GRAD
+            # prologues that build them and avr_bn_grad_rows
+            gmax = torch.zeros(2 * nb + 2, device=dev, dtype=torch.int32)
+            if nb == 0:
+                gmax[0:1] = _max_bits(Gx[0])
             DN = torch.empty(max(nb, 1), M, H, device=dev, dtype=F32)  # d loss / d fc_0 output (pre-BN)
             dn_max = torch.zeros(max(nb, 1), device=dev, dtype=torch.int32)
             gp2 = torch.empty(M, H, device=dev, dtype=F32)
@@ -249,7 +252,7 @@ class _FieldTrainBN(torch.autograd.Function):
             for b in range(nb - 1, -1, -1):
                 # fc_1[b]^T: operand = Gx[b+1] (for b < nb-1 built in the prologue from block b+1's BN backward)
                 if b == nb - 1:
-                    pro = dict(prologue=_lib.BN_PLAIN, src=Gx[nb], ld_src=H)
+                    pro = dict(prologue=_lib.BN_PLAIN, src=Gx[nb], ld_src=H, operand_max=gmax[nb:])
                 else:
                     c = gs1[b + 1]
                     pro = dict(prologue=_lib.BN_GRAD, src=gp1[b + 1], ld_src=H, src_pre=X[b + 1], src_res=Gx[b + 2],
