@@ -1,7 +1,6 @@
 """Diagnostic: one avr_bn_layer_run launch (the BatchNorm / layer-by-layer training GEMM) timed alone at the --bn
 step's row count, per d_hidden and layer kind: us per launch, HBM bytes per launch (the rows each reads and writes) and the x3 MFMA work, as fractions of 8 TB/s and 833 TF.
 usage: python scripts/bn_layer_bench.py [rows]"""
-import ctypes
 import os
 import sys
 
@@ -67,7 +66,6 @@ def main():
             print(f"H {H:3d} {name:42s}: {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s ({nbytes / us / 1e3 / 8000:.3f} of "
                   f"8 TB/s)  {flops / us / 1e6:6.1f} TF/s fp32-eq ({flops / us / 1e6 / 833.3:.3f} of the x3 peak)",
                   flush=True)
-    _ = ctypes
 
 
 if __name__ == "__main__":
