@@ -1,7 +1,7 @@
 """Isolated timing of avr_weight_grads on a training step's layer list: WG_CONF=default (the fine pass of
 conf/default.conf: 9 hidden 512 x 512 layers) or default_mv (train.py's conf/default_mv.conf: 13), plus lin_in
 (512 x 44) and lin_out (4 x 512), M = 4 scenes x 512 rays x 96 samples. WG_SPLITS="a,b,..." times explicit K-splits
-beside the library's own choice. Prints ms per call and TFLOP/s (fp32-equivalent). Diagnostic only."""
+beside the library's own choice; WG_THIN=0 leaves out lin_in / lin_out. Prints ms per call and TFLOP/s (fp32-equivalent). Diagnostic only."""
 import os
 import sys
 import time
@@ -24,8 +24,10 @@ def main():
     d4 = torch.randn(M, 4, generator=g).to(dev)
     mb = ops._max_bits
     layers = [(Gs[i % 7], Xs[i % 8], mb(Gs[i % 7]), mb(Xs[i % 8]), i < 6) for i in range(n_hidden)]
-    layers += [(Gs[6], zf, mb(Gs[6]), mb(zf), True), (d4, Xs[7], mb(d4), mb(Xs[7]), True)]
-    flops = 2.0 * M * (n_hidden * 512 * 512 + 512 * 44 + 4 * 512)
+    thin = os.environ.get("WG_THIN", "1") == "1"   # WG_THIN=0: without lin_in / lin_out (their tiles' cost)
+    if thin:
+        layers += [(Gs[6], zf, mb(Gs[6]), mb(zf), True), (d4, Xs[7], mb(d4), mb(Xs[7]), True)]
+    flops = 2.0 * M * (n_hidden * 512 * 512 + (512 * 44 + 4 * 512 if thin else 0))
     splits = [None] + [int(x) for x in os.environ.get("WG_SPLITS", "").split(",") if x]
     for n in splits:
         ops.weight_grads(layers, M, n_split=n)
@@ -35,7 +37,7 @@ def main():
             ops.weight_grads(layers, M, n_split=n)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / reps
-        print(f"M={M} hidden={n_hidden} n_split={n or 'auto'} weight_grads {dt * 1e3:.3f} ms/call (incl. partial sums) "
+        print(f"M={M} hidden={n_hidden} thin={int(thin)} n_split={n or 'auto'} weight_grads {dt * 1e3:.3f} ms/call (incl. partial sums) "
               f"{flops / dt / 1e12:.1f} TFLOP/s fp32-eq", flush=True)
 
 
