@@ -99,6 +99,7 @@ CASES = [  # d_hidden, n_blocks, d_latent, combine_layer, SB, NS, spade, combine
     (128, 4, 128, 2, 1, 3, False, "max"),
     (64, 3, 64, 2, 2, 2, True, "average"),
     (64, 3, 64, 2, 2, 2, True, "max"),
+    (256, 3, 64, 2, 2, 2, True, "max"),
     (512, 5, 512, 3, 1, 2, True, "average"),
 ]
 

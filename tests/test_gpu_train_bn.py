@@ -92,7 +92,7 @@ def _grads_bn(net, xyz, vd, w, coarse, hip, latent_grad=False):
 
 
 @pytest.mark.parametrize("d_hidden,n_blocks,combine_layer,sb,n", [(64, 3, 1000, 1, 1000), (128, 5, 3, 2, 700),
-                                                                  (512, 3, 1000, 1, 512),
+                                                                  (256, 3, 2, 2, 333), (512, 3, 1000, 1, 512),
                                                                   (512, 5, 3, 1, 1536)])
 def test_bn_training_grads_match_fp64(d_hidden, n_blocks, combine_layer, sb, n):
     from avr.bn_train import bn_train_eligible
