@@ -229,6 +229,57 @@ __device__ __forceinline__ void save_layer(const FieldArgs& a, int layer, const 
   for (int q = 0; q < MW; ++q) mk[q * 64] = bits[q];
 }
 
+// Training forward on the 8-wave layout (d_hidden 512: FT 4 x NW 8, two waves per SIMD as in inference; the
+// 4-wave layout's materialised layer input v does not fit its 256 registers): the two-pass publish of
+// act(acc * f [+ b]) also stores each value as its act row and its relu mask bit, the bits in the 4-wave
+// layout's mask words (field_bwd_x3_kernel<8, 4> reads them: the 16-feature tile 4 wid + ft is tile
+// 4 (wid & 1) + ft of 4-wave wave wid >> 1, word 2 (wid & 1) + ft / 2 there); the workgroup's max goes to *lmax.
+template <int FT, int NW, bool BIAS>
+__device__ __forceinline__ float publish_affine_save(uint4* X16, const floatx4 (&acc)[FT][4], float f,
+                                                     const floatx4 (&bv)[FT], float mx, float* red, int wid, int lane,
+                                                     int g, int j, const FieldArgs& a, int layer, int64_t base,
+                                                     int64_t roff, float* lmax) {
+  static_assert(FT == 4 && NW == 8, "8-wave training forward: d_hidden 512");
+  constexpr int HID = 16 * FT * NW;
+  if (lane == 0) red[wid] = mx;
+  lds_barrier();
+  const float m = red_max<NW>(red);
+  if (wid == 0 && lane == 0) *lmax = m;
+  const float s_x = pow2_scale_for(m);
+  char* xb = reinterpret_cast<char*>(X16);
+  // the tile's rows from a wave-uniform base, 32-bit lane offsets recomputed here from an opaque lane id (hoisted
+  // out of the block loop, the per-row addresses would stay live across it and spill)
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+  g = ln >> 4;
+  j = ln & 15;
+  float* act = a.act + (int64_t)layer * a.act_stride + (roff + base) * HID;
+  const int nval = a.M - base < 64 ? (int)(a.M - base) : 64;
+  unsigned bits[2] = {0u, 0u};
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    const int ftg = FT * wid + ft;
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      const floatx4 y = relu_affine<BIAS, 0>(acc[ft][sg], f, bv[ft]);
+      uint2 hi, lo;
+      split4(y, s_x, hi, lo);
+      const int s = 16 * sg + j;
+      *reinterpret_cast<uint2*>(xb + xidx(ftg >> 1, 0, g, s) * 16 + (ftg & 1) * 8) = hi;
+      *reinterpret_cast<uint2*>(xb + xidx(ftg >> 1, 1, g, s) * 16 + (ftg & 1) * 8) = lo;
+      if (s < nval) __builtin_nontemporal_store(y, reinterpret_cast<floatx4*>(act + (unsigned)(s * HID + 16 * ftg + 4 * g)));
+      const int idx = (ft * 4 + sg) * 4;
+      bits[idx >> 5] |= ((y.x > 0.f ? 1u : 0u) | (y.y > 0.f ? 2u : 0u) | (y.z > 0.f ? 4u : 0u) | (y.w > 0.f ? 8u : 0u))
+                        << (idx & 31);
+    }
+  }
+  unsigned* mk = a.mask + ((((int64_t)layer * gridDim.x + blockIdx.x) * 4 + (wid >> 1)) * 4 + 2 * (wid & 1)) * 64 + ln;
+  mk[0] = bits[0];
+  mk[64] = bits[1];
+  lds_barrier();
+  return s_x;
+}
+
 // Work split: NW waves (4: one per SIMD; 8: two per SIMD, which doubles the
 // VALU issue rate of the epilogues and hides one wave's stalls behind the
 // other); wave w owns the FT 16-row feature tiles FT*w .. FT*w + FT-1.
@@ -249,7 +300,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
   // 8 waves (256 registers each): two-pass epilogues instead of a materialised layer input v
   constexpr bool TWO = NW > 4;
   constexpr int NPF = TWO ? FT : kPrefetch;   // chunk-0 weight tiles loaded ahead of each layer's publish
-  static_assert(!(SAVE && TWO), "the training forward keeps the 4-wave layout");
+  static_assert(!(SAVE && TWO) || (FT == 4 && ACT == 0 && !SPADE), "8-wave training forward: ReLU, d_hidden 512");
   static_assert(!(SAVE && BN), "BatchNorm nets train on the module path");
   static_assert(!(SAVE && SPADE) && !(BN && SPADE), "use_spade: inference without BatchNorm only");
   static_assert(ACT == 0 || !BN, "Softplus: without BatchNorm only");
@@ -314,7 +365,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
         *reinterpret_cast<int4*>(tail->tex + 4 * s) = make_int4(geo.bl.tex[0], geo.bl.tex[1], geo.bl.tex[2], geo.bl.tex[3]);
         *reinterpret_cast<float4*>(tail->w + 4 * s) = make_float4(geo.bl.w[0], geo.bl.w[1], geo.bl.w[2], geo.bl.w[3]);
       }
-  #pragma unroll
+#pragma unroll
       for (int d = 0; d < 3; ++d) { xr[d] = geo.xr[d]; vr[d] = geo.vr[d]; }
     }
     AVR_STAMP(27);
@@ -329,7 +380,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       // npe are zeroed; the rare |argument| > 8192 takes sinf (uniform branch)
       float arg[PES];
       bool big = false;
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < PES; ++i) {
         const int q = gg + NW * i, jj = q / 3, dd = q - 3 * jj;
         const float x = dd == 0 ? xr[0] : (dd == 1 ? xr[1] : xr[2]);
@@ -340,11 +391,11 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
         big |= q < npe && fabsf(arg[i]) > 8192.f;
       }
       if (__builtin_expect(__any(big), 0)) {
-  #pragma unroll
+#pragma unroll
         for (int i = 0; i < PES; ++i)
           if (fabsf(arg[i]) > 8192.f) pe[i] = sinf(arg[i]);
       }
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < PES; ++i) {
         pe[i] = gg + NW * i < npe ? pe[i] : 0.f;
         mx = fmaxf(mx, fabsf(pe[i]));
@@ -362,7 +413,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       const int64_t m = base + 16 * (wid & 3) + j;
       if (m < a.M) {
         float* zr = a.zf + (roff + m) * a.zf_ld;
-  #pragma unroll
+#pragma unroll
         for (int i = 0; i < PES; ++i)
           if (gg + NW * i < npe) __builtin_nontemporal_store(pe[i], zr + 3 + gg + NW * i);
         if (gg < 3) {
@@ -387,7 +438,7 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
         *reinterpret_cast<_Float16*>(xb + xidx(c, 0, gg, s) * 16 + 2 * e) = hi;
         *reinterpret_cast<_Float16*>(xb + xidx(c, 1, gg, s) * 16 + 2 * e) = (_Float16)(y - (float)hi);
       };
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < PES; ++i)
         if (gg + NW * i < npe) put(3 + gg + NW * i, pe[i]);
       if (gg < 3) { put(gg, xo); put(3 + npe + gg, vo); }
@@ -397,10 +448,10 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     AVR_STAMP(2);
     // ---- lin_in: h = (b_in + W_in . X) * S_h ; h stays scaled by S_h
     S_h = layer_scale(a.packed, L, 0) * s_x;
-  #pragma unroll
+#pragma unroll
     for (int ft = 0; ft < FT; ++ft) {
       const floatx4 b = *reinterpret_cast<const floatx4*>(a.packed + L.b_in + 16 * (FT * wid + ft) + 4 * g);
-  #pragma unroll
+#pragma unroll
       for (int sg = 0; sg < 4; ++sg) h[ft][sg] = b * S_h;
     }
     AVR_STAMP(3);
@@ -502,6 +553,9 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     if constexpr (TWO) {
       // the fc_1 bias loads are issued before the t publish, whose barriers cover their latency
       if constexpr (BN) s_x = publish_bn<FT, NW>(X16, h, 1.0f / S_h, bn_a, bn_c, mx, red, wid, lane, g, j);
+      else if constexpr (SAVE)
+        s_x = publish_affine_save<FT, NW, false>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j, a, 2 * b, base,
+                                                 roff, &tail->lmax[2 * b]);
       else s_x = publish_affine<FT, NW, false, ACT>(X16, h, 1.0f / S_h, bz, mx, red, wid, lane, g, j, beta);
       AVR_STAMP(6 + 5 * (b & 3));
       const float S_t = layer_scale(a.packed, L, 2 + 2 * b) * s_x;
@@ -515,7 +569,10 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
       load_bias<FT, true>(bb, a.packed + L.b_fc1[b], wid, g);
       prefetch_a<FT, NPF>(A0, W1, lane);
       if (b == 1) AVR_STAMP(21);
-      s_x = publish_affine<FT, NW, true, ACT>(X16, t, 1.0f / S_t, bv, mx, red, wid, lane, g, j, beta);
+      if constexpr (SAVE)
+        s_x = publish_affine_save<FT, NW, true>(X16, t, 1.0f / S_t, bv, mx, red, wid, lane, g, j, a, 2 * b + 1, base,
+                                                roff, &tail->lmax[2 * b + 1]);
+      else s_x = publish_affine<FT, NW, true, ACT>(X16, t, 1.0f / S_t, bv, mx, red, wid, lane, g, j, beta);
       AVR_STAMP(8 + 5 * (b & 3));
       // fc_1 accumulates onto the residual, rescaled to this layer's scale (+ b1)
       const float S1 = layer_scale(a.packed, L, 3 + 2 * b) * s_x;
@@ -586,19 +643,58 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
     const float mxw = act_bound<ACT>(max_relu_affine<FT, false>(h, f, bz), beta);
     const float s_w = pow2_scale_for(mxw);
     floatx4 part[4];
+    // SAVE: lin_out's input (layer 2 n_blocks) as act rows and mask bits (publish_affine_save's layout), the
+    // workgroup's max through red
+    unsigned sbits[2] = {0u, 0u};
+    const int lout = 2 * a.n_blocks;
+    if constexpr (SAVE) {
+      float* sact = a.act + (int64_t)lout * a.act_stride + (roff + base) * HID;
+      const int snval = a.M - base < 64 ? (int)(a.M - base) : 64;
 #pragma unroll
-    for (int sg = 0; sg < 4; ++sg) {
-      part[sg] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int sg = 0; sg < 4; ++sg) {
+        part[sg] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int cc = 0; cc < 2; ++cc) {
-        uint2 h0, l0, h1, l1;
-        split4(relu_affine<false, ACT>(h[2 * cc][sg], f, bz[0], beta), s_w, h0, l0);
-        split4(relu_affine<false, ACT>(h[2 * cc + 1][sg], f, bz[0], beta), s_w, h1, l1);
-        const half8 bh = __builtin_bit_cast(half8, make_uint4(h0.x, h0.y, h1.x, h1.y));
-        const half8 bl = __builtin_bit_cast(half8, make_uint4(l0.x, l0.y, l1.x, l1.y));
-        part[sg] = mfma32h(Aw[cc].hi, bh, part[sg]);
-        part[sg] = mfma32h(Aw[cc].hi, bl, part[sg]);
-        part[sg] = mfma32h(Aw[cc].lo, bh, part[sg]);
+        for (int cc = 0; cc < 2; ++cc) {
+          uint2 h0, l0, h1, l1;
+          const floatx4 y0 = relu_affine<false, ACT>(h[2 * cc][sg], f, bz[0], beta);
+          const floatx4 y1 = relu_affine<false, ACT>(h[2 * cc + 1][sg], f, bz[0], beta);
+          if constexpr (SAVE) {
+            const int srow = 16 * sg + j;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const floatx4 y = q ? y1 : y0;
+              const int ft = 2 * cc + q, ftg = FT * wid + ft;
+              if (srow < snval)
+                __builtin_nontemporal_store(y, reinterpret_cast<floatx4*>(sact + (unsigned)(srow * HID + 16 * ftg + 4 * g)));
+              const int idx = (ft * 4 + sg) * 4;
+              sbits[idx >> 5] |= ((y.x > 0.f ? 1u : 0u) | (y.y > 0.f ? 2u : 0u) | (y.z > 0.f ? 4u : 0u) |
+                                  (y.w > 0.f ? 8u : 0u)) << (idx & 31);
+            }
+          }
+          split4(y0, s_w, h0, l0);
+          split4(y1, s_w, h1, l1);
+          const half8 bh = __builtin_bit_cast(half8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+          const half8 bl = __builtin_bit_cast(half8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+          part[sg] = mfma32h(Aw[cc].hi, bh, part[sg]);
+          part[sg] = mfma32h(Aw[cc].hi, bl, part[sg]);
+          part[sg] = mfma32h(Aw[cc].lo, bh, part[sg]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        part[sg] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+          uint2 h0, l0, h1, l1;
+          split4(relu_affine<false, ACT>(h[2 * cc][sg], f, bz[0], beta), s_w, h0, l0);
+          split4(relu_affine<false, ACT>(h[2 * cc + 1][sg], f, bz[0], beta), s_w, h1, l1);
+          const half8 bh = __builtin_bit_cast(half8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+          const half8 bl = __builtin_bit_cast(half8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+          part[sg] = mfma32h(Aw[cc].hi, bh, part[sg]);
+          part[sg] = mfma32h(Aw[cc].hi, bl, part[sg]);
+          part[sg] = mfma32h(Aw[cc].lo, bh, part[sg]);
+        }
       }
     }
     const float un = 1.0f / (layer_scale(a.packed, L, 1) * s_w);
@@ -610,9 +706,23 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
         pbuf[wid * 64 + 16 * sg + j] = make_float4(o.x, o.y, o.z, o.w);
       }
     }
+    if constexpr (SAVE) {
+      unsigned* mk = a.mask + ((((int64_t)lout * gridDim.x + blockIdx.x) * 4 + (wid >> 1)) * 4 + 2 * (wid & 1)) * 64 +
+                     lane;
+      mk[0] = sbits[0];
+      mk[64] = sbits[1];
+      if (lane == 0) red[wid] = mxw;
+    }
     lds_barrier();
     AVR_STAMP(25);
     if (wid >= 4) return;
+    if constexpr (SAVE) {
+      // the layer maxima: one atomic per workgroup and layer (lin_out's input: the waves' maxima met in red)
+      const int nl = 2 * a.n_blocks + 1;
+      if (a.act_max && wid == 0 && lane < nl)
+        publish_max(a.act_max + lane, lane == nl - 1 ? red_max<NW>(red) : tail->lmax[lane]);
+      if (a.zf_max && threadIdx.x == 64) publish_max(a.zf_max, tail->zmax);
+    }
     const int s = 16 * wid + j;
     const int64_t m = base + s;
     if (g == 0 && m < a.M) {
@@ -803,6 +913,11 @@ static int x3_waves() {
   return (e && atoi(e) == 4) ? 4 : 8;
 }
 
+static int save_waves() {
+  const char* e = getenv("AVR_X3_SAVE_WAVES");
+  return (e && atoi(e) == 4) ? 4 : 8;
+}
+
 int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s) {
   // inference at d_hidden 512: 8 waves x 4 tiles (+2.7-4.7 % over the 4-wave layout on the same box);
   // AVR_X3_WAVES=4 selects the 4-wave layout (diagnostics)
@@ -844,6 +959,8 @@ int dispatch_field_x3(int d_hidden, const FieldArgs& a, hipStream_t s) {
     return fail(AVR_E_UNSUPPORTED, "field x3: d_hidden %d", d_hidden);
   }
   if (d_hidden == 512 && !a.act && x3_waves() == 8) return launch_x3<4, 8, false>(a, s);
+  // training forward at d_hidden 512: the 8-wave layout too (AVR_X3_SAVE_WAVES=4: the 4-wave one, A/B)
+  if (d_hidden == 512 && a.act && save_waves() == 8) return launch_x3<4, 8, true>(a, s);
   switch (d_hidden) {
     case 64: return a.act ? launch_x3<1, 4, true>(a, s) : launch_x3<1, 4, false>(a, s);
     case 128: return a.act ? launch_x3<2, 4, true>(a, s) : launch_x3<2, 4, false>(a, s);
