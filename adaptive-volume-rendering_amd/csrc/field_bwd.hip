@@ -33,11 +33,15 @@ __device__ __forceinline__ floatx4 masked(const floatx4& v, const unsigned* mb, 
   return r;
 }
 
+// (8 waves, d_hidden 512: the masks are in the 4-wave layout -- wave w's tile 4 w + ft is tile 4 (w & 1) + ft of
+// 4-wave wave w >> 1, its words 2 (w & 1) + q there)
 template <int FT, int NW>
 __device__ __forceinline__ void load_mask(unsigned (&mb)[mask_words(FT)], const unsigned* mask, int layer, int lane,
                                           int wid) {
   constexpr int MW = mask_words(FT);
-  const unsigned* mk = mask + (((int64_t)layer * gridDim.x + blockIdx.x) * NW + wid) * MW * 64 + lane;
+  const unsigned* mk = NW == 8 ? mask + ((((int64_t)layer * gridDim.x + blockIdx.x) * 4 + (wid >> 1)) * 4 +
+                                         2 * (wid & 1)) * 64 + lane
+                               : mask + (((int64_t)layer * gridDim.x + blockIdx.x) * NW + wid) * MW * 64 + lane;
 #pragma unroll
   for (int q = 0; q < MW; ++q) mb[q] = mk[q * 64];
 }
@@ -83,6 +87,26 @@ __device__ __forceinline__ RowSideH<HID> grad_side(const BwdArgs& a, int layer, 
   RowSideH<HID> rs;
   rs.template init<HID>(a.G + (int64_t)layer * a.g_stride + (roff + base) * HID, s_x, a.M - base, wid);
   return rs;
+}
+
+template <int HID>
+__device__ __forceinline__ RowSide8<HID> grad_side8(const BwdArgs& a, int layer, float s_x, int64_t base, int64_t roff,
+                                                    int wid) {
+  RowSide8<HID> rs;
+  rs.init8(a.G + (int64_t)layer * a.g_stride + (roff + base) * HID, s_x, a.M - base, wid);
+  return rs;
+}
+
+// the K loop of one backward GEMM: 4 waves (gemm_x3 with the row side task) or 8 (gemm_x3_sg_side)
+template <int FT, int NW, int HID>
+__device__ __forceinline__ void bwd_gemm(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* W, const uint4* X16,
+                                         int lane, const BwdArgs& a, int layer, float s_x, int64_t base, int64_t roff,
+                                         int wid) {
+  constexpr int KC = HID / 32, NTT = FT * NW;
+  if constexpr (NW == 8)
+    gemm_x3_sg_side<FT, true>(acc, A0, W, KC, 64 * NTT, X16, lane, grad_side8<HID>(a, layer, s_x, base, roff, wid));
+  else
+    gemm_x3<FT, true, false>(acc, A0, W, KC, 64 * NTT, X16, lane, grad_side<HID>(a, layer, s_x, base, roff, wid));
 }
 
 template <int FT>
@@ -162,10 +186,10 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
     // LDS during those GEMMs (RowSide), not stored as a burst ahead of the weight loads
     float mx = absmax<FT>(dx);
     const uint4* W1 = PB + a.LB.fc1t[b] / 4 + 2 * 64 * FT * wid;
-    prefetch_a<FT>(A0, W1, lane);
+    prefetch_a<FT, NW == 8 ? FT : kPrefetch>(A0, W1, lane);
     float s_x = publish<FT, NW>(X16, dx, mx, red, wid, lane, g, j, &lmax[2 * b + 1]);
     load_mask<FT, NW>(mb, a.mask, 2 * b + 1, lane, wid);
-    gemm_x3<FT, true, false>(t, A0, W1, KC, 64 * NTT, X16, lane, grad_side<HID>(a, 2 * b + 1, s_x, base, roff, wid));
+    bwd_gemm<FT, NW, HID>(t, A0, W1, X16, lane, a, 2 * b + 1, s_x, base, roff, wid);
     float inv = 1.0f / (bwd_scale(a.packed_bwd, 3 + 2 * b) * s_x);
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
@@ -175,10 +199,10 @@ __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
     mx = absmax<FT>(t);
     // ---- fc_0^T
     const uint4* W0 = PB + a.LB.fc0t[b] / 4 + 2 * 64 * FT * wid;
-    prefetch_a<FT>(A0, W0, lane);
+    prefetch_a<FT, NW == 8 ? FT : kPrefetch>(A0, W0, lane);
     s_x = publish<FT, NW>(X16, t, mx, red, wid, lane, g, j, &lmax[2 * b]);
     load_mask<FT, NW>(mb, a.mask, 2 * b, lane, wid);
-    gemm_x3<FT, true, false>(t, A0, W0, KC, 64 * NTT, X16, lane, grad_side<HID>(a, 2 * b, s_x, base, roff, wid));
+    bwd_gemm<FT, NW, HID>(t, A0, W0, X16, lane, a, 2 * b, s_x, base, roff, wid);
     inv = 1.0f / (bwd_scale(a.packed_bwd, 2 + 2 * b) * s_x);
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
@@ -213,13 +237,24 @@ static int launch_bwd(const BwdArgs& a, hipStream_t s) {
   return check_launch("field_bwd_x3_kernel");
 }
 
+// d_hidden 512, ReLU: 8 waves x 4 tiles, two waves per SIMD as the forward (AVR_X3_BWD_WAVES=4: the 4-wave
+// layout, A/B); Softplus keeps the 4-wave layout (its slopes come from the act rows)
+static int bwd_waves() {
+  const char* e = getenv("AVR_X3_BWD_WAVES");
+  return (e && atoi(e) == 4) ? 4 : 8;
+}
+
 template <int ACT>
 static int dispatch_bwd_act(int d_hidden, const BwdArgs& a, hipStream_t s) {
   switch (d_hidden) {
     case 64: return launch_bwd<1, 4, ACT>(a, s);
     case 128: return launch_bwd<2, 4, ACT>(a, s);
     case 256: return launch_bwd<4, 4, ACT>(a, s);
-    case 512: return launch_bwd<8, 4, ACT>(a, s);
+    case 512:
+      if constexpr (ACT == 0) {
+        if (bwd_waves() == 8) return launch_bwd<4, 8, ACT>(a, s);
+      }
+      return launch_bwd<8, 4, ACT>(a, s);
   }
   return fail(AVR_E_UNSUPPORTED, "field backward: d_hidden %d", d_hidden);
 }

@@ -261,6 +261,71 @@ __device__ __forceinline__ void gemm_x3_sg(floatx4 (&acc)[FT][4], FragX3 (&A0)[F
   }
 }
 
+// The 8-wave K loop with a side task (the backward chain's G rows, RowSide8): chunk_step_sg plus the task's LDS
+// read of chunk c in sample group 0 and its row stores in sample group 2.
+template <int FT, bool ZERO, typename Side>
+__device__ __forceinline__ void chunk_step_sg_side(floatx4 (&acc)[FT][4], const FragX3 (&A)[FT], FragX3 (&An)[FT],
+                                                   const uint4* __restrict__ wn, unsigned lo, BPair& B,
+                                                   const uint4* X16, int c, int cn, int g, int j, Side& side) {
+  static_assert(FT == 4, "one next-chunk tile per sample group");
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg) {
+    if (sg == 0) side.load(X16, c);
+    const BPair Bn = sg < 3 ? read_b(X16, c, sg + 1, g, j) : read_b(X16, cn, 0, g, j);
+    An[sg] = load_frag(wn + (lo + 2 * 64 * sg));
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      acc[ft][sg] = mfma32h(A[ft].hi, B.hi, ZERO ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[ft][sg]);
+      acc[ft][sg] = mfma32h(A[ft].hi, B.lo, acc[ft][sg]);
+      acc[ft][sg] = mfma32h(A[ft].lo, B.hi, acc[ft][sg]);
+    }
+    if (sg == 2) side.store(c);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    B = Bn;
+  }
+}
+
+template <int FT, bool ZERO, typename Side>
+__device__ __forceinline__ void gemm_x3_sg_side(floatx4 (&acc)[FT][4], FragX3 (&A0)[FT], const uint4* __restrict__ W,
+                                                int KC, int cstride, const uint4* X16, int lane, Side side) {
+  const int g = lane >> 4, j = lane & 15;
+  const unsigned lo = lane;
+  FragX3 A1[FT];
+  BPair B = read_b(X16, 0, 0, g, j);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int c = 0; c < KC; c += 2) {
+    const int c2 = c + 2 < KC ? c + 2 : c + 1;
+    const uint4* w1 = W + (int64_t)2 * (c + 1) * cstride;
+    const uint4* w2 = W + (int64_t)2 * c2 * cstride;
+    if (ZERO && c == 0)
+      chunk_step_sg_side<FT, true>(acc, A0, A1, w1, lo, B, X16, c, c + 1, g, j, side);
+    else
+      chunk_step_sg_side<FT, false>(acc, A0, A1, w1, lo, B, X16, c, c + 1, g, j, side);
+    chunk_step_sg_side<FT, false>(acc, A1, A0, w2, lo, B, X16, c + 1, c2, g, j, side);
+  }
+}
+
+// RowSide for 8 waves: waves w and w + 4 share sample 16 (w & 3) + j; wave w copies the K-chunks of parity w >> 2
+template <int HID>
+struct RowSide8 : RowSide {
+  int par;
+  __device__ __forceinline__ void init8(float* rows0, float s_x, int64_t nrows, int w) {
+    init<HID>(rows0, s_x, nrows, w & 3);
+    par = w >> 2;
+  }
+  __device__ __forceinline__ void load(const uint4* X16, int c) {
+    if ((c & 1) == par) RowSide::load(X16, c);
+  }
+  __device__ __forceinline__ void store(int c) {
+    if ((c & 1) == par) store_hid<HID>(c);
+  }
+};
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not
 // for its outstanding global loads (the next layer's weight prefetch stays in
 // flight; __syncthreads would drain it).
