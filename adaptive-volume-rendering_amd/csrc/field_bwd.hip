@@ -130,7 +130,6 @@ template <int FT, int NW, int ACT>
 __global__ void __launch_bounds__(64 * NW, 1) field_bwd_x3_kernel(BwdArgs a) {
   constexpr int HID = 16 * FT * NW;
   constexpr int KC = HID / 32;
-  constexpr int NTT = FT * NW;
   constexpr int MW = mask_words(FT);
   extern __shared__ float lds[];
   uint4* X16 = reinterpret_cast<uint4*>(lds);   // KC chunks x 8 KiB, the forward's operand layout
