@@ -471,7 +471,8 @@ class FusedField:
         gradients as GEMMs over the samples (see _FieldTrain)."""
         mlp = self._mlp(coarse)
         names = train_param_names(mlp)
-        params = [dict(mlp.named_parameters())[n] for n in names]
+        named = dict(mlp.named_parameters())   # once (a dict per name walked the module tree per parameter)
+        params = [named[n] for n in names]
         return _FieldTrain.apply(self, coarse, names, xyz, viewdirs, self.net.encoder.latent, *params)
 
 

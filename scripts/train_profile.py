@@ -2,7 +2,8 @@
 their input shapes and the Python call sites of the copies / cats / fills (what the kernel list calls
 direct_copy, CatArrayBatchedCopy, FillFunctor). Not part of the product or the bench.
 
-env: CONF (default_mv | default), STEPS, BN (1: train.py --bn), RENDERER (volume | adaptive: AdaptiveVolumeRenderer, train.py:268-273)
+env: CONF (default_mv | default), STEPS, BN (1: train.py --bn), RENDERER (volume | adaptive: AdaptiveVolumeRenderer, train.py:268-273),
+CPUSORT=1 (also the ops by host time)
 """
 import os
 import sys
@@ -63,6 +64,10 @@ with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_sh
     torch.cuda.synchronize()
 print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_device_time_total", row_limit=45,
                                                          max_name_column_width=40, max_shapes_column_width=70))
+if os.environ.get("CPUSORT") == "1":   # host time: what keeps the GPU waiting between launches
+    print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=40, max_name_column_width=60))
+    print(prof.key_averages(group_by_stack_n=4).table(sort_by="cpu_time_total", row_limit=30,
+                                                      max_name_column_width=40, max_src_column_width=120))
 for name in ("aten::copy_", "aten::cat", "aten::fill_", "aten::zero_", "aten::abs", "aten::amax", "aten::max"):
     print(f"==== {name} by stack")
     print(prof.key_averages(group_by_stack_n=6).table(sort_by="self_device_time_total", row_limit=8,
