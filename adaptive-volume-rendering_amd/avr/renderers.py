@@ -276,8 +276,12 @@ class _LSTMMarch(nn.Module):
     def _initial_distance(self, SB, num_rays, device, noise):
         if noise is not None and "initial_distance" in noise:
             return noise["initial_distance"].reshape(SB, num_rays, 1).to(device)
-        # renderers.py:322 / :402: drawn on the CPU generator, then moved
-        return torch.zeros((SB, num_rays, 1)).normal_(mean=0.8, std=5e-2).to(device)
+        # renderers.py:322 / :402: drawn on the CPU generator, then moved -- through pinned memory, asynchronously:
+        # a pageable host-to-device copy waits for the stream to drain, a bubble in every training step
+        d = torch.zeros((SB, num_rays, 1)).normal_(mean=0.8, std=5e-2)
+        if torch.device(device).type != "cuda":
+            return d.to(device)
+        return d.pin_memory().to(device, non_blocking=True)
 
     def _gate_table(self, phi):
         lat = phi.encoder.latent
