@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p

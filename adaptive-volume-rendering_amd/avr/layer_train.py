@@ -10,15 +10,18 @@ statistics: the operand is relu(x), the backward's mask [pre > 0]) and does the 
 the rows:
   forward   X[0] = lin_in(z_feature); per block b: (b < combine_layer) X'[b] = S_b * X[b] + T_b with T_b / S_b the
             bilinear blends of the per-texel lin_z / scale_z tables (avr_latent_features on the x3 tables:
-            both carry their biases with use_spade; without it T_b has none and lin_z's bias is folded into the
-            producing layer's bias); (b == combine_layer, NS > 1) X'[b] = combine(X[b]); N[b] = fc_0(relu(X'[b]));
+            both carry their biases with use_spade; without it T_b has none, lin_z's bias is folded into the
+            producing layer's bias and T_b is gathered in that layer's epilogue, avr_bn_layer's lin_z_table); (b == combine_layer, NS > 1) X'[b] = combine(X[b]); N[b] = fc_0(relu(X'[b]));
             X[b+1] = fc_1(relu(N[b])) + X'[b]; out = lin_out(relu(X[nb])), sigmoid / relu.
-  backward  the transposed layers on avr_bn_layer_run (W^T . g masked by [pre > 0]), the spade product rule
+  backward  the transposed layers on avr_bn_layer_run (W^T . g masked by [pre > 0]; fc_0^T adds the residual's
+            g in its epilogue), the spade product rule
             (d X = S * g, d S = g * X, d T = g) and torch's own adjoint of the combine between them; every weight
             gradient on avr_weight_grads (split-K x3; relu(X) rebuilt from the pre-activation rows in the
             staging), scale_z's against (g * X) rows; the latent / point gradients through the input functions
             as in avr.field._FieldTrain.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -114,7 +117,18 @@ class _FieldTrainLayers(torch.autograd.Function):
             zfp = torch.zeros(M1, zs, device=dev, dtype=F32)
             zfp[:, :d_in] = zf
             tables = fused.tables_batch(coarse, K, fast=True)                     # (K, n_tables, HW, H)
-            T = [_gather(fused, tables[:, b].contiguous(), K, NS, p, B, H) for b in range(nz)]
+            # without use_spade, X'[b] = X[b] + T_b: the T rows gathered in the epilogue of the layer producing X[b]
+            # (avr_bn_layer's lin_z_table, as avr.bn_train; nz <= combine_layer, so X[b] is X'[b] and no T row is
+            # stored); use_spade's product, or more scenes than one launch takes, gathers them here
+            zk = not spade and 0 < nz and K <= _lib.AVR_MAX_SCENES
+            views = (ViewDesc * K)(*[fused.view(k, NS) for k in range(K)]) if zk else None
+
+            def lin_z(b):
+                if not zk or b >= nz:
+                    return {}
+                return dict(lin_z_table=tables[0, b], lin_z_scene_stride=tables.stride(0), xyz=p,
+                            views=ctypes.addressof(views), n_views=K, rows_per_scene=B)
+            T = [] if zk else [_gather(fused, tables[:, b].contiguous(), K, NS, p, B, H) for b in range(nz)]
             S = [_gather(fused, tables[:, nz + b].contiguous(), K, NS, p, B, H) for b in range(nz)] if spade else []
             lz_b = [P[f"lin_z.{b}.bias"].detach().to(F32) for b in range(nz)]
             fold = (lambda b: 0) if spade else (lambda b: lz_b[b] if b < nz else 0)   # biases in the tables?
@@ -128,11 +142,12 @@ class _FieldTrainLayers(torch.autograd.Function):
             rows = lambda b: M1 if b < cl else M2   # noqa: E731  (rows of block b)
             Xpre = [torch.empty(M1, H, device=dev, dtype=F32)]
             _run(dims, _layer(n_rows=M1, mode=_lib.BN_FWD, prologue=_lib.BN_PLAIN, in_dim=64, in_valid=d_in, src=zfp,
-                              ld_src=zs, blob=blob, layer=0, bias=b_in, out=Xpre[0], partial=part), stream)
+                              ld_src=zs, blob=blob, layer=0, bias=b_in, out=Xpre[0], partial=part, **lin_z(0)),
+                 stream)
             Xin, N = [], []
             for b in range(nb):
                 x = Xpre[b]
-                if b < nz:                                                  # models.py:583-588
+                if b < nz and not zk:                                       # models.py:583-588
                     x = torch.addcmul(T[b], S[b], x) if spade else x + T[b]
                 if b == cl and NS > 1:
                     x = combine_interleaved(x, (NS, B), mlp.combine_type).reshape(M2, H)
@@ -148,7 +163,7 @@ class _FieldTrainLayers(torch.autograd.Function):
                 _run(dims, _layer(n_rows=m, mode=_lib.BN_FWD, prologue=_lib.BN_RELU, in_dim=H, in_valid=H, src=N[b],
                                   ld_src=H, in_mu=idt.zero, in_scale=idt.one, in_shift=idt.zero,
                                   operand_max=amax[2 * b + 1:], blob=blob, layer=3 + 2 * b, bias=b1[b], add1=x,
-                                  out=Xpre[b + 1], partial=part), stream)
+                                  out=Xpre[b + 1], partial=part, **lin_z(b + 1)), stream)
             a_out = torch.relu(Xpre[nb])
             raw = torch.addmm(P["lin_out.bias"].detach().to(F32), a_out, P["lin_out.weight"].detach().to(F32).t())
             out = torch.cat([torch.sigmoid(raw[:, :3]), torch.relu(raw[:, 3:4])], -1).reshape(SB, B, 4)
@@ -201,15 +216,15 @@ class _FieldTrainLayers(torch.autograd.Function):
                                   ld_src=H, operand_max=omax[2 * b + 1:], blob=bwd, layer=3 + 2 * b, out=gp2,
                                   pre_rows=N[b], out_mu=idt.zero, out_invstd=idt.one, out_scale=idt.one,
                                   out_shift=idt.zero, partial=part), stream)
-                gp1 = torch.empty(m, H, device=dev, dtype=F32)
+                # fc_0^T, the residual's g added in its epilogue: d loss / d X'[b] (residual + fc_0 path)
+                gin = torch.empty(m, H, device=dev, dtype=F32)
                 _run(dims, _layer(n_rows=m, mode=_lib.BN_BWD, prologue=_lib.BN_PLAIN, in_dim=H, in_valid=H, src=gp2,
-                                  ld_src=H, operand_max=omax[2 * b:], blob=bwd, layer=2 + 2 * b, out=gp1,
+                                  ld_src=H, operand_max=omax[2 * b:], blob=bwd, layer=2 + 2 * b, out=gin,
                                   pre_rows=Xin[b], out_mu=idt.zero, out_invstd=idt.one, out_scale=idt.one,
-                                  out_shift=idt.zero, partial=part), stream)
+                                  out_shift=idt.zero, add1=g, partial=part), stream)
                 relu_x = (idt.zero, idt.one, idt.zero)     # X = relu(rows), rebuilt in the staging
                 blk[b] = [(gp2, Xin[b], omax[2 * b:2 * b + 1], amax[2 * b:2 * b + 1], True, relu_x),
                           (g, N[b], omax[2 * b + 1:2 * b + 2], amax[2 * b + 1:2 * b + 2], True, relu_x)]
-                gin = g + gp1                                  # d loss / d X'[b] (residual + fc_0 path)
                 if b == cl and NS > 1:                         # torch's adjoint of the views' combine
                     with torch.enable_grad():
                         xr = Xpre[b].detach().requires_grad_(True)
@@ -226,6 +241,7 @@ class _FieldTrainLayers(torch.autograd.Function):
             g_in0 = g                                          # d loss / d lin_in output
             for b in range(nb):
                 (wl1 if b < cl else wl2).extend(blk[b])
+            g_in0_max = _max_bits(g_in0)                       # (without use_spade also Gz[0]'s: the same rows)
             lat_feat = None
             if nz > 0:
                 hwc = fused.latent_hwc_all(latent)
@@ -234,11 +250,11 @@ class _FieldTrainLayers(torch.autograd.Function):
                 lat_feat = _gather(fused, hwc, K, NS, p, B, net.d_latent)
                 lat_max = fused.latent_max_bits(latent)
                 for b in range(nz):
-                    wl1.append((Gz[b], lat_feat, Gz_max[b] if Gz_max[b] is not None else _max_bits(Gz[b]), lat_max,
-                                True))
+                    zmax = Gz_max[b] if Gz_max[b] is not None else g_in0_max if Gz[b] is g_in0 else _max_bits(Gz[b])
+                    wl1.append((Gz[b], lat_feat, zmax, lat_max, True))
                 for b in range(nz if spade else 0):
                     wl1.append((Gs[b], lat_feat, _max_bits(Gs[b]), lat_max, True))
-            wl1.append((g_in0, zfp, _max_bits(g_in0), _max_bits(zfp), True))
+            wl1.append((g_in0, zfp, g_in0_max, _max_bits(zfp), True))
             wl2.append((d4, a_out, _max_bits(d4), _max_bits(a_out), True))
             if M1 == M2:     # one source view: every layer over the same rows, one launch
                 r = weight_grads(wl1 + wl2, M1)

@@ -427,6 +427,14 @@ __global__ void __launch_bounds__(64 * NW, NW > 4 ? 1 : 2) bn_layer_kernel(BnArg
       s1[ft] = sum16(s1[ft]);
       s2[ft] = sum16(s2[ft]);
     }
+    if (a.add1) {   // a residual gradient added to the stored rows (the statistics are of gp alone)
+      floatx4 t[FT][4];
+      load_rows(a.add1, t);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg) acc[ft][sg] += t[ft][sg];
+    }
     store_rows(a.out, acc);
   }
   if (j == 0) {
@@ -700,8 +708,10 @@ extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* 
     if ((rc = field_bwd_layout(dims, &LB))) return rc;
     a.w = l->blob + (ly % 2 == 0 ? LB.fc0t[(ly - 2) / 2] : LB.fc1t[(ly - 2) / 2]);
     hdr = reinterpret_cast<const unsigned*>(l->blob);
+    AVR_REQUIRE(!l->add2 && !l->lin_z_table, "avr_bn_layer_run: AVR_BN_BWD adds add1 only");
     a.pre_rows = l->pre_rows; a.out_mu = l->out_mu; a.out_invstd = l->out_invstd;
     a.out_scale = l->out_scale; a.out_shift = l->out_shift;
+    a.add1 = l->add1;
   }
   a.hdr = hdr;
   a.hdr_idx = ly;

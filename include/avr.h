@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 13
+#define AVR_ABI_VERSION 14
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -367,8 +367,9 @@ int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_s
  *     partial (n_wg, 2, out_dim) = per 64-row workgroup (mean, sum of squared deviations) of out's columns.
  *   mode AVR_BN_BWD: gp = (W^T . op) * [(pre_rows - out_mu) * out_scale + out_shift > 0] with W^T from the
  *     backward blob (avr_field_pack_bwd): the relu mask of the forward's AVR_BN_RELU operand, recomputed from
- *     the pre-BN rows (ABI 12; the relu'd operands need not be stored); out = gp; partial = per workgroup
- *     (sum gp, sum gp * xhat), xhat = (pre_rows - out_mu) * out_invstd.
+ *     the pre-BN rows (ABI 12; the relu'd operands need not be stored); out = gp (+ add1: ABI 14, a residual
+ *     gradient, ld d_hidden; add2 / lin_z_table must be NULL); partial = per workgroup (sum gp, sum gp * xhat),
+ *     xhat = (pre_rows - out_mu) * out_invstd.
  *   The operand op (n_rows, in_dim), read from src (columns >= in_valid are 0):
  *     AVR_BN_PLAIN op = src;
  *     AVR_BN_RELU  op = relu((src - in_mu) * in_scale + in_shift)                 (forward: relu(bn_0(x)));
@@ -398,7 +399,7 @@ typedef struct {
   const float* in_m1; const float* in_m2; const float* in_invstd;
   float* operand_out; uint32_t* operand_max;
   const float* blob; int layer;
-  const float* bias; const float* add1; const float* add2;   /* AVR_BN_FWD (rows ld d_hidden) */
+  const float* bias; const float* add1; const float* add2;   /* AVR_BN_FWD; add1 also BWD (rows ld d_hidden) */
   float* out;                                                 /* (n_rows, d_hidden) */
   const float* pre_rows;                                      /* AVR_BN_BWD (ld d_hidden) */
   const float* out_mu; const float* out_invstd; const float* out_scale; const float* out_shift;

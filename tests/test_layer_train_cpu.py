@@ -88,11 +88,18 @@ def _install(monkeypatch, net):
             for k in ("add1", "add2"):
                 if kw.get(k) is not None:
                     out = out + kw[k]
+            if kw.get("lin_z_table") is not None:    # the T rows gathered in the epilogue (scene-major rows)
+                tz = kw["lin_z_table"]
+                tab = tz.as_strided((kw["n_views"],) + tuple(tz.shape), (kw["lin_z_scene_stride"],) + tz.stride())
+                out = out + gather(fused, tab, kw["n_views"], net.num_views_per_obj, kw["xyz"],
+                                   kw["rows_per_scene"], tz.shape[1])
         else:
             assert kw["prologue"] == _lib.BN_PLAIN
             op = src
             mask = torch.relu((kw["pre_rows"] - kw["out_mu"]) * kw["out_scale"] + kw["out_shift"]) > 0
             out = (src @ W) * mask
+            if kw.get("add1") is not None:           # the residual gradient (ABI 14)
+                out = out + kw["add1"]
         if kw.get("operand_max") is not None:     # publish max |operand| (float bits, max with what is there)
             m = torch.maximum(op.abs().max().reshape(1), kw["operand_max"][:1].view(torch.float32))
             kw["operand_max"][:1].copy_(m.view(torch.int32))
@@ -131,6 +138,16 @@ def _install(monkeypatch, net):
 ], ids=lambda c: f"h{c[0]}-nb{c[1]}-cl{c[3]}-sb{c[4]}-ns{c[5]}{'-spade' if c[6] else ''}-{c[7]}")
 @pytest.mark.parametrize("coarse", [True, False])
 def test_layer_train_logic_matches_autograd(monkeypatch, case, coarse):
+    _check(monkeypatch, case, coarse)
+
+
+def test_layer_train_gathered_lin_z_rows(monkeypatch):
+    """More scenes than one layer launch takes: the T rows gathered and added in torch (not in the epilogue)."""
+    monkeypatch.setattr(_lib, "AVR_MAX_SCENES", 3)
+    _check(monkeypatch, (16, 3, 64, 2, 2, 2, False, "average"), True)
+
+
+def _check(monkeypatch, case, coarse):
     d_hidden, n_blocks, d_latent, cl, SB, NS, spade, ctype = case
     net = _net(d_hidden, n_blocks, d_latent, cl, SB, NS, spade, ctype)
     fused = _install(monkeypatch, net)
