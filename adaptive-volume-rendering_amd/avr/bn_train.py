@@ -13,8 +13,9 @@ GEMM's prologue (avr_bn_grad_stats reduces the two means, dgamma and dbeta); the
 existing split-K x3 kernel (avr_weight_grads). The relu'd operands relu(bn_0(.)) are never stored: the
 backward's relu masks and the weight gradients' staging rebuild them from the pre-BN rows (ABI 12).
 
-The thin ends stay in torch: the z_feature input (positional encoding, models.py:763-789), lin_out's 4
-outputs with sigmoid / relu, and the input gradients (grid_sample adjoint), as in avr.field._FieldTrain.
+lin_out's 4 outputs with sigmoid / relu and their backward run as one pass over the rows each
+(avr_lin_out_fwd_rows / avr_lin_out_bwd_rows). The thin ends stay in torch: the z_feature input (positional
+encoding, models.py:763-789) and the input gradients (grid_sample adjoint), as in avr.field._FieldTrain.
 """
 import ctypes
 
@@ -134,6 +135,7 @@ class _FieldTrainBN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, fused, coarse, names, xyz, viewdirs, latent, *params):
+        from .ops import lin_out_rows
         net = fused.net
         mlp = fused._mlp(coarse)
         P = dict(zip(names, params))
@@ -198,21 +200,21 @@ class _FieldTrainBN(torch.autograd.Function):
                                   operand_max=amax[2 * b + 1:], blob=blob,
                                   layer=3 + 2 * b, bias=b1[b], add1=X[b], out=X[b + 1], partial=part,
                                   **lin_z(b + 1)), stream)
-            # lin_out on relu(x) (4 outputs; models.py:592), sigmoid rgb / relu sigma (models.py:856-862)
-            a_out = torch.relu(X[nb])
-            raw = torch.addmm(P["lin_out.bias"].detach().to(F32), a_out, P["lin_out.weight"].detach().to(F32).t())
-            out = torch.cat([torch.sigmoid(raw[:, :3]), torch.relu(raw[:, 3:4])], -1).reshape(SB, B, 4)
+            # lin_out on relu(x) (4 outputs; models.py:592), sigmoid rgb / relu sigma (models.py:856-862), and
+            # max relu(x) for its weight gradient's scale (relu(x) itself is not stored)
+            out, a_max = lin_out_rows(X[nb], P["lin_out.weight"].detach(), P["lin_out.bias"].detach())
+            out = out.reshape(SB, B, 4)
         ctx.fused, ctx.coarse, ctx.names, ctx.entry = fused, coarse, names, entry
-        ctx.keep = (X, N, amax, a_out, zfp, st1, st2, betas)
+        ctx.keep = (X, N, amax, a_max, zfp, st1, st2, betas)
         ctx.save_for_backward(xyz, viewdirs, latent, out, *params)
         return out
 
     @staticmethod
     def backward(ctx, grad_out):
-        from .ops import _max_bits, sum_of_products, weight_grads
+        from .ops import _max_bits, lin_out_rows_bwd, sum_of_products, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         fused, entry, names = ctx.fused, ctx.entry, ctx.names
-        X, N, amax, a_out, zfp, st1, st2, betas = ctx.keep
+        X, N, amax, a_max, zfp, st1, st2, betas = ctx.keep
         ctx.keep = None
         net = fused.net
         P = dict(zip(names, params))
@@ -228,12 +230,10 @@ class _FieldTrainBN(torch.autograd.Function):
         want_xyz = ctx.needs_input_grad[3]
         with torch.no_grad():
             bwd = fused.packed_bwd(ctx.coarse, entry)
-            y = out.reshape(M, 4)
-            go = grad_out.reshape(M, 4).to(F32)
-            d4 = torch.cat([go[:, :3] * ((1.0 - y[:, :3]) * y[:, :3]), go[:, 3:] * (y[:, 3:] > 0)], -1).contiguous()
             Gx = torch.empty(nb + 1, M, H, device=dev, dtype=F32)      # d loss / d X[k]
-            # relu backward of lin_out's input in one pass (aten threshold_backward: g where X > 0, else 0)
-            Gx[nb] = torch.ops.aten.threshold_backward(d4 @ P["lin_out.weight"].detach().to(F32), X[nb], 0.0)
+            # the activations' backward (d4), lin_out^T and its relu's backward (g where X > 0, else 0) in one pass
+            d4, _, d4_max = lin_out_rows_bwd(grad_out.reshape(M, 4), out.reshape(M, 4), P["lin_out.weight"].detach(),
+                                             X[nb], g=Gx[nb])
             # Gx[k] maxima (k = 0..nb): Gx[nb]'s published by fc_1[nb-1]^T's operand pass, the others by the GRAD
             # prologues that build them and avr_bn_grad_rows
             gmax = torch.zeros(2 * nb + 2, device=dev, dtype=torch.int32)
@@ -300,7 +300,9 @@ class _FieldTrainBN(torch.autograd.Function):
                 layers.append((Gx[b], lat_feat, gmax[b:b + 1], lat_max, True))
             zf_max = _max_bits(zfp)
             layers.append((Gx[0], zfp, gmax[0:1], zf_max, True))
-            layers.append((d4, a_out, _max_bits(d4), _max_bits(a_out), True))
+            ident = (torch.zeros(H, device=dev, dtype=F32), torch.ones(H, device=dev, dtype=F32),
+                     torch.zeros(H, device=dev, dtype=F32))       # relu(X[nb]) rebuilt in the staging
+            layers.append((d4, X[nb], d4_max, a_max, True, ident))
             res = weight_grads(layers, M)
             grads = {"lin_out.weight": res[-1][0], "lin_out.bias": res[-1][1]}
             w_in, b_in = res[-2]

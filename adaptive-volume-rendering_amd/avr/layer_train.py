@@ -95,6 +95,7 @@ class _FieldTrainLayers(torch.autograd.Function):
     def forward(ctx, fused, coarse, names, xyz, viewdirs, latent, *params):
         from .bn_train import _layer, _partial, _run
         from .models import combine_interleaved
+        from .ops import lin_out_rows
         net = fused.net
         mlp = fused._mlp(coarse)
         P = dict(zip(names, params))
@@ -164,11 +165,11 @@ class _FieldTrainLayers(torch.autograd.Function):
                                   ld_src=H, in_mu=idt.zero, in_scale=idt.one, in_shift=idt.zero,
                                   operand_max=amax[2 * b + 1:], blob=blob, layer=3 + 2 * b, bias=b1[b], add1=x,
                                   out=Xpre[b + 1], partial=part, **lin_z(b + 1)), stream)
-            a_out = torch.relu(Xpre[nb])
-            raw = torch.addmm(P["lin_out.bias"].detach().to(F32), a_out, P["lin_out.weight"].detach().to(F32).t())
-            out = torch.cat([torch.sigmoid(raw[:, :3]), torch.relu(raw[:, 3:4])], -1).reshape(SB, B, 4)
+            # lin_out + sigmoid / relu in one pass (max relu(x) for its weight gradient; relu(x) not stored)
+            out, a_max = lin_out_rows(Xpre[nb], P["lin_out.weight"].detach(), P["lin_out.bias"].detach())
+            out = out.reshape(SB, B, 4)
         ctx.fused, ctx.coarse, ctx.names, ctx.entry = fused, coarse, names, entry
-        ctx.keep = (Xpre, Xin, N, S, amax, zfp, a_out, idt, p, cl)
+        ctx.keep = (Xpre, Xin, N, S, amax, zfp, a_max, idt, p, cl)
         ctx.save_for_backward(xyz, viewdirs, latent, out, *params)
         return out
 
@@ -176,9 +177,9 @@ class _FieldTrainLayers(torch.autograd.Function):
     def backward(ctx, grad_out):
         from .bn_train import _layer, _partial, _run
         from .models import combine_interleaved
-        from .ops import _max_bits, sum_of_products, weight_grads
+        from .ops import _max_bits, lin_out_rows_bwd, sum_of_products, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
-        Xpre, Xin, N, S, amax, zfp, a_out, idt, p, cl = ctx.keep
+        Xpre, Xin, N, S, amax, zfp, a_max, idt, p, cl = ctx.keep
         ctx.keep = None
         fused, entry, names = ctx.fused, ctx.entry, ctx.names
         net = fused.net
@@ -198,16 +199,16 @@ class _FieldTrainLayers(torch.autograd.Function):
         with torch.no_grad():
             bwd = fused.packed_bwd(ctx.coarse, entry)
             part = _partial(M1, H, dev)
-            y = out.reshape(M2, 4)
-            go = grad_out.reshape(M2, 4).to(F32)
-            d4 = torch.cat([go[:, :3] * ((1.0 - y[:, :3]) * y[:, :3]), go[:, 3:] * (y[:, 3:] > 0)], -1).contiguous()
-            g = torch.ops.aten.threshold_backward(d4 @ P["lin_out.weight"].detach().to(F32), Xpre[nb], 0.0)
+            # the activations' backward (d4), lin_out^T and its relu's backward in one pass
+            d4, g, d4_max = lin_out_rows_bwd(grad_out.reshape(M2, 4), out.reshape(M2, 4),
+                                             P["lin_out.weight"].detach(), Xpre[nb])
             wl1, wl2 = [], []           # weight-gradient layers over M1 / M2 rows
             Gz, Gs, Gz_max = [None] * nz, [None] * nz, [None] * nz
             blk = [None] * nb
             # max |operand| of every backward layer call, published by the layer kernels (the weight gradients'
             # scales for gp2 and g without a reduction pass over the rows): [2b] fc_0^T's, [2b + 1] fc_1^T's
             omax = torch.zeros(2 * nb, device=dev, dtype=torch.int32)
+            relu_x = (idt.zero, idt.one, idt.zero)         # X = relu(rows), rebuilt in the staging
             for b in range(nb - 1, -1, -1):
                 m = M1 if b < cl else M2
                 # fc_1^T: gradient at N[b]; fc_0^T: the fc_0 path's gradient at X'[b]
@@ -222,10 +223,12 @@ class _FieldTrainLayers(torch.autograd.Function):
                                   ld_src=H, operand_max=omax[2 * b:], blob=bwd, layer=2 + 2 * b, out=gin,
                                   pre_rows=Xin[b], out_mu=idt.zero, out_invstd=idt.one, out_scale=idt.one,
                                   out_shift=idt.zero, add1=g, partial=part), stream)
-                relu_x = (idt.zero, idt.one, idt.zero)     # X = relu(rows), rebuilt in the staging
                 blk[b] = [(gp2, Xin[b], omax[2 * b:2 * b + 1], amax[2 * b:2 * b + 1], True, relu_x),
                           (g, N[b], omax[2 * b + 1:2 * b + 2], amax[2 * b + 1:2 * b + 2], True, relu_x)]
-                if b == cl and NS > 1:                         # torch's adjoint of the views' combine
+                if b == cl and NS > 1 and mlp.combine_type == "average":
+                    # the mean's adjoint (torch's MeanBackward: the gradient expanded over the views, / NS)
+                    gin = (gin.reshape(SB, 1, B, H).expand(SB, NS, B, H) / NS).reshape(M1, H)   # one pass
+                elif b == cl and NS > 1:                       # torch's adjoint of the views' combine
                     with torch.enable_grad():
                         xr = Xpre[b].detach().requires_grad_(True)
                         yc = combine_interleaved(xr, (NS, B), mlp.combine_type).reshape(M2, H)
@@ -255,7 +258,7 @@ class _FieldTrainLayers(torch.autograd.Function):
                 for b in range(nz if spade else 0):
                     wl1.append((Gs[b], lat_feat, _max_bits(Gs[b]), lat_max, True))
             wl1.append((g_in0, zfp, g_in0_max, _max_bits(zfp), True))
-            wl2.append((d4, a_out, _max_bits(d4), _max_bits(a_out), True))
+            wl2.append((d4, Xpre[nb], d4_max, a_max, True, relu_x))
             if M1 == M2:     # one source view: every layer over the same rows, one launch
                 r = weight_grads(wl1 + wl2, M1)
                 r1, r2 = r[:len(wl1)], r[len(wl1):]

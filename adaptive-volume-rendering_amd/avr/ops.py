@@ -378,6 +378,33 @@ def _max_bits(t):
     return torch.maximum(mx.abs(), mn.abs()).reshape(1).to(torch.float32).view(torch.int32)
 
 
+def lin_out_rows(x, weight, bias):
+    """lin_out of the layer-by-layer training paths over (n, d_hidden) rows x: (out (n, 4) = [sigmoid rgb,
+    relu sigma] of relu(x) . weight^T + bias (models.py:592, 856-862), max relu(x) as int32 float bits)
+    (avr_lin_out_fwd_rows, one pass over x)."""
+    n, H = x.shape
+    out = torch.empty(n, 4, device=x.device, dtype=F32)
+    xmax = torch.zeros(1, device=x.device, dtype=torch.int32)
+    call("avr_lin_out_fwd_rows", n, H, ptr(x), x.stride(0), ptr(_f32c(weight)), ptr(_f32c(bias)), ptr(out),
+         ptr(xmax), stream_of(x))
+    return out, xmax
+
+
+def lin_out_rows_bwd(grad_out, out, weight, pre, g=None):
+    """The backward of lin_out_rows: (d_raw (n, 4), g (n, d_hidden) = d_raw . weight where pre > 0, max |d_raw|
+    as int32 float bits) (avr_lin_out_bwd_rows; torch's sigmoid / relu / threshold backward in one pass); g may
+    be given (contiguous rows)."""
+    n, H = pre.shape
+    d_raw = torch.empty(n, 4, device=pre.device, dtype=F32)
+    if g is None:
+        g = torch.empty(n, H, device=pre.device, dtype=F32)
+    assert g.shape == (n, H) and g.is_contiguous() and g.dtype == F32
+    dmax = torch.zeros(1, device=pre.device, dtype=torch.int32)
+    call("avr_lin_out_bwd_rows", n, H, ptr(_f32c(grad_out)), ptr(_f32c(out)), ptr(_f32c(weight)), ptr(pre),
+         pre.stride(0), ptr(d_raw), ptr(g), ptr(dmax), stream_of(pre))
+    return d_raw, g, dmax
+
+
 _DW_TILE = 256        # avr_weight_grads output tile (weight_grad.hip kDwTile), one workgroup per CU
 
 

@@ -422,6 +422,19 @@ int avr_bn_grad_stats(const float* partial, int64_t n_rows, int n_cols, const fl
 int avr_bn_grad_rows(int64_t n_rows, int n_cols, const float* g, const float* pre, const float* res,
                      const float* coef, const float* m1, const float* m2, const float* mu, const float* invstd,
                      float* out, uint32_t* out_max, void* stream);
+/* lin_out over row-major rows (ABI 14), the layer-by-layer paths' output layer (avr.bn_train, avr.layer_train;
+ * replaces their torch relu / addmm / sigmoid / threshold_backward, models.py:592, 856-862), d_hidden 64 .. 512
+ * (a multiple of 64), every pointer 16-B aligned, weight (4, d_hidden) and bias (4) as nn.Linear holds them:
+ * avr_lin_out_fwd_rows: out (n_rows, 4) = [sigmoid(raw[0:3]), relu(raw[3])], raw = relu(x) . weight^T + bias,
+ *   x (n_rows, ld_x); x_max (or NULL): max relu(x) as float bits, max with what is there.
+ * avr_lin_out_bwd_rows: d_raw (n_rows, 4) = grad_out * [y (1 - y) rgb, (y > 0) sigma] with y = out (torch's
+ *   sigmoid / relu backward), g (n_rows, d_hidden) = d_raw . weight where pre > 0, else 0 (aten
+ *   threshold_backward; pre (n_rows, ld_pre) = lin_out's input before its relu); d_raw_max (or NULL): max |d_raw|
+ *   as float bits, max with what is there. */
+int avr_lin_out_fwd_rows(int64_t n_rows, int d_hidden, const float* x, int64_t ld_x, const float* weight,
+                         const float* bias, float* out, uint32_t* x_max, void* stream);
+int avr_lin_out_bwd_rows(int64_t n_rows, int d_hidden, const float* grad_out, const float* out, const float* weight,
+                         const float* pre, int64_t ld_pre, float* d_raw, float* g, uint32_t* d_raw_max, void* stream);
 
 /* Latent features at points — SpatialEncoder.index (models.py:245-274) as
  * NewPixelNeRFNet.forward uses it (models.py:753-810): bilinear / border /

@@ -146,3 +146,29 @@ def test_layer_train_grads_match_fp64(case):
             print(f"{case} coarse={coarse}: worst HIP gradient error vs float64 {worst:.2e} of max |grad|")
     finally:
         layer_train._FieldTrainLayers.apply = orig
+
+
+@pytest.mark.parametrize("H,n,pad", [(64, 1, 0), (192, 5, 4), (512, 1003, 0), (512, 40000, 8)])
+def test_lin_out_rows_vs_fp64(H, n, pad):
+    """avr_lin_out_fwd_rows / avr_lin_out_bwd_rows (the layer-by-layer paths' output layer) against float64 torch:
+    out and g within 1e-5 of their scale, d_raw bit-equal to torch's fp32 activation backward (same two
+    roundings), g exactly 0 where pre <= 0, both maxima exact; rows with a leading dimension past d_hidden."""
+    from avr import ops
+    g = torch.Generator().manual_seed(H + n)
+    xw = torch.randn(n, H + pad, generator=g).to(DEV)
+    x = xw[:, :H]
+    W = (torch.randn(4, H, generator=g) * 0.05).to(DEV)
+    b = torch.randn(4, generator=g).to(DEV)
+    out, xmax = ops.lin_out_rows(x, W, b)
+    raw = torch.relu(x.double()) @ W.double().t() + b.double()
+    ref = torch.cat([torch.sigmoid(raw[:, :3]), torch.relu(raw[:, 3:])], -1)
+    assert float((out.double() - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
+    assert int(xmax) == int(torch.relu(x).max().reshape(1).view(torch.int32))
+    go = torch.randn(n, 4, generator=g).to(DEV)
+    d4, gr, dmax = ops.lin_out_rows_bwd(go, out, W, x)
+    d4_ref = torch.cat([go[:, :3] * ((1.0 - out[:, :3]) * out[:, :3]), go[:, 3:] * (out[:, 3:] > 0)], -1)
+    assert torch.equal(d4, d4_ref)
+    assert int(dmax) == int(d4_ref.abs().max().reshape(1).view(torch.int32))
+    g_ref = (d4.double() @ W.double()) * (x > 0)
+    assert float((gr.double() - g_ref).abs().max()) <= 1e-5 * max(float(g_ref.abs().max()), 1e-30)
+    assert bool((gr[x <= 0] == 0).all())

@@ -117,6 +117,25 @@ def _install(monkeypatch, net):
             res.append((g.t() @ x, g.sum(0) if want_bias else None))
         return res
 
+    def bits(t):
+        return t.abs().max().reshape(1).view(torch.int32)
+
+    def lin_out_rows(x, weight, bias):
+        """avr_lin_out_fwd_rows' contract."""
+        raw = torch.relu(x) @ weight.t() + bias
+        return torch.cat([torch.sigmoid(raw[:, :3]), torch.relu(raw[:, 3:])], -1), bits(torch.relu(x))
+
+    def lin_out_rows_bwd(grad_out, out, weight, pre, g=None):
+        """avr_lin_out_bwd_rows' contract."""
+        d4 = torch.cat([grad_out[:, :3] * ((1.0 - out[:, :3]) * out[:, :3]), grad_out[:, 3:] * (out[:, 3:] > 0)], -1)
+        gr = torch.ops.aten.threshold_backward(d4 @ weight, pre, 0.0)
+        if g is not None:
+            g.copy_(gr)
+            gr = g
+        return d4, gr, bits(d4)
+
+    monkeypatch.setattr(ops, "lin_out_rows", lin_out_rows)
+    monkeypatch.setattr(ops, "lin_out_rows_bwd", lin_out_rows_bwd)
     monkeypatch.setattr(fused, "packed", packed)
     monkeypatch.setattr(fused, "packed_bwd", lambda coarse, entry=None: None)
     monkeypatch.setattr(fused, "tables_batch", tables_batch)
