@@ -7,7 +7,8 @@
 #   prof   rocprofv3 --kernel-trace --stats of a short bench command        -> $OUT/bench_kernel_stats.csv
 #   train  bench.py --mode train for each conf in CONFS (+ TRAIN_ARGS)      -> $OUT/bench_train_<conf>.log
 #   tprof  rocprofv3 kernel stats of the HIP train step (CONFS' last conf)  -> $OUT/train_kernel_stats.csv
-#   trainx the --bn and the AdaptiveVolumeRenderer train steps (default_mv) -> $OUT/bench_train_{bn,adaptive}_mv.log
+#   trainx the --bn, AdaptiveVolumeRenderer, NS 2 and spade + NS 2 train steps (default_mv)
+#          -> $OUT/bench_train_{bn,adaptive,views2,spade_views2}_mv.log
 #   bprof  rocprofv3 kernel stats of the --bn HIP train step (default_mv)   -> $OUT/train_bn_kernel_stats.csv
 # env: TAG (default r04), STEPS (default all), PYTEST_ARGS (extra pytest args, e.g. "-k philox"), CONFS.
 set -u
@@ -54,7 +55,7 @@ if has tprof; then
   head -6 $OUT/train_kernel_stats.csv | cut -c1-160
 fi
 if has trainx; then
-  for x in "bn:--bn" "adaptive:--renderer adaptive"; do
+  for x in "bn:--bn" "adaptive:--renderer adaptive" "views2:--views 2" "spade_views2:--spade --views 2"; do
     timeout -k 10 300 python -u bench.py --mode train --conf default_mv ${x#*:} --steps 20 --warmup 5 > $OUT/bench_train_${x%%:*}_mv.log 2>&1
     rc=$?; tail -1 $OUT/bench_train_${x%%:*}_mv.log | cut -c1-300; echo; [ $rc -eq 0 ] || { echo "train ${x%%:*} rc=$rc"; exit $rc; }
   done
