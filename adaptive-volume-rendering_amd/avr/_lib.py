@@ -56,7 +56,7 @@ class WGradLayer(ctypes.Structure):
     _fields_ = [("grad", c_void_p), ("ld_grad", i64), ("input", c_void_p), ("ld_input", i64),
                 ("out_dim", c_int), ("in_dim", c_int), ("grad_max", c_void_p), ("input_max", c_void_p),
                 ("partial", c_void_p), ("bias_partial", c_void_p),
-                ("in_mu", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p)]
+                ("in_mu", c_void_p), ("in_scale", c_void_p), ("in_shift", c_void_p), ("input_relu", c_int)]
 
 
 BN_FWD, BN_BWD = 0, 1

@@ -300,9 +300,7 @@ class _FieldTrainBN(torch.autograd.Function):
                 layers.append((Gx[b], lat_feat, gmax[b:b + 1], lat_max, True))
             zf_max = _max_bits(zfp)
             layers.append((Gx[0], zfp, gmax[0:1], zf_max, True))
-            ident = (torch.zeros(H, device=dev, dtype=F32), torch.ones(H, device=dev, dtype=F32),
-                     torch.zeros(H, device=dev, dtype=F32))       # relu(X[nb]) rebuilt in the staging
-            layers.append((d4, X[nb], d4_max, a_max, True, ident))
+            layers.append((d4, X[nb], d4_max, a_max, True, "relu"))   # relu(X[nb]) rebuilt in the staging
             res = weight_grads(layers, M)
             grads = {"lin_out.weight": res[-1][0], "lin_out.bias": res[-1][1]}
             w_in, b_in = res[-2]

@@ -208,7 +208,7 @@ class _FieldTrainLayers(torch.autograd.Function):
             # max |operand| of every backward layer call, published by the layer kernels (the weight gradients'
             # scales for gp2 and g without a reduction pass over the rows): [2b] fc_0^T's, [2b + 1] fc_1^T's
             omax = torch.zeros(2 * nb, device=dev, dtype=torch.int32)
-            relu_x = (idt.zero, idt.one, idt.zero)         # X = relu(rows), rebuilt in the staging
+            relu_x = "relu"                                # X = relu(rows), rebuilt in the staging
             for b in range(nb - 1, -1, -1):
                 m = M1 if b < cl else M2
                 # fc_1^T: gradient at N[b]; fc_0^T: the fc_0 path's gradient at X'[b]

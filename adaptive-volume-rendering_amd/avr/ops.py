@@ -430,7 +430,8 @@ def weight_grads(layers, n_rows, n_split=None):
     of `layers` (avr_weight_grads: split-K x3 MFMA). grad (n_rows, out) / input
     (n_rows, in) fp32 row-major (row strides may exceed the widths); *_max: int32
     (1,) float bits of max |.|; bn = (mu, scale, shift) (in,) each: X = relu((input - mu) * scale + shift)
-    per column, a training-mode BatchNorm's operand rebuilt from its pre-BN rows (input_max then of X).
+    per column, a training-mode BatchNorm's operand rebuilt from its pre-BN rows (input_max then of X), or
+    bn = "relu": X = relu(input).
     Returns [(dW (out, in), db (out,) or None)]."""
     if not layers:
         return []
@@ -454,6 +455,10 @@ def weight_grads(layers, n_rows, n_split=None):
         for k, (g, x, gmax, xmax, want_bias, *bn) in enumerate(chunk):
             O, I = g.shape[1], x.shape[1]
             bn = bn[0] if bn else None
+            relu = isinstance(bn, str)
+            if relu and bn != "relu":
+                raise _lib.AVRError(f"weight_grads: unknown input transform {bn!r}")
+            bn = None if relu else bn
             for t in (g, x):
                 if t.dtype != torch.float32 or t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
                     raise _lib.AVRError("weight_grads: operands must be fp32 rows, 16-B aligned, unit column stride")
@@ -465,7 +470,7 @@ def weight_grads(layers, n_rows, n_split=None):
             off += sizes[k]
             arr[k] = _lib.WGradLayer(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), O, I, gmax.data_ptr(),
                                      xmax.data_ptr(), part.data_ptr(), 0 if bpart is None else bpart.data_ptr(),
-                                     *([t.data_ptr() for t in bn] if bn is not None else [None] * 3))
+                                     *([t.data_ptr() for t in bn] if bn is not None else [None] * 3), int(relu))
             dw = torch.empty(O, I, device=dev, dtype=torch.float32)
             db = torch.empty(O, device=dev, dtype=torch.float32) if want_bias else None
             dw_ptrs[k], db_ptrs[k] = dw.data_ptr(), (db.data_ptr() if want_bias else None)

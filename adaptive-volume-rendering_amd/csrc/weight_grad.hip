@@ -44,6 +44,7 @@ struct DwLayerDev {
   float* part;
   float* bpart;
   const float* xmu; const float* xscale; const float* xshift;   // NULL, or X = relu((x - mu) * scale + shift)
+  int xrelu;                                                     // (xmu NULL) X = relu(x)
 };
 
 struct DwArgs {
@@ -169,6 +170,8 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
                      // also wait for the chunk loads in flight behind it: the counter is in order)
         const lds_floatx4* P = (const lds_floatx4*)(lds + 2 * kDwStage);
         xv = bn_relu4(xv, P[cc], P[64 + cc], P[128 + cc]);
+      } else if (D.xrelu) {   // identity statistics: bn_relu4's result with mu 0, scale 1, shift 0, no parameters
+        xv = floatx4{fmaxf(xv.x, 0.f), fmaxf(xv.y, 0.f), fmaxf(xv.z, 0.f), fmaxf(xv.w, 0.f)};
       }
     split4(xv, sX, hi, lo);
     *(lds_u32x2*)(st + 2 * kDwImg + off) = u32x2{hi.x, hi.y};
@@ -422,8 +425,11 @@ extern "C" int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int
                      ((reinterpret_cast<uintptr_t>(s.in_mu) | reinterpret_cast<uintptr_t>(s.in_scale) |
                        reinterpret_cast<uintptr_t>(s.in_shift)) % 16) == 0),
                 "avr_weight_grads: layer %d: in_mu / in_scale / in_shift all NULL or all set (16-B aligned)", l);
+    AVR_REQUIRE(!s.input_relu || !s.in_mu, "avr_weight_grads: layer %d: input_relu with in_mu / in_scale / in_shift",
+                l);
     D.xmu = s.in_mu; D.xscale = s.in_scale; D.xshift = s.in_shift;
-    xf = xf || s.in_mu;
+    D.xrelu = s.input_relu;
+    xf = xf || s.in_mu || s.input_relu;
     tiles += ((s.out_dim + kDwTile - 1) / kDwTile) * D.nIt;
   }
   a.tiles = tiles;

@@ -344,6 +344,9 @@ typedef struct {
    * 16-B aligned) -- a training-mode BatchNorm's operand rebuilt from its pre-BN rows (avr_bn_layer's
    * AVR_BN_RELU, bit for bit); input_max is then the max of the rebuilt values. */
   const float* in_mu; const float* in_scale; const float* in_shift;
+  /* ABI 14: nonzero (in_mu / in_scale / in_shift NULL): the layer input is relu(input) (the layer-by-layer path's
+   * identity statistics without their column parameters); input_max is then the max of relu(input). */
+  int input_relu;
 } avr_wgrad_layer;
 int avr_weight_grads(const avr_wgrad_layer* layers, int n_layers, int64_t n_rows, int n_split, void* stream);
 /* The caller's sum above, for the whole layer list in one launch (ABI 9): dw[l] (out_dim, in_dim) =

@@ -1,7 +1,8 @@
 """Isolated timing of avr_weight_grads on a training step's layer list: WG_CONF=default (the fine pass of
 conf/default.conf: 9 hidden 512 x 512 layers) or default_mv (train.py's conf/default_mv.conf: 13), plus lin_in
 (512 x 44) and lin_out (4 x 512), M = 4 scenes x 512 rays x 96 samples. WG_SPLITS="a,b,..." times explicit K-splits
-beside the library's own choice; WG_THIN=0 leaves out lin_in / lin_out. Prints ms per call and TFLOP/s (fp32-equivalent). Diagnostic only."""
+beside the library's own choice; WG_THIN=0 leaves out lin_in / lin_out; WG_XF=ident|bn|relu adds the staging's
+BatchNorm-relu (or relu-only) transform to the hidden layers. Prints ms per call and TFLOP/s (fp32-equivalent). Diagnostic only."""
 import os
 import sys
 import time
@@ -23,7 +24,18 @@ def main():
     zf = torch.randn(M, 44, generator=g).to(dev)
     d4 = torch.randn(M, 4, generator=g).to(dev)
     mb = ops._max_bits
-    layers = [(Gs[i % 7], Xs[i % 8], mb(Gs[i % 7]), mb(Xs[i % 8]), i < 6) for i in range(n_hidden)]
+    # WG_XF=ident / bn: the hidden layers' X rebuilt in the staging as relu((x - mu) * scale + shift) (identity
+    # statistics as avr.layer_train passes them, or BatchNorm-like ones as avr.bn_train)
+    xf = os.environ.get("WG_XF", "none")
+    if xf == "ident":
+        tf = (torch.zeros(512, device=dev), torch.ones(512, device=dev), torch.zeros(512, device=dev))
+    elif xf == "relu":
+        tf = "relu"
+    elif xf == "bn":
+        tf = ((torch.rand(512, generator=g) * 0.2).to(dev), (torch.rand(512, generator=g) + 0.5).to(dev),
+              (torch.randn(512, generator=g) * 0.1).to(dev))
+    layers = [(Gs[i % 7], Xs[i % 8], mb(Gs[i % 7]), mb(Xs[i % 8]), i < 6) + ((tf,) if xf != "none" else ())
+              for i in range(n_hidden)]
     thin = os.environ.get("WG_THIN", "1") == "1"   # WG_THIN=0: without lin_in / lin_out (their tiles' cost)
     if thin:
         layers += [(Gs[6], zf, mb(Gs[6]), mb(zf), True), (d4, Xs[7], mb(d4), mb(Xs[7]), True)]
@@ -37,7 +49,7 @@ def main():
             ops.weight_grads(layers, M, n_split=n)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / reps
-        print(f"M={M} hidden={n_hidden} thin={int(thin)} n_split={n or 'auto'} weight_grads {dt * 1e3:.3f} ms/call (incl. partial sums) "
+        print(f"M={M} hidden={n_hidden} thin={int(thin)} xf={xf} n_split={n or 'auto'} weight_grads {dt * 1e3:.3f} ms/call (incl. partial sums) "
               f"{flops / dt / 1e12:.1f} TFLOP/s fp32-eq", flush=True)
 
 

@@ -293,6 +293,15 @@ def test_weight_grads_bn_transform_vs_fp64(M, O, I, ld):
         np.testing.assert_allclose(db.cpu().numpy(), bref, rtol=0, atol=2e-6 * float(np.abs(bref).max()))
     with pytest.raises(Exception, match="BatchNorm transform"):
         ops.weight_grads([(G, pre[:, :I], mb(G), mb(X), True, (mu, scale, shift[:-4]))], M)
+    # ABI 14: the relu-only transform (input_relu) beside the BatchNorm one and an untransformed layer
+    R = torch.relu(pre[:, :I])
+    lay = [(G2, pre[:, :I], mb(G2), mb(R), False, "relu")] + lay
+    res = ops.weight_grads(lay, M)
+    for (dW, _), GG, XX in zip(res, (G2, G, G2), (R, X, Xp)):
+        ref = (GG.double().t() @ XX.double()).float().cpu().numpy()
+        scale_r = max(float(np.abs(ref).max()), 1e-30)
+        assert float(np.abs(dW.cpu().numpy() - ref).max()) <= 2e-6 * scale_r
+    assert res[0][1] is None
 
 
 def test_latent_features_kernel_vs_grid_sample():

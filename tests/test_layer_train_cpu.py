@@ -111,7 +111,9 @@ def _install(monkeypatch, net):
             assert g.shape[0] == x.shape[0] == n_rows
             # the scales' inputs: max |G| exactly (the operand maxima the layer kernels publish, or a reduction)
             assert float(gmax.view(torch.float32)[0]) == float(g.abs().max()), "wrong max |G|"
-            if bn:
+            if bn and bn[0] == "relu":
+                x = torch.relu(x)
+            elif bn:
                 mu, sc, sh = bn[0]
                 x = torch.relu((x - mu) * sc + sh)
             res.append((g.t() @ x, g.sum(0) if want_bias else None))
