@@ -405,16 +405,19 @@ class _MarchTrain(torch.autograd.Function):
             d_b = d_grads[1024:1088]
             d_wout = d_grads[1088:1104].reshape(1, 16)
             d_bout = d_grads[1104:1105]
+            # per-scene products summed after (the einsum's single K = SB * H*W product ran on a handful of
+            # workgroups: 183 vs 41 us, scripts/march_gemm_bench.py)
             if ctx.L == SB:
-                d_wih = torch.einsum("sth,sct->hc", d_tab, lat_t)
+                d_wih = torch.bmm(d_tab.transpose(1, 2), lat_t.transpose(1, 2)).sum(0)          # (64, C)
             else:
-                d_wih = torch.einsum("th,ct->hc", d_tab.sum(0), lat_t[0])
+                d_wih = torch.mm(d_tab.sum(0).t(), lat_t[0].t())
             d_lat = None
             if ctx.needs_input_grad[5] and not getattr(ctx.phi, "stop_encoder_grad", False):
-                dl = torch.matmul(d_tab, w_ih.detach().float())                         # (SB, H*W, C)
+                # W_ih^T d_tab^T: written in the latent's own (C, H*W) layout, no transpose pass (71 vs 24 us)
+                dl = torch.matmul(w_ih.detach().float().t(), d_tab.transpose(1, 2))             # (SB, C, H*W)
                 if ctx.L != SB:
                     dl = dl.sum(0, keepdim=True)
-                d_lat = dl.transpose(1, 2).reshape(latent.shape).to(latent.dtype)
+                d_lat = dl.reshape(latent.shape).to(latent.dtype)
         return (None, None, None, None, None, d_lat, d_wih.to(w_ih.dtype), d_whh, d_b.clone(), d_b.clone(), d_wout,
                 d_bout)
 
