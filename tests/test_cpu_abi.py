@@ -58,6 +58,22 @@ def test_invalid_arguments_return_codes():
     assert n.value == ((fp32 + 63) // 64) * 64 + x3
 
 
+def test_lin_out_rows_argument_checks():
+    """avr_lin_out_fwd_rows / avr_lin_out_bwd_rows (ABI 14): zero rows is a no-op, d_hidden outside 64..512 or not
+    a multiple of 64 and null pointers are refused before any HIP call."""
+    from avr import _lib
+    lib = _lib.load()
+    f, b = lib.avr_lin_out_fwd_rows, lib.avr_lin_out_bwd_rows
+    assert f(0, 512, None, 512, None, None, None, None, None) == 0
+    assert b(0, 512, None, None, None, None, 512, None, None, None, None) == 0
+    for H in (0, 32, 100, 576):
+        assert f(4, H, None, 512, None, None, None, None, None) == 1001
+        assert b"d_hidden" in lib.avr_last_error_string()
+    assert f(4, 512, None, 512, None, None, None, None, None) == 1001
+    assert b"null" in lib.avr_last_error_string()
+    assert b(4, 256, None, None, None, None, 256, None, None, None, None) == 1001
+
+
 def test_ops_refuse_host_tensors():
     from avr import _lib, ops
     with pytest.raises(_lib.AVRError):
