@@ -124,7 +124,7 @@ def forward_train_bn(fused, xyz, viewdirs, coarse):
     """The rf(xyz, viewdirs, coarse) protocol for a training-mode BatchNorm net (autograd when enabled)."""
     mlp = fused._mlp(coarse)
     names = train_param_names_bn(mlp)
-    named = dict(mlp.named_parameters())
+    named, _, _ = fused._state(mlp)
     params = [named[n] for n in names]
     return _FieldTrainBN.apply(fused, coarse, names, xyz, viewdirs, fused.net.encoder.latent, *params)
 

@@ -157,6 +157,7 @@ class FusedField:
         self._packed = {}     # coarse(bool) -> (key, _Packed)
         self._view_cache = {}
         self._latent_cache = {}   # per latent version: channels-last copies, max |latent| (both MLPs share them)
+        self._slots = {}          # id(mlp) -> (mlp, [(name, owner dict, key)] params, [...] float buffers)
 
     def invalidate(self):
         """Drop every cached blob, table and view descriptor (avr.parallel.broadcast_scene calls it after
@@ -207,6 +208,22 @@ class FusedField:
         return self._latent_cached("max", latent, lambda: _max_bits(latent))
 
     # ----------------------------------------------------------- parameters
+    def _state(self, mlp):
+        """(named parameters, parameters, floating-point buffers) of mlp in named_parameters() / buffers() order,
+        read through each owning module's dict: the module tree is walked once per mlp (a walk per call was a
+        large part of the adaptive step's host time), and a parameter or buffer replaced later is still seen."""
+        hit = self._slots.get(id(mlp))
+        if hit is None or hit[0] is not mlp:
+            mods = list(mlp.named_modules())
+            ps = [(f"{mn}.{n}" if mn else n, m._parameters, n) for mn, m in mods
+                  for n, t in m._parameters.items() if t is not None]
+            bs = [(f"{mn}.{n}" if mn else n, m._buffers, n) for mn, m in mods
+                  for n, t in m._buffers.items() if t is not None and t.is_floating_point()]
+            hit = (mlp, ps, bs)
+            self._slots[id(mlp)] = hit
+        named = {full: d[k] for full, d, k in hit[1]}
+        return named, list(named.values()), [d[k] for _, d, k in hit[2]]
+
     def _mlp(self, coarse):
         net = self.net
         return net.mlp_coarse if (coarse or net.mlp_fine is None) else net.mlp_fine
@@ -222,7 +239,8 @@ class FusedField:
         """bn_fold=False: the training-mode BatchNorm path's blob (avr.bn_train): x3, raw fc_0 weights (no
         eval-BN folding, dims.bn = 0), cached beside the inference blob."""
         mlp = self._mlp(coarse)
-        params = [p.detach() for p in mlp.parameters()] + [b for b in mlp.buffers() if b.is_floating_point()]
+        _, ps, bs = self._state(mlp)
+        params = ps + bs
         # the precision is part of the key: an x3 blob holds only the fragments the x3 kernels read
         # (avr_field_pack), and net.fused() switches a FusedField's precision in place
         slot = coarse if bn_fold else (coarse, "bn_train")
@@ -471,7 +489,7 @@ class FusedField:
         gradients as GEMMs over the samples (see _FieldTrain)."""
         mlp = self._mlp(coarse)
         names = train_param_names(mlp)
-        named = dict(mlp.named_parameters())   # once (a dict per name walked the module tree per parameter)
+        named, _, _ = self._state(mlp)
         params = [named[n] for n in names]
         return _FieldTrain.apply(self, coarse, names, xyz, viewdirs, self.net.encoder.latent, *params)
 

@@ -62,7 +62,7 @@ def forward_train_layers(fused, xyz, viewdirs, coarse):
     """The rf(xyz, viewdirs, coarse) protocol on this path (autograd when enabled)."""
     mlp = fused._mlp(coarse)
     names = train_param_names_layers(mlp)
-    named = dict(mlp.named_parameters())
+    named, _, _ = fused._state(mlp)
     return _FieldTrainLayers.apply(fused, coarse, names, xyz, viewdirs, fused.net.encoder.latent,
                                    *[named[n] for n in names])
 
