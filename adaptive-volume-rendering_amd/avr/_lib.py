@@ -61,6 +61,7 @@ class WGradLayer(ctypes.Structure):
 
 BN_FWD, BN_BWD = 0, 1
 BN_PLAIN, BN_RELU, BN_GRAD = 0, 1, 2
+BN_LAYER_LIN_Z_T = 34     # avr.h AVR_BN_LAYER_LIN_Z_T: + b, lin_z[b]^T of the backward blob (ABI 14)
 
 
 class BnLayer(ctypes.Structure):

@@ -494,6 +494,35 @@ class FusedField:
         return _FieldTrain.apply(self, coarse, names, xyz, viewdirs, self.net.encoder.latent, *params)
 
 
+def _feat_grad(fused, entry, bwd, Gz, P, Mt):
+    """The looked-up latent features' gradient sum_b Gz[b] . W_z[b] (the point / latent gradients' input):
+    avr_bn_layer_run's lin_z[b]^T layers from the backward blob (x3, ABI 14), one launch per layer adding the
+    previous layers' sum in its epilogue, where they apply (d_latent == d_hidden, ReLU, 64..512 wide); else
+    fp32 library GEMMs (avr.ops.sum_of_products)."""
+    from .bn_train import _layer, _partial, _run
+    from .ops import sum_of_products
+    dims = entry.dims
+    H, nz = dims.d_hidden, dims.n_lin_z
+    if not (dims.d_latent == H and H in (64, 128, 256, 512) and not dims.spade and not dims.bn
+            and not dims.beta > 0 and Mt > 0 and all(g.is_contiguous() for g in Gz)):
+        return sum_of_products([(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)])
+    dev = Gz[0].device
+    part = _partial(Mt, H, dev)
+    stream = stream_of(Gz[0])
+    prev = None
+    saved, dims.precision = dims.precision, _lib.FIELD_X3
+    try:
+        for b in range(nz):
+            out = torch.empty(Mt, H, device=dev, dtype=F32)
+            _run(dims, _layer(n_rows=Mt, mode=_lib.BN_BWD, prologue=_lib.BN_PLAIN, in_dim=H, in_valid=H, src=Gz[b],
+                              ld_src=H, blob=bwd, layer=_lib.BN_LAYER_LIN_Z_T + b, add1=prev, out=out, partial=part),
+                 stream)
+            prev = out
+    finally:
+        dims.precision = saved
+    return prev
+
+
 def train_param_names(mlp):
     """The ResnetFC parameters the training path differentiates, in a fixed order."""
     names = ["lin_in.weight", "lin_in.bias", "lin_out.weight", "lin_out.bias"]
@@ -647,7 +676,7 @@ class _FieldTrain(torch.autograd.Function):
             d_look = None
             if not net.stop_encoder_grad:
                 with torch.no_grad():
-                    g_feat = sum_of_products([(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)])
+                    g_feat = _feat_grad(fused, entry, bwd, Gz, P, Mt)
                     d_look = torch.empty(Mt, 3, device=dev, dtype=F32)
                     hwc = fused.latent_hwc_all(latent)
                     p = xyz.detach().to(F32).contiguous()
@@ -669,7 +698,7 @@ class _FieldTrain(torch.autograd.Function):
                 outs, grads_out = [], []
                 if nz > 0:
                     outs.append(feat)
-                    grads_out.append(sum_of_products([(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)]))
+                    grads_out.append(_feat_grad(fused, entry, bwd, Gz, P, Mt))
                 if want_xyz:
                     outs.append(zft)
                     grads_out.append(G[2 * nb] @ P["lin_in.weight"].detach())

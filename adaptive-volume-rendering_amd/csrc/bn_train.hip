@@ -398,6 +398,14 @@ __global__ void __launch_bounds__(64 * NW, NW > 4 ? 1 : 2) bn_layer_kernel(BnArg
       }
       s2[ft] = sum16(s2[ft]);
     }
+  } else if (!a.pre_rows) {   // lin_z[b]^T (ABI 14): no mask, no statistics; add1 / the store below are shared
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      s1[ft] = zero4;
+      s2[ft] = zero4;
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) acc[ft][sg] = acc[ft][sg] * inv;
+    }
   } else {
     // gp = (W^T . op) * relu mask of the forward operand, recomputed from the pre-BN row (bn_relu4, as the
     // forward did); the pre-BN rows also give xhat for the statistics (sums of gp and of gp * xhat)
@@ -427,6 +435,8 @@ __global__ void __launch_bounds__(64 * NW, NW > 4 ? 1 : 2) bn_layer_kernel(BnArg
       s1[ft] = sum16(s1[ft]);
       s2[ft] = sum16(s2[ft]);
     }
+  }
+  if constexpr (MODE == AVR_BN_BWD) {
     if (a.add1) {   // a residual gradient added to the stored rows (the statistics are of gp alone)
       floatx4 t[FT][4];
       load_rows(a.add1, t);
@@ -680,7 +690,8 @@ extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* 
   a.opnd_max = l->operand_max;
   // the layer's fragments and its header word (0 lin_in, 2 + 2b fc_0[b], 3 + 2b fc_1[b])
   const int ly = l->layer;
-  AVR_REQUIRE(ly == 0 || (ly >= 2 && ly < 2 + 2 * nb), "avr_bn_layer_run: layer %d", ly);
+  const bool lzt = l->mode == AVR_BN_BWD && ly >= AVR_BN_LAYER_LIN_Z_T && ly < AVR_BN_LAYER_LIN_Z_T + dims->n_lin_z;
+  AVR_REQUIRE(ly == 0 || (ly >= 2 && ly < 2 + 2 * nb) || lzt, "avr_bn_layer_run: layer %d", ly);
   const unsigned* hdr;
   if (l->mode == AVR_BN_FWD) {
     AVR_REQUIRE(ly != 0 || l->in_dim == 64, "avr_bn_layer_run: lin_in's operand is 64 columns");
@@ -701,12 +712,21 @@ extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* 
       a.ztab = l->lin_z_table; a.ztab_stride = l->lin_z_scene_stride; a.zrows = l->rows_per_scene; a.zxyz = l->xyz;
     }
   } else {
-    AVR_REQUIRE(ly >= 2 && l->in_dim == H, "avr_bn_layer_run: the backward runs fc_0 / fc_1 (d_hidden columns)");
-    AVR_REQUIRE(l->pre_rows && l->out_mu && l->out_invstd && l->out_scale && l->out_shift,
-                "avr_bn_layer_run: AVR_BN_BWD needs pre_rows, out_mu, out_invstd, out_scale, out_shift");
+    AVR_REQUIRE(ly >= 2 && l->in_dim == H,
+                "avr_bn_layer_run: the backward runs fc_0 / fc_1 / lin_z (d_hidden columns)");
     BwdLayout LB;
     if ((rc = field_bwd_layout(dims, &LB))) return rc;
-    a.w = l->blob + (ly % 2 == 0 ? LB.fc0t[(ly - 2) / 2] : LB.fc1t[(ly - 2) / 2]);
+    if (lzt) {
+      AVR_REQUIRE(LB.lzt[ly - AVR_BN_LAYER_LIN_Z_T] >= 0,
+                  "avr_bn_layer_run: lin_z^T needs d_latent == d_hidden (%d, %d) and no use_spade", dims->d_latent, H);
+      AVR_REQUIRE(!l->pre_rows && !l->out_mu && !l->out_invstd && !l->out_scale && !l->out_shift,
+                  "avr_bn_layer_run: lin_z^T has no relu mask (pre_rows / out_* NULL)");
+      a.w = l->blob + LB.lzt[ly - AVR_BN_LAYER_LIN_Z_T];
+    } else {
+      AVR_REQUIRE(l->pre_rows && l->out_mu && l->out_invstd && l->out_scale && l->out_shift,
+                  "avr_bn_layer_run: AVR_BN_BWD needs pre_rows, out_mu, out_invstd, out_scale, out_shift");
+      a.w = l->blob + (ly % 2 == 0 ? LB.fc0t[(ly - 2) / 2] : LB.fc1t[(ly - 2) / 2]);
+    }
     hdr = reinterpret_cast<const unsigned*>(l->blob);
     AVR_REQUIRE(!l->add2 && !l->lin_z_table, "avr_bn_layer_run: AVR_BN_BWD adds add1 only");
     a.pre_rows = l->pre_rows; a.out_mu = l->out_mu; a.out_invstd = l->out_invstd;

@@ -100,6 +100,12 @@ static int make_bwd_layout(const avr_field_dims* d, BwdLayout* LB) {
     LB->fc0t[b] = o; o += S;
     LB->fc1t[b] = o; o += S;
   }
+  // lin_z[b]^T (d_latent x d_hidden after the transpose: a hidden layer's shape when d_latent == d_hidden) for
+  // avr_bn_layer_run's transposed products (the point gradient's sum_b Gz[b] . W_z[b])
+  for (int b = 0; b < AVR_MAX_BLOCKS; ++b) {
+    LB->lzt[b] = -1;
+    if (b < d->n_lin_z && d->d_latent == d->d_hidden && !d->spade) { LB->lzt[b] = o; o += S; }
+  }
   LB->total = o;
   return AVR_OK;
 }
@@ -731,6 +737,10 @@ extern "C" int avr_field_pack_bwd(const avr_field_dims* dims, const avr_resnetfc
     if ((rc = add_x3(bt, w->fc0_w[b], H, H, KC, NT, hdr + 2 + 2 * b, packed_bwd + LB.fc0t[b], true))) return rc;
     if ((rc = add_x3(bt, w->fc1_w[b], H, H, KC, NT, hdr + 3 + 2 * b, packed_bwd + LB.fc1t[b], true))) return rc;
   }
+  for (int b = 0; b < AVR_MAX_BLOCKS; ++b)
+    if (LB.lzt[b] >= 0 &&
+        (rc = add_x3(bt, w->lin_z_w[b], H, H, KC, NT, hdr + kBwdLinZHdr + b, packed_bwd + LB.lzt[b], true)))
+      return rc;
   return run_x3(bt, s);
 }
 

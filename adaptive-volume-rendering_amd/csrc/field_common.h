@@ -44,11 +44,14 @@ constexpr int kX3PackJobs = kX3MaxLayers + 2 * AVR_MAX_BLOCKS;  // layers of one
 
 // Backward blob (avr_field_pack_bwd): header (64 words, max|W| bits per layer
 // in the forward's numbering) + x3 fragments of fc_0[b]^T and fc_1[b]^T in the
-// forward's [c][ft][lane] order.
+// forward's [c][ft][lane] order, then (ABI 14, d_latent == d_hidden) lin_z[b]^T
+// (header word kBwdLinZHdr + b; -1 when absent).
 struct BwdLayout {
   int64_t fc0t[AVR_MAX_BLOCKS], fc1t[AVR_MAX_BLOCKS];
+  int64_t lzt[AVR_MAX_BLOCKS];
   int64_t total;          // floats
 };
+constexpr int kBwdLinZHdr = AVR_BN_LAYER_LIN_Z_T;   // header words 34 .. 41
 
 // Training forward / backward (x3 path): relu masks of the 2 * n_blocks + 1
 // GEMM inputs, one bit per (feature, sample) a lane holds, bit

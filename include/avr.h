@@ -372,7 +372,9 @@ int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_s
  *     backward blob (avr_field_pack_bwd): the relu mask of the forward's AVR_BN_RELU operand, recomputed from
  *     the pre-BN rows (ABI 12; the relu'd operands need not be stored); out = gp (+ add1: ABI 14, a residual
  *     gradient, ld d_hidden; add2 / lin_z_table must be NULL); partial = per workgroup (sum gp, sum gp * xhat),
- *     xhat = (pre_rows - out_mu) * out_invstd.
+ *     xhat = (pre_rows - out_mu) * out_invstd. ABI 14: layer AVR_BN_LAYER_LIN_Z_T + b (b < n_lin_z, d_latent ==
+ *     d_hidden, no use_spade) is lin_z[b]^T with no mask (pre_rows and the out_* vectors NULL): out = W_z[b]^T .
+ *     op (+ add1), the point gradient's sum_b Gz[b] . W_z[b] one layer at a time; the partial is zeros.
  *   The operand op (n_rows, in_dim), read from src (columns >= in_valid are 0):
  *     AVR_BN_PLAIN op = src;
  *     AVR_BN_RELU  op = relu((src - in_mu) * in_scale + in_shift)                 (forward: relu(bn_0(x)));
@@ -388,6 +390,7 @@ int avr_weight_grads_reduce(const avr_wgrad_layer* layers, int n_layers, int n_s
  *   it), out_max as operand_max; out must not overlap g, pre or res.                                                                               */
 #define AVR_BN_FWD 0
 #define AVR_BN_BWD 1
+#define AVR_BN_LAYER_LIN_Z_T 34   /* + b: lin_z[b]^T from the backward blob (AVR_BN_BWD, ABI 14; see below) */
 #define AVR_BN_PLAIN 0
 #define AVR_BN_RELU 1
 #define AVR_BN_GRAD 2

@@ -172,3 +172,34 @@ def test_lin_out_rows_vs_fp64(H, n, pad):
     g_ref = (d4.double() @ W.double()) * (x > 0)
     assert float((gr.double() - g_ref).abs().max()) <= 1e-5 * max(float(g_ref.abs().max()), 1e-30)
     assert bool((gr[x <= 0] == 0).all())
+
+
+@pytest.mark.parametrize("H,nb,cl,M", [(64, 3, 2, 333), (256, 3, 3, 64), (512, 5, 3, 1000)])
+def test_lin_z_transposed_layers_vs_fp64(H, nb, cl, M):
+    """The looked-up features' gradient sum_b Gz[b] . W_z[b] on avr_bn_layer_run's lin_z[b]^T layers (ABI 14: the
+    backward blob's transposed lin_z fragments, no mask, each layer adding the previous sum) against float64, and
+    the library fallback where the layers do not apply (d_latent != d_hidden)."""
+    from avr.field import _feat_grad
+    net = _net(H, nb, H, (8, 8), cl)
+    fused = net.fused()
+    mlp = net.mlp_coarse
+    entry = fused.packed(True)
+    bwd = fused.packed_bwd(True, entry)
+    nz = entry.dims.n_lin_z
+    assert nz == min(cl, nb)
+    g = torch.Generator().manual_seed(H + M)
+    Gz = [(torch.randn(M, H, generator=g) * 10.0 ** (-b)).to(DEV) for b in range(nz)]
+    P = {f"lin_z.{b}.weight": mlp.lin_z[b].weight for b in range(nz)}
+    got = _feat_grad(fused, entry, bwd, Gz, P, M)
+    ref = sum(Gz[b].double() @ P[f"lin_z.{b}.weight"].detach().double() for b in range(nz))
+    err = float((got.double() - ref).abs().max() / ref.abs().max())
+    assert err <= 2e-6, err
+    # d_latent 64 != d_hidden 128: the fallback's fp32 GEMMs
+    net2 = _net(128, 3, 64, (8, 8), 2)
+    f2 = net2.fused()
+    e2 = f2.packed(True)
+    Gz2 = [torch.randn(M, 128, generator=g).to(DEV) for _ in range(2)]
+    P2 = {f"lin_z.{b}.weight": net2.mlp_coarse.lin_z[b].weight for b in range(2)}
+    got2 = _feat_grad(f2, e2, f2.packed_bwd(True, e2), Gz2, P2, M)
+    ref2 = sum(Gz2[b].double() @ P2[f"lin_z.{b}.weight"].detach().double() for b in range(2))
+    assert float((got2.double() - ref2).abs().max() / ref2.abs().max()) <= 2e-6
