@@ -177,6 +177,7 @@ class _FieldTrainLayers(torch.autograd.Function):
     def backward(ctx, grad_out):
         from .bn_train import _layer, _partial, _run
         from .models import combine_interleaved
+        from .field import _feat_grad
         from .ops import _max_bits, lin_out_rows_bwd, sum_of_products, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         Xpre, Xin, N, S, amax, zfp, a_max, idt, p, cl = ctx.keep
@@ -291,10 +292,13 @@ class _FieldTrainLayers(torch.autograd.Function):
                 feat, zft = net.mlp_inputs(x, viewdirs.detach(), latent=lat)
                 outs, grads_out = [], []
                 if nz > 0:
-                    pairs = [(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)]
-                    pairs += [(Gs[b], P[f"scale_z.{b}.weight"].detach()) for b in range(nz if spade else 0)]
                     outs.append(feat)
-                    grads_out.append(sum_of_products(pairs))
+                    if spade:
+                        pairs = [(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)]
+                        pairs += [(Gs[b], P[f"scale_z.{b}.weight"].detach()) for b in range(nz)]
+                        grads_out.append(sum_of_products(pairs))
+                    else:   # the lin_z^T layers on the x3 layer GEMM where they apply (avr.field._feat_grad)
+                        grads_out.append(_feat_grad(fused, entry, bwd, Gz, P, M1))
                 if want_xyz:
                     outs.append(zft)
                     grads_out.append(g_in0 @ P["lin_in.weight"].detach())

@@ -8,7 +8,7 @@ module (models.py:541-592, 739-863). The kernels themselves are held to float64 
 import pytest
 import torch
 
-from avr import _lib, bn_train, layer_train, ops
+from avr import _lib, bn_train, field, layer_train, ops
 
 
 def _net(d_hidden, n_blocks, d_latent, cl, SB, NS, spade, ctype, hw=(6, 7), seed=0):
@@ -73,6 +73,8 @@ def _install(monkeypatch, net):
 
     def weight_of(layer, bwd):
         mlp = cur["mlp"]
+        if layer >= _lib.BN_LAYER_LIN_Z_T:       # the backward blob's lin_z[b]^T (ABI 14)
+            return mlp.lin_z[layer - _lib.BN_LAYER_LIN_Z_T].weight.detach()
         if layer == 0:
             return mlp.lin_in.weight.detach()
         blk = mlp.blocks[(layer - 2) // 2]
@@ -96,8 +98,11 @@ def _install(monkeypatch, net):
         else:
             assert kw["prologue"] == _lib.BN_PLAIN
             op = src
-            mask = torch.relu((kw["pre_rows"] - kw["out_mu"]) * kw["out_scale"] + kw["out_shift"]) > 0
-            out = (src @ W) * mask
+            if kw.get("pre_rows") is None:           # lin_z^T: no mask
+                out = src @ W
+            else:
+                mask = torch.relu((kw["pre_rows"] - kw["out_mu"]) * kw["out_scale"] + kw["out_shift"]) > 0
+                out = (src @ W) * mask
             if kw.get("add1") is not None:           # the residual gradient (ABI 14)
                 out = out + kw["add1"]
         if kw.get("operand_max") is not None:     # publish max |operand| (float bits, max with what is there)
@@ -143,6 +148,7 @@ def _install(monkeypatch, net):
     monkeypatch.setattr(fused, "tables_batch", tables_batch)
     monkeypatch.setattr(layer_train, "_gather", gather)
     monkeypatch.setattr(layer_train, "stream_of", lambda t: None)
+    monkeypatch.setattr(field, "stream_of", lambda t: None)
     monkeypatch.setattr(bn_train, "_layer", lambda **kw: kw)
     monkeypatch.setattr(bn_train, "_run", run)
     monkeypatch.setattr(bn_train, "_partial", lambda M, H, dev: torch.empty(1))
@@ -156,6 +162,7 @@ def _install(monkeypatch, net):
     (16, 3, 64, 2, 2, 2, True, "average"),
     (32, 4, 64, 1, 1, 3, True, "max"),
     (16, 2, 128, 1, 2, 2, False, "max"),
+    (64, 3, 64, 2, 2, 2, False, "average"),     # d_latent == d_hidden: the feature gradient on lin_z^T layers
 ], ids=lambda c: f"h{c[0]}-nb{c[1]}-cl{c[3]}-sb{c[4]}-ns{c[5]}{'-spade' if c[6] else ''}-{c[7]}")
 @pytest.mark.parametrize("coarse", [True, False])
 def test_layer_train_logic_matches_autograd(monkeypatch, case, coarse):
