@@ -125,6 +125,19 @@ class _precision:
         return False
 
 
+# Submodule (re)registrations anywhere in the process: FusedField._state's cached slots are rebuilt after one, so a
+# module replaced in an MLP (mlp.lin_in = nn.Linear(...)) is seen; parameters and buffers replaced in place are read
+# through their owners' dicts anyway.
+_MODULE_GEN = [0]
+
+
+def _module_registered(module, name, submodule):
+    _MODULE_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_module_registration_hook(_module_registered)
+
+
 def _version_key(tensors):
     return tuple((t.data_ptr(), t._version) for t in tensors)
 
@@ -210,16 +223,17 @@ class FusedField:
     # ----------------------------------------------------------- parameters
     def _state(self, mlp):
         """(named parameters, parameters, floating-point buffers) of mlp in named_parameters() / buffers() order,
-        read through each owning module's dict: the module tree is walked once per mlp (a walk per call was a
-        large part of the adaptive step's host time), and a parameter or buffer replaced later is still seen."""
+        read through each owning module's dict: the module tree is walked once per mlp and again after any
+        submodule registration (a walk per call was a large part of the adaptive step's host time), and a
+        parameter or buffer replaced later is still seen."""
         hit = self._slots.get(id(mlp))
-        if hit is None or hit[0] is not mlp:
+        if hit is None or hit[0] is not mlp or hit[3] != _MODULE_GEN[0]:
             mods = list(mlp.named_modules())
             ps = [(f"{mn}.{n}" if mn else n, m._parameters, n) for mn, m in mods
                   for n, t in m._parameters.items() if t is not None]
             bs = [(f"{mn}.{n}" if mn else n, m._buffers, n) for mn, m in mods
                   for n, t in m._buffers.items() if t is not None and t.is_floating_point()]
-            hit = (mlp, ps, bs)
+            hit = (mlp, ps, bs, _MODULE_GEN[0])
             self._slots[id(mlp)] = hit
         named = {full: d[k] for full, d, k in hit[1]}
         return named, list(named.values()), [d[k] for _, d, k in hit[2]]

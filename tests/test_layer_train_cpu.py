@@ -206,3 +206,29 @@ def _check(monkeypatch, case, coarse):
         s = float(ref[k].abs().max()) or 1.0
         err = float((got[k] - ref[k]).abs().max())
         assert err <= 1e-4 * s, f"{k}: {err:.3e} of max |grad| {s:.3e}"
+
+
+def test_fused_field_parameter_slots_follow_replacements():
+    """FusedField._state (the cached per-module slots behind packed() / forward_train's parameter lists): the same
+    tensors as named_parameters() in the same order, a parameter replaced in place and a submodule replaced after
+    the first call both seen, and no rebuild while nothing is registered."""
+    import torch.nn as nn
+    from avr import field as fld
+    net = _net(16, 3, 64, 2, 1, 1, False, "average")
+    fused = net.fused()
+    mlp = net.mlp_coarse
+    named, ps, bs = fused._state(mlp)
+    ref = dict(mlp.named_parameters())
+    assert list(named) == list(ref) and all(named[k] is ref[k] for k in ref)
+    assert [id(t) for t in ps] == [id(t) for t in mlp.parameters()]
+    assert [id(b) for b in bs] == [id(b) for b in mlp.buffers() if b.is_floating_point()]
+    slots = fused._slots[id(mlp)]
+    fused._state(mlp)
+    assert fused._slots[id(mlp)] is slots                      # cached
+    mlp.lin_out.weight = nn.Parameter(torch.zeros_like(mlp.lin_out.weight))
+    assert fused._state(mlp)[0]["lin_out.weight"] is mlp.lin_out.weight
+    old = mlp.lin_in
+    mlp.lin_in = nn.Linear(old.in_features, old.out_features)
+    named = fused._state(mlp)[0]
+    assert named["lin_in.weight"] is mlp.lin_in.weight and named["lin_in.weight"] is not old.weight
+    assert fld._MODULE_GEN[0] == fused._slots[id(mlp)][3]
