@@ -77,7 +77,7 @@ class BnLayer(ctypes.Structure):
                 ("out_shift", c_void_p),
                 ("partial", c_void_p),
                 ("lin_z_table", c_void_p), ("lin_z_scene_stride", i64), ("xyz", c_void_p), ("views", c_void_p),
-                ("n_views", c_int), ("rows_per_scene", i64)]
+                ("n_views", c_int), ("rows_per_scene", i64), ("out_max", c_void_p)]
 
 
 # name -> argtypes (all return int status)

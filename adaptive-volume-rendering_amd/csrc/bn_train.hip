@@ -37,6 +37,7 @@ struct BnArgs {
   // ztab + scene * ztab_stride at zxyz[m] in zviews[scene]), or ztab = null
   const float* ztab; int64_t ztab_stride, zrows;
   const float* zxyz;
+  unsigned* out_max;            // backward: max |out| of the stored rows, or null
   View zviews[AVR_MAX_SCENES];
 };
 
@@ -446,6 +447,19 @@ __global__ void __launch_bounds__(64 * NW, NW > 4 ? 1 : 2) bn_layer_kernel(BnArg
         for (int sg = 0; sg < 4; ++sg) acc[ft][sg] += t[ft][sg];
     }
     store_rows(a.out, acc);
+    if (a.out_max) {   // the stored rows only (dead rows hold row m0's addend)
+      float m = 0.f;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg)
+          if (live(sg)) {
+            const floatx4 v = acc[ft][sg];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          }
+      m = wave_max(m);
+      if (lane == 0) publish_max(a.out_max, m);
+    }
   }
   if (j == 0) {
     float* part = a.part + (int64_t)blockIdx.x * 2 * HID;
@@ -698,6 +712,7 @@ extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* 
     AVR_REQUIRE(ly == 0 || l->in_dim == H, "avr_bn_layer_run: a hidden layer's operand is d_hidden columns");
     a.w = l->blob + (ly == 0 ? L.x3_in : (ly % 2 == 0 ? L.x3_fc0[(ly - 2) / 2] : L.x3_fc1[(ly - 2) / 2]));
     hdr = reinterpret_cast<const unsigned*>(l->blob + L.x3_hdr);
+    AVR_REQUIRE(!l->out_max, "avr_bn_layer_run: out_max is a backward-mode field");
     a.bias = l->bias; a.add1 = l->add1; a.add2 = l->add2;
     if (l->lin_z_table) {
       AVR_REQUIRE(l->xyz && l->views && l->n_views >= 1 && l->n_views <= AVR_MAX_SCENES && l->rows_per_scene > 0 &&
@@ -732,6 +747,7 @@ extern "C" int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* 
     a.pre_rows = l->pre_rows; a.out_mu = l->out_mu; a.out_invstd = l->out_invstd;
     a.out_scale = l->out_scale; a.out_shift = l->out_shift;
     a.add1 = l->add1;
+    a.out_max = l->out_max;
   }
   a.hdr = hdr;
   a.hdr_idx = ly;

@@ -416,6 +416,9 @@ typedef struct {
    * world point xyz[m] (n_rows, 3) in views[s] -- avr_latent_features' lookup and blend, bit for bit. */
   const float* lin_z_table; int64_t lin_z_scene_stride;
   const float* xyz; const avr_view_desc* views; int n_views; int64_t rows_per_scene;
+  /* AVR_BN_BWD (ABI 14): NULL, or max |out| over the stored rows as float bits, max with what is there (the next
+   * weight gradient's scale without a reduction pass over the rows) */
+  uint32_t* out_max;
 } avr_bn_layer;
 int avr_bn_layer_run(const avr_field_dims* dims, const avr_bn_layer* l, void* stream);
 /* Floats of an avr_bn_layer partial buffer for n_rows rows of n_cols columns: the per-workgroup partials

@@ -105,6 +105,9 @@ def _install(monkeypatch, net):
                 out = (src @ W) * mask
             if kw.get("add1") is not None:           # the residual gradient (ABI 14)
                 out = out + kw["add1"]
+        if kw.get("out_max") is not None:         # backward: max |out| of the stored rows (ABI 14)
+            m = torch.maximum(out.abs().max().reshape(1), kw["out_max"][:1].view(torch.float32))
+            kw["out_max"][:1].copy_(m.view(torch.int32))
         if kw.get("operand_max") is not None:     # publish max |operand| (float bits, max with what is there)
             m = torch.maximum(op.abs().max().reshape(1), kw["operand_max"][:1].view(torch.float32))
             kw["operand_max"][:1].copy_(m.view(torch.int32))
