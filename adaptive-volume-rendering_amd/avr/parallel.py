@@ -209,7 +209,12 @@ def render_sharded(render_fn, cam2world, intrinsics, x_pix, tile=64, group=None,
     out = torch.empty(world * SB, cap, 7, device=dev, dtype=torch.float32)
     if timer is not None:
         timer.lap("reassembly")
-    dist.all_gather_into_tensor(out, packed, group=group)
+    if dist.get_backend(group) == "gloo" and dev.type != "cpu":   # gloo moves host memory (one-GPU rehearsals)
+        out_h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(out_h, packed.cpu(), group=group)
+        out.copy_(out_h)
+    else:
+        dist.all_gather_into_tensor(out, packed, group=group)
     if timer is not None:
         timer.lap("all_gather")
     out = out.view(world, SB, cap, 7)

@@ -708,6 +708,12 @@ def pmc_traffic(args, timeout=240):
             "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None, "dispatches": n, "clock_ghz": clock}, "ok"
 
 
+def _comm_device(device):
+    """Where a cross-rank reduction's tensor lives: the GPU on RCCL, the host on gloo."""
+    import torch.distributed as dist
+    return torch.device("cpu") if dist.is_initialized() and dist.get_backend() == "gloo" else device
+
+
 def time_steps(step, steps, warmup, world, device):
     """W untimed steps, then K timed steps between barrier + synchronize on
     both sides; the max over ranks. Returns (seconds, last output)."""
@@ -727,7 +733,7 @@ def time_steps(step, steps, warmup, world, device):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=_comm_device(device), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
     return elapsed, out
@@ -966,8 +972,15 @@ def main():
         if "RANK" not in os.environ:   # --dist at one rank without a launcher: a one-rank rendezvous on 127.0.0.1
             os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                               MASTER_PORT=str(_free_port()))
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if os.environ.get("AVR_BENCH_ONE_GPU_GLOO") == "1":
+            # rehearsal of the N > 1 path on a one-GPU box: every rank on GPU 0, the group on gloo (RCCL needs one
+            # GPU per rank); the timing means nothing, the code path is the multi-GPU one
+            local_rank = 0
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
 
@@ -1061,7 +1074,7 @@ def main():
     field_ms = timer.total_ms()
     field_launches = len(timer.events)
     if use_dist:
-        t = torch.tensor([field_ms], device=device, dtype=torch.float64)
+        t = torch.tensor([field_ms], device=_comm_device(device), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         field_ms = float(t[0])
     assert bool(torch.isfinite(out).all())
