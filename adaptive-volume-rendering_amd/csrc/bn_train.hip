@@ -11,8 +11,9 @@
 // one power-of-two scale per workgroup and written to LDS; the K loop is theirs (x3: three
 // v_mfma_f32_16x16x32_f16 per product, fp32 accumulate, weights streamed one chunk ahead); the epilogue works in
 // the accumulator layout -- adds bias / residual / lin_z rows (forward) or applies the relu mask (backward,
-// recomputed from the pre-BN rows: the relu'd operands are never stored), stores the rows and
-// reduces this workgroup's column statistics. A finalize launch between
+// recomputed from the pre-BN rows: the relu'd operands are never stored; ABI 14: lin_z^T layers without a mask,
+// an added residual gradient and the stored rows' max), stores the rows and reduces this workgroup's column
+// statistics. A finalize launch between
 // layers (bn_stats_kernel / bn_grad_stats_kernel) combines the workgroups' partials in fp64.
 #include "x3_gemm.h"
 
