@@ -210,10 +210,11 @@ class _FieldTrainLayers(torch.autograd.Function):
             # scales for gp2 and g without a reduction pass over the rows): [2b] fc_0^T's, [2b + 1] fc_1^T's
             omax = torch.zeros(2 * nb, device=dev, dtype=torch.int32)
             relu_x = "relu"                                # X = relu(rows), rebuilt in the staging
-            # g_in0 (lin_in's output gradient) is block 0's fc_0^T output as stored unless spade's product or the
-            # views' combine follows it there: its max then comes from that launch (ABI 14 out_max)
-            in0_max = torch.zeros(1, device=dev, dtype=torch.int32) if not spade and not (cl == 0 and NS > 1) \
-                else None
+            # max |stored rows| of each block's fc_0^T launch (ABI 14 out_max): Gz[b] for b < n_lin_z (<= the
+            # combine layer, so no combine adjoint follows them), and g_in0 (lin_in's output gradient) unless
+            # spade's product or the views' combine follows block 0's launch
+            fc0t_max = torch.zeros(max(nb, 1), device=dev, dtype=torch.int32)
+            in0_direct = nb > 0 and not spade and not (cl == 0 and NS > 1)
             for b in range(nb - 1, -1, -1):
                 m = M1 if b < cl else M2
                 # fc_1^T: gradient at N[b]; fc_0^T: the fc_0 path's gradient at X'[b]
@@ -227,8 +228,7 @@ class _FieldTrainLayers(torch.autograd.Function):
                 _run(dims, _layer(n_rows=m, mode=_lib.BN_BWD, prologue=_lib.BN_PLAIN, in_dim=H, in_valid=H, src=gp2,
                                   ld_src=H, operand_max=omax[2 * b:], blob=bwd, layer=2 + 2 * b, out=gin,
                                   pre_rows=Xin[b], out_mu=idt.zero, out_invstd=idt.one, out_scale=idt.one,
-                                  out_shift=idt.zero, add1=g, out_max=in0_max if b == 0 else None,
-                                  partial=part), stream)
+                                  out_shift=idt.zero, add1=g, out_max=fc0t_max[b:b + 1], partial=part), stream)
                 blk[b] = [(gp2, Xin[b], omax[2 * b:2 * b + 1], amax[2 * b:2 * b + 1], True, relu_x),
                           (g, N[b], omax[2 * b + 1:2 * b + 2], amax[2 * b + 1:2 * b + 2], True, relu_x)]
                 if b == cl and NS > 1 and mlp.combine_type == "average":
@@ -241,17 +241,15 @@ class _FieldTrainLayers(torch.autograd.Function):
                         gin, = torch.autograd.grad(yc, xr, gin)
                 if b < nz:
                     Gz[b] = gin.contiguous()
+                    Gz_max[b] = fc0t_max[b:b + 1]
                     if spade:                                  # X' = S * X + T (models.py:585-587)
                         Gs[b] = (gin * Xpre[b]).contiguous()
                         gin = S[b] * gin
-                    elif b > 0:                                # gin is the next fc_1^T's operand: its max comes free
-                        Gz_max[b] = omax[2 * b - 1:2 * b]
                 g = gin.contiguous()
             g_in0 = g                                          # d loss / d lin_in output
             for b in range(nb):
                 (wl1 if b < cl else wl2).extend(blk[b])
-            # (without use_spade also Gz[0]'s: the same rows)
-            g_in0_max = in0_max if (in0_max is not None and nb > 0) else _max_bits(g_in0)
+            g_in0_max = fc0t_max[0:1] if in0_direct else _max_bits(g_in0)
             lat_feat = None
             if nz > 0:
                 hwc = fused.latent_hwc_all(latent)
@@ -260,7 +258,7 @@ class _FieldTrainLayers(torch.autograd.Function):
                 lat_feat = _gather(fused, hwc, K, NS, p, B, net.d_latent)
                 lat_max = fused.latent_max_bits(latent)
                 for b in range(nz):
-                    zmax = Gz_max[b] if Gz_max[b] is not None else g_in0_max if Gz[b] is g_in0 else _max_bits(Gz[b])
+                    zmax = Gz_max[b]
                     wl1.append((Gz[b], lat_feat, zmax, lat_max, True))
                 for b in range(nz if spade else 0):
                     wl1.append((Gs[b], lat_feat, _max_bits(Gs[b]), lat_max, True))
