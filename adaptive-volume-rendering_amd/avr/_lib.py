@@ -151,6 +151,7 @@ _SIGS = {
     "avr_lin_out_fwd_rows": [i64, c_int, c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_lin_out_bwd_rows": [i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, c_void_p, c_void_p,
                              c_void_p],
+    "avr_spade_bwd_rows": [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_stream_copy": [c_void_p, c_void_p, i64, c_void_p],
     "avr_stream_fill": [c_void_p, i64, c_uint32, c_void_p],
 }

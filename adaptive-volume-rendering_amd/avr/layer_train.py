@@ -178,7 +178,7 @@ class _FieldTrainLayers(torch.autograd.Function):
         from .bn_train import _layer, _partial, _run
         from .models import combine_interleaved
         from .field import _feat_grad
-        from .ops import _max_bits, lin_out_rows_bwd, sum_of_products, weight_grads
+        from .ops import _max_bits, lin_out_rows_bwd, spade_bwd_rows, sum_of_products, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         Xpre, Xin, N, S, amax, zfp, a_max, idt, p, cl = ctx.keep
         ctx.keep = None
@@ -204,7 +204,7 @@ class _FieldTrainLayers(torch.autograd.Function):
             d4, g, d4_max = lin_out_rows_bwd(grad_out.reshape(M2, 4), out.reshape(M2, 4),
                                              P["lin_out.weight"].detach(), Xpre[nb])
             wl1, wl2 = [], []           # weight-gradient layers over M1 / M2 rows
-            Gz, Gs, Gz_max = [None] * nz, [None] * nz, [None] * nz
+            Gz, Gs, Gz_max, Gs_max = [None] * nz, [None] * nz, [None] * nz, [None] * nz
             blk = [None] * nb
             # max |operand| of every backward layer call, published by the layer kernels (the weight gradients'
             # scales for gp2 and g without a reduction pass over the rows): [2b] fc_0^T's, [2b + 1] fc_1^T's
@@ -243,8 +243,8 @@ class _FieldTrainLayers(torch.autograd.Function):
                     Gz[b] = gin.contiguous()
                     Gz_max[b] = fc0t_max[b:b + 1]
                     if spade:                                  # X' = S * X + T (models.py:585-587)
-                        Gs[b] = (gin * Xpre[b]).contiguous()
-                        gin = S[b] * gin
+                        # dS = g * X (+ its max for scale_z's weight gradient), dX = S * g: one pass
+                        Gs[b], gin, Gs_max[b] = spade_bwd_rows(Gz[b], Xpre[b].contiguous(), S[b])
                 g = gin.contiguous()
             g_in0 = g                                          # d loss / d lin_in output
             for b in range(nb):
@@ -261,7 +261,7 @@ class _FieldTrainLayers(torch.autograd.Function):
                     zmax = Gz_max[b]
                     wl1.append((Gz[b], lat_feat, zmax, lat_max, True))
                 for b in range(nz if spade else 0):
-                    wl1.append((Gs[b], lat_feat, _max_bits(Gs[b]), lat_max, True))
+                    wl1.append((Gs[b], lat_feat, Gs_max[b], lat_max, True))
             wl1.append((g_in0, zfp, g_in0_max, _max_bits(zfp), True))
             wl2.append((d4, Xpre[nb], d4_max, a_max, True, relu_x))
             if M1 == M2:     # one source view: every layer over the same rows, one launch

@@ -405,6 +405,18 @@ def lin_out_rows_bwd(grad_out, out, weight, pre, g=None):
     return d_raw, g, dmax
 
 
+def spade_bwd_rows(g, x, s):
+    """The spade product rule's backward (avr_spade_bwd_rows): (g * x, s * g, max |g * x| as int32 float bits) in
+    one pass over contiguous fp32 tensors of one shape, bit-identical to torch's two products."""
+    for t in (g, x, s):
+        if t.dtype != F32 or not t.is_contiguous() or t.shape != g.shape or t.data_ptr() % 16:
+            raise _lib.AVRError("spade_bwd_rows: contiguous 16-B aligned fp32 tensors of one shape")
+    gs, g_out = torch.empty_like(g), torch.empty_like(g)
+    gmax = torch.zeros(1, device=g.device, dtype=torch.int32)
+    call("avr_spade_bwd_rows", g.numel(), ptr(g), ptr(x), ptr(s), ptr(gs), ptr(g_out), ptr(gmax), stream_of(g))
+    return gs, g_out, gmax
+
+
 _DW_TILE = 256        # avr_weight_grads output tile (weight_grad.hip kDwTile), one workgroup per CU
 
 

@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
     *(lds_u32x2*)(st + off) = u32x2{hi.x, hi.y};
     *(lds_u32x2*)(st + kDwImg + off) = u32x2{lo.x, lo.y};
     floatx4 xv = xn[u];
-    if constexpr (XF)
+    if constexpr (XF) {
       if (D.xmu) {   // block-uniform; the parameters from LDS (a global load here would make the wait for it
                      // also wait for the chunk loads in flight behind it: the counter is in order)
         const lds_floatx4* P = (const lds_floatx4*)(lds + 2 * kDwStage);
@@ -173,6 +173,7 @@ __global__ void __launch_bounds__(NW * 64, 1) weight_grad_kernel(DwArgs a) {
       } else if (D.xrelu) {   // identity statistics: bn_relu4's result with mu 0, scale 1, shift 0, no parameters
         xv = floatx4{fmaxf(xv.x, 0.f), fmaxf(xv.y, 0.f), fmaxf(xv.z, 0.f), fmaxf(xv.w, 0.f)};
       }
+    }
     split4(xv, sX, hi, lo);
     *(lds_u32x2*)(st + 2 * kDwImg + off) = u32x2{hi.x, hi.y};
     *(lds_u32x2*)(st + 3 * kDwImg + off) = u32x2{lo.x, lo.y};

@@ -440,6 +440,11 @@ int avr_bn_grad_rows(int64_t n_rows, int n_cols, const float* g, const float* pr
  *   sigmoid / relu backward), g (n_rows, d_hidden) = d_raw . weight where pre > 0, else 0 (aten
  *   threshold_backward; pre (n_rows, ld_pre) = lin_out's input before its relu); d_raw_max (or NULL): max |d_raw|
  *   as float bits, max with what is there. */
+/* The spade product rule's backward (ABI 14; avr.layer_train, models.py:585-587: X' = S * X + T): over n values
+ * (a multiple of 4, 16-B aligned arrays) gs = g * x and g_out = s * g, each one fp32 product as torch's mul (bit
+ * for bit); gs_max (or NULL): max |gs| as float bits, max with what is there. */
+int avr_spade_bwd_rows(int64_t n, const float* g, const float* x, const float* s, float* gs, float* g_out,
+                       uint32_t* gs_max, void* stream);
 int avr_lin_out_fwd_rows(int64_t n_rows, int d_hidden, const float* x, int64_t ld_x, const float* weight,
                          const float* bias, float* out, uint32_t* x_max, void* stream);
 int avr_lin_out_bwd_rows(int64_t n_rows, int d_hidden, const float* grad_out, const float* out, const float* weight,

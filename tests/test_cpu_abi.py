@@ -74,6 +74,18 @@ def test_lin_out_rows_argument_checks():
     assert b(4, 256, None, None, None, None, 256, None, None, None, None) == 1001
 
 
+def test_spade_bwd_rows_argument_checks():
+    """avr_spade_bwd_rows (ABI 14): zero values is a no-op; a count not a multiple of 4 and null pointers are
+    refused before any HIP call."""
+    from avr import _lib
+    lib = _lib.load()
+    assert lib.avr_spade_bwd_rows(0, None, None, None, None, None, None, None) == 0
+    assert lib.avr_spade_bwd_rows(6, None, None, None, None, None, None, None) == 1001
+    assert b"multiple of 4" in lib.avr_last_error_string()
+    assert lib.avr_spade_bwd_rows(8, None, None, None, None, None, None, None) == 1001
+    assert b"null" in lib.avr_last_error_string()
+
+
 def test_ops_refuse_host_tensors():
     from avr import _lib, ops
     with pytest.raises(_lib.AVRError):

@@ -203,3 +203,15 @@ def test_lin_z_transposed_layers_vs_fp64(H, nb, cl, M):
     got2 = _feat_grad(f2, e2, f2.packed_bwd(True, e2), Gz2, P2, M)
     ref2 = sum(Gz2[b].double() @ P2[f"lin_z.{b}.weight"].detach().double() for b in range(2))
     assert float((got2.double() - ref2).abs().max() / ref2.abs().max()) <= 2e-6
+
+
+@pytest.mark.parametrize("n", [4, 1000, 512 * 4097])
+def test_spade_bwd_rows_bit_exact(n):
+    """avr_spade_bwd_rows (the spade product rule's backward, ABI 14): g * x and s * g equal torch's products bit
+    for bit, max |g * x| exact."""
+    from avr import ops
+    g0 = torch.Generator().manual_seed(n)
+    g, x, s = (torch.randn(n // 4, 4, generator=g0).to(DEV) for _ in range(3))
+    gs, go, gmax = ops.spade_bwd_rows(g, x, s)
+    assert torch.equal(gs, g * x) and torch.equal(go, s * g)
+    assert int(gmax) == int((g * x).abs().max().reshape(1).view(torch.int32))

@@ -144,6 +144,12 @@ def _install(monkeypatch, net):
             gr = g
         return d4, gr, bits(d4)
 
+    def spade_bwd_rows(g, x, s):
+        """avr_spade_bwd_rows' contract."""
+        gs = g * x
+        return gs, s * g, bits(gs)
+
+    monkeypatch.setattr(ops, "spade_bwd_rows", spade_bwd_rows)
     monkeypatch.setattr(ops, "lin_out_rows", lin_out_rows)
     monkeypatch.setattr(ops, "lin_out_rows_bwd", lin_out_rows_bwd)
     monkeypatch.setattr(fused, "packed", packed)
