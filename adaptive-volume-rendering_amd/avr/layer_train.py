@@ -6,19 +6,20 @@ views, utils.py:71-81), alone or together, ReLU, no BatchNorm.
 Both put an elementwise step between the fused kernels' 64-sample GEMM chains: the spade product needs the
 interpolated scale rows, the combine mixes rows of different views (workgroups), so this path runs the MLP one
 layer at a time on avr_bn_layer_run (the BatchNorm path's x3 layer GEMM over row-major fp32 rows, with identity
-statistics: the operand is relu(x), the backward's mask [pre > 0]) and does the elementwise steps in torch on
-the rows:
+statistics: the operand is relu(x), the backward's mask [pre > 0]) with the elementwise steps between:
   forward   X[0] = lin_in(z_feature); per block b: (b < combine_layer) X'[b] = S_b * X[b] + T_b with T_b / S_b the
-            bilinear blends of the per-texel lin_z / scale_z tables (avr_latent_features on the x3 tables:
-            both carry their biases with use_spade; without it T_b has none, lin_z's bias is folded into the
-            producing layer's bias and T_b is gathered in that layer's epilogue, avr_bn_layer's lin_z_table); (b == combine_layer, NS > 1) X'[b] = combine(X[b]); N[b] = fc_0(relu(X'[b]));
-            X[b+1] = fc_1(relu(N[b])) + X'[b]; out = lin_out(relu(X[nb])), sigmoid / relu.
-  backward  the transposed layers on avr_bn_layer_run (W^T . g masked by [pre > 0]; fc_0^T adds the residual's
-            g in its epilogue), the spade product rule
-            (d X = S * g, d S = g * X, d T = g) and torch's own adjoint of the combine between them; every weight
+            bilinear blends of the per-texel lin_z / scale_z tables (avr_latent_features on the x3 tables: both
+            carry their biases with use_spade, the product in torch; without it T_b has none, lin_z's bias is
+            folded into the producing layer's bias and T_b is gathered in that layer's epilogue, avr_bn_layer's
+            lin_z_table); (b == combine_layer, NS > 1) X'[b] = combine(X[b]) (torch); N[b] = fc_0(relu(X'[b]));
+            X[b+1] = fc_1(relu(N[b])) + X'[b]; out = lin_out(relu(X[nb])), sigmoid / relu (avr_lin_out_fwd_rows).
+  backward  lin_out and its activations (avr_lin_out_bwd_rows); the transposed layers on avr_bn_layer_run
+            (W^T . g masked by [pre > 0]; fc_0^T adds the residual's g in its epilogue and publishes the max of
+            what it stores), the spade product rule (d X = S * g, d S = g * X: avr_spade_bwd_rows; d T = g) and
+            the combine's adjoint (the mean's in closed form, torch's for the max) between them; every weight
             gradient on avr_weight_grads (split-K x3; relu(X) rebuilt from the pre-activation rows in the
             staging), scale_z's against (g * X) rows; the latent / point gradients through the input functions
-            as in avr.field._FieldTrain.
+            as in avr.field._FieldTrain (the features' gradient on the lin_z^T layers where they apply).
 """
 import ctypes
 
