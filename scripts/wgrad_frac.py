@@ -15,16 +15,17 @@ def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
     conf = sys.argv[2] if len(sys.argv) > 2 else "default_mv"
     mac = sum(o * i for o, i in LAYERS[conf])
-    rows_per_pass = {"786432": 4 * 512 * 96, "524288": 4 * 512 * 64}   # bwd grid -> samples (SB x R x N)
+    # the backward chain's workgroups (64 samples each, any wave count) -> samples (SB x R x N) of the pass
+    passes = {4 * 512 * 96: "fine", 4 * 512 * 64: "coarse"}
     pending, out = None, {"fine": [], "coarse": []}
     for r in rows:
         n = r["Kernel_Name"]
         if "field_bwd" in n:
-            pending = r["Grid_Size_X"]
-        elif "weight_grad_kernel" in n and pending in rows_per_pass:
+            pending = int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]) * 64
+        elif "weight_grad_kernel" in n and pending in passes:
             ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-            M = rows_per_pass[pending]
-            out["fine" if pending == "786432" else "coarse"].append((ms, 2.0 * M * mac / (ms * 1e-3) / 1e12, M))
+            M = pending
+            out[passes[pending]].append((ms, 2.0 * M * mac / (ms * 1e-3) / 1e12, M))
     for k, v in out.items():
         v.sort()
         ms, tf, M = v[len(v) // 2]
