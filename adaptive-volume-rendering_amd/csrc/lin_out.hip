@@ -29,8 +29,8 @@ __device__ __forceinline__ float max64(float v, int lane) {
   return v;
 }
 
-// QL = d_hidden / 64 float4 columns per lane
-template <int QL>
+// QL = d_hidden / 64 float4 columns per lane; RR rows per lane group per pass (independent loads in flight)
+template <int QL, int RR>
 __global__ void __launch_bounds__(kLinOutThreads) lin_out_fwd_rows_kernel(int64_t M, const float* __restrict__ x,
                                                                          int64_t ld, const float* __restrict__ w,
                                                                          const float* __restrict__ b,
@@ -45,32 +45,39 @@ __global__ void __launch_bounds__(kLinOutThreads) lin_out_fwd_rows_kernel(int64_
   const floatx4 bias = ld4g(b);
   float amax = 0.f;
   const int64_t nw = (int64_t)gridDim.x * (kLinOutThreads / 64);
-  for (int64_t r0 = ((int64_t)blockIdx.x * (kLinOutThreads / 64) + (threadIdx.x >> 6)) * 4; r0 < M; r0 += nw * 4) {
-    const int64_t row = r0 + rs;
-    const bool valid = row < M;
-    floatx4 xv[QL];
+  for (int64_t r0 = ((int64_t)blockIdx.x * (kLinOutThreads / 64) + (threadIdx.x >> 6)) * 4 * RR; r0 < M;
+       r0 += nw * 4 * RR) {
+    floatx4 xv[RR][QL];
 #pragma unroll
-    for (int i = 0; i < QL; ++i)
-      xv[i] = valid ? ld4g(x + row * ld + 4 * (j + 16 * i)) : floatx4{0.f, 0.f, 0.f, 0.f};
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < RR; ++q) {
+      const int64_t row = r0 + 4 * q + rs;
 #pragma unroll
-    for (int i = 0; i < QL; ++i) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a = fmaxf(xv[i][e], 0.f);
-        amax = fmaxf(amax, a);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s[k] = __builtin_fmaf(a, wv[k][i][e], s[k]);
-      }
+      for (int i = 0; i < QL; ++i)
+        xv[q][i] = row < M ? ld4g(x + row * ld + 4 * (j + 16 * i)) : floatx4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) s[k] = sum16(s[k], lane);
-    if (valid && j == 0) {
-      floatx4 o;
+    for (int q = 0; q < RR; ++q) {
+      const int64_t row = r0 + 4 * q + rs;
+      float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 3; ++k) o[k] = fdiv(1.f, fadd(1.f, expf(-fadd(s[k], bias[k]))));
-      o[3] = fmaxf(fadd(s[3], bias[3]), 0.f);
-      *reinterpret_cast<floatx4*>(out + 4 * row) = o;
+      for (int i = 0; i < QL; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = fmaxf(xv[q][i][e], 0.f);
+          amax = fmaxf(amax, a);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) s[k] = __builtin_fmaf(a, wv[k][i][e], s[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[k] = sum16(s[k], lane);
+      if (row < M && j == 0) {
+        floatx4 o;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o[k] = fdiv(1.f, fadd(1.f, expf(-fadd(s[k], bias[k]))));
+        o[3] = fmaxf(fadd(s[3], bias[3]), 0.f);
+        *reinterpret_cast<floatx4*>(out + 4 * row) = o;
+      }
     }
   }
   if (xmax) {
@@ -79,7 +86,7 @@ __global__ void __launch_bounds__(kLinOutThreads) lin_out_fwd_rows_kernel(int64_
   }
 }
 
-template <int QL>
+template <int QL, int RR>
 __global__ void __launch_bounds__(kLinOutThreads) lin_out_bwd_rows_kernel(
     int64_t M, const float* __restrict__ gout, const float* __restrict__ y, const float* __restrict__ w,
     const float* __restrict__ pre, int64_t ld, float* __restrict__ draw, float* __restrict__ g, unsigned* dmax) {
@@ -92,35 +99,52 @@ __global__ void __launch_bounds__(kLinOutThreads) lin_out_bwd_rows_kernel(
     for (int i = 0; i < QL; ++i) wv[k][i] = ld4g(w + k * H + 4 * (j + 16 * i));
   float m = 0.f;
   const int64_t nw = (int64_t)gridDim.x * (kLinOutThreads / 64);
-  for (int64_t r0 = ((int64_t)blockIdx.x * (kLinOutThreads / 64) + (threadIdx.x >> 6)) * 4; r0 < M; r0 += nw * 4) {
-    const int64_t row = r0 + rs;
-    if (row >= M) continue;   // no cross-row exchange below
-    const floatx4 go = ld4g(gout + 4 * row), yv = ld4g(y + 4 * row);
-    floatx4 d;   // torch's sigmoid / relu backward of the activations, as avr.bn_train wrote them
+  for (int64_t r0 = ((int64_t)blockIdx.x * (kLinOutThreads / 64) + (threadIdx.x >> 6)) * 4 * RR; r0 < M;
+       r0 += nw * 4 * RR) {
+    floatx4 pv[RR][QL], d[RR];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) d[k] = fmul(go[k], fmul(fsub(1.f, yv[k]), yv[k]));
-    d[3] = fmul(go[3], yv[3] > 0.f ? 1.f : 0.f);
-    if (j == 0) *reinterpret_cast<floatx4*>(draw + 4 * row) = d;
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
-    floatx4 pv[QL];
+    for (int q = 0; q < RR; ++q) {
+      const int64_t row = r0 + 4 * q + rs;
+      const int64_t rr = row < M ? row : M - 1;   // a row past the end reloads the last (never stored)
+      const floatx4 go = ld4g(gout + 4 * rr), yv = ld4g(y + 4 * rr);
 #pragma unroll
-    for (int i = 0; i < QL; ++i) pv[i] = ld4g(pre + row * ld + 4 * (j + 16 * i));
+      for (int i = 0; i < QL; ++i) pv[q][i] = ld4g(pre + rr * ld + 4 * (j + 16 * i));
+      // torch's sigmoid / relu backward of the activations, as avr.bn_train wrote them
 #pragma unroll
-    for (int i = 0; i < QL; ++i) {
-      floatx4 o;
+      for (int k = 0; k < 3; ++k) d[q][k] = fmul(go[k], fmul(fsub(1.f, yv[k]), yv[k]));
+      d[q][3] = fmul(go[3], yv[3] > 0.f ? 1.f : 0.f);
+    }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = __builtin_fmaf(d[3], wv[3][i][e], __builtin_fmaf(d[2], wv[2][i][e],
-                                       __builtin_fmaf(d[1], wv[1][i][e], fmul(d[0], wv[0][i][e]))));
-        o[e] = pv[i][e] <= 0.f ? 0.f : v;   // aten threshold_backward(v, pre, 0)
+    for (int q = 0; q < RR; ++q) {
+      const int64_t row = r0 + 4 * q + rs;
+      if (row >= M) continue;   // no cross-lane exchange below
+      if (j == 0) *reinterpret_cast<floatx4*>(draw + 4 * row) = d[q];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(d[q][0]), fabsf(d[q][1])), fmaxf(fabsf(d[q][2]), fabsf(d[q][3]))));
+#pragma unroll
+      for (int i = 0; i < QL; ++i) {
+        floatx4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = __builtin_fmaf(d[q][3], wv[3][i][e], __builtin_fmaf(d[q][2], wv[2][i][e],
+                                         __builtin_fmaf(d[q][1], wv[1][i][e], fmul(d[q][0], wv[0][i][e]))));
+          o[e] = pv[q][i][e] <= 0.f ? 0.f : v;   // aten threshold_backward(v, pre, 0)
+        }
+        __builtin_nontemporal_store(o, reinterpret_cast<floatx4*>(g + row * H + 4 * (j + 16 * i)));
       }
-      __builtin_nontemporal_store(o, reinterpret_cast<floatx4*>(g + row * H + 4 * (j + 16 * i)));
     }
   }
   if (dmax) {
     m = max64(m, lane);
     if (lane == 0) publish_max(dmax, m);
   }
+}
+
+// rows per lane group per pass: the forward one, the backward two (scripts/lin_out_bench.py at 131 072 / 98 304
+// rows: forward 54 / 45 us with one row, 56 / 49 with two; backward 91 / 78 with one, 88 / 66 with two);
+// AVR_LIN_OUT_RR=1|2 sets both (A/B)
+static int lin_out_rr(int dflt) {
+  const char* e = getenv("AVR_LIN_OUT_RR");
+  return e ? (atoi(e) == 1 ? 1 : 2) : dflt;
 }
 
 static unsigned lin_out_grid(int64_t M) {
@@ -133,16 +157,22 @@ static unsigned lin_out_grid(int64_t M) {
 
 using namespace avr;
 
-#define AVR_LIN_OUT_DISPATCH(H, KERNEL, ...)                                  \
-  switch (H) {                                                                \
-    case 64: KERNEL<1><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;   \
-    case 128: KERNEL<2><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;  \
-    case 192: KERNEL<3><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;  \
-    case 256: KERNEL<4><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;  \
-    case 320: KERNEL<5><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;  \
-    case 384: KERNEL<6><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;  \
-    case 448: KERNEL<7><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;  \
-    default: KERNEL<8><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;   \
+#define AVR_LIN_OUT_CASES(RR, KERNEL, ...)                                         \
+  switch (H) {                                                                     \
+    case 64: KERNEL<1, RR><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;    \
+    case 128: KERNEL<2, RR><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;   \
+    case 192: KERNEL<3, RR><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;   \
+    case 256: KERNEL<4, RR><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;   \
+    case 320: KERNEL<5, RR><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;   \
+    case 384: KERNEL<6, RR><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;   \
+    case 448: KERNEL<7, RR><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;   \
+    default: KERNEL<8, RR><<<grid, kLinOutThreads, 0, s>>>(__VA_ARGS__); break;    \
+  }
+#define AVR_LIN_OUT_DISPATCH(RR_DEFAULT, KERNEL, ...)            \
+  if (lin_out_rr(RR_DEFAULT) == 1) {                              \
+    AVR_LIN_OUT_CASES(1, KERNEL, __VA_ARGS__)                     \
+  } else {                                                        \
+    AVR_LIN_OUT_CASES(2, KERNEL, __VA_ARGS__)                     \
   }
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -158,7 +188,8 @@ extern "C" int avr_lin_out_fwd_rows(int64_t n_rows, int d_hidden, const float* x
               "avr_lin_out_fwd_rows: 16-B aligned rows and tensors (ld_x %lld)", (long long)ld_x);
   const unsigned grid = lin_out_grid(n_rows);
   hipStream_t s = as_stream(stream);
-  AVR_LIN_OUT_DISPATCH(d_hidden, lin_out_fwd_rows_kernel, n_rows, x, ld_x, weight, bias, out, x_max)
+  const int H = d_hidden;
+  AVR_LIN_OUT_DISPATCH(1, lin_out_fwd_rows_kernel, n_rows, x, ld_x, weight, bias, out, x_max)
   return check_launch("lin_out_fwd_rows_kernel");
 }
 
@@ -174,7 +205,7 @@ extern "C" int avr_lin_out_bwd_rows(int64_t n_rows, int d_hidden, const float* g
               "avr_lin_out_bwd_rows: 16-B aligned rows and tensors (ld_pre %lld)", (long long)ld_pre);
   const unsigned grid = lin_out_grid(n_rows);
   hipStream_t s = as_stream(stream);
-  AVR_LIN_OUT_DISPATCH(d_hidden, lin_out_bwd_rows_kernel, n_rows, grad_out, out, weight, pre, ld_pre, d_raw, g,
-                       d_raw_max)
+  const int H = d_hidden;
+  AVR_LIN_OUT_DISPATCH(2, lin_out_bwd_rows_kernel, n_rows, grad_out, out, weight, pre, ld_pre, d_raw, g, d_raw_max)
   return check_launch("lin_out_bwd_rows_kernel");
 }
