@@ -319,7 +319,7 @@ class _FieldTrainBN(torch.autograd.Function):
                 x = xyz.detach().requires_grad_(want_xyz)
                 feat, zft = net.mlp_inputs(x, viewdirs.detach(), latent=lat)
                 outs, grads_out = [], []
-                if nz > 0:
+                if nz > 0 and not net.stop_encoder_grad:   # a detached lookup (models.py:810-811) carries none
                     outs.append(feat)
                     grads_out.append(sum_of_products([(Gx[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)]))
                 if want_xyz:

@@ -663,7 +663,8 @@ class _FieldTrain(torch.autograd.Function):
         # lin_out (4 outputs): d out through sigmoid / relu (torch: g * (1 - y) * y, g * (y > 0))
         y = out.reshape(Mt, 4)
         go = grad_out.reshape(Mt, 4)
-        d4 = torch.cat([go[:, :3] * ((1.0 - y[:, :3]) * y[:, :3]), go[:, 3:] * (y[:, 3:] > 0)], -1).contiguous()
+        d4 = torch.cat([torch.ops.aten.sigmoid_backward(go[:, :3], y[:, :3]),
+                        torch.ops.aten.threshold_backward(go[:, 3:], y[:, 3:], 0.0)], -1).contiguous()
         layers.append((d4, act[2 * nb], _max_bits(d4), act_max[2 * nb:2 * nb + 1], True))
         res = weight_grads(layers, Mt)
         grads = {"lin_out.weight": res[-1][0], "lin_out.bias": res[-1][1]}

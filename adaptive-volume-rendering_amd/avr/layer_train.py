@@ -296,7 +296,9 @@ class _FieldTrainLayers(torch.autograd.Function):
                 x = xyz.detach().requires_grad_(want_xyz)
                 feat, zft = net.mlp_inputs(x, viewdirs.detach(), latent=lat)
                 outs, grads_out = [], []
-                if nz > 0:
+                # with stop_encoder_grad the looked-up latent is detached (models.py:810-811): no gradient reaches
+                # the points through the lookup, z_feature's part alone (as avr.field._FieldTrain)
+                if nz > 0 and not net.stop_encoder_grad:
                     outs.append(feat)
                     if spade:
                         pairs = [(Gz[b], P[f"lin_z.{b}.weight"].detach()) for b in range(nz)]

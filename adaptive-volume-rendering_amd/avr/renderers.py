@@ -389,18 +389,19 @@ class _MarchTrain(torch.autograd.Function):
         n = rd.shape[0]
         R = n // SB
         with torch.no_grad():
-            # deterministic backward (ABI 13): the table gradient in fp64, the parameter sums in a fixed order
-            d_tab64 = torch.zeros(tables.shape, device=rd.device, dtype=torch.float64)
+            # bit-deterministic backward (ABI 15): the table gradient as int64 fixed-point sums, the parameter sums
+            # in a fixed order; no floating-point atomics
+            d_tab = torch.empty(tables.shape, device=rd.device, dtype=torch.float32)
             d_grads = torch.empty(64 * 16 + 64 + 16 + 1, device=rd.device, dtype=torch.float32)
-            ns = ctypes.c_int64(0)
-            _lib.check(_lib.load().avr_raymarch_bwd_scratch_floats(n, ctypes.byref(ns)), "avr_raymarch_bwd_scratch_floats")
-            scratch = torch.empty(max(ns.value, 1), device=rd.device, dtype=torch.float32)
+            nb = ctypes.c_int64(0)
+            _lib.check(_lib.load().avr_raymarch_bwd_scratch_bytes(n, ctx.steps, tables.numel(), ctypes.byref(nb)),
+                       "avr_raymarch_bwd_scratch_bytes")
+            scratch = torch.empty(max(nb.value, 1), device=rd.device, dtype=torch.uint8)
             gw = grad_world.float().reshape(n, 3).contiguous()
             stop = bool(getattr(ctx.phi, "stop_encoder_grad", False))   # detached lookup: no position gradient
             _lib.call("avr_raymarch_bwd", ctx.views, SB, _lib.ptr(tables), _lib.ptr(P[0]), _lib.ptr(P[3]),
                       _lib.ptr(rd), _lib.ptr(trace), _lib.ptr(state), _lib.ptr(gw), R, ctx.steps, 0 if stop else 1,
-                      _lib.ptr(d_tab64), _lib.ptr(d_grads), _lib.ptr(scratch), _lib.stream_of(gw))
-            d_tab = d_tab64.float()
+                      _lib.ptr(d_tab), _lib.ptr(d_grads), _lib.ptr(scratch), scratch.numel(), _lib.stream_of(gw))
             d_whh = d_grads[:1024].reshape(64, 16)
             d_b = d_grads[1024:1088]
             d_wout = d_grads[1088:1104].reshape(1, 16)

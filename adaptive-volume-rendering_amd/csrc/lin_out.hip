@@ -109,10 +109,11 @@ __global__ void __launch_bounds__(kLinOutThreads) lin_out_bwd_rows_kernel(
       const floatx4 go = ld4g(gout + 4 * rr), yv = ld4g(y + 4 * rr);
 #pragma unroll
       for (int i = 0; i < QL; ++i) pv[q][i] = ld4g(pre + rr * ld + 4 * (j + 16 * i));
-      // torch's sigmoid / relu backward of the activations, as avr.bn_train wrote them
+      // aten's sigmoid_backward ((go (1 - y)) y, left to right) and ReluBackward's threshold_backward (a select:
+      // go where y > 0, else 0 -- a NaN / inf go on an inactive sigma gives 0, as torch's)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) d[q][k] = fmul(go[k], fmul(fsub(1.f, yv[k]), yv[k]));
-      d[q][3] = fmul(go[3], yv[3] > 0.f ? 1.f : 0.f);
+      for (int k = 0; k < 3; ++k) d[q][k] = fmul(fmul(go[k], fsub(1.f, yv[k])), yv[k]);
+      d[q][3] = yv[3] > 0.f ? go[3] : 0.f;
     }
 #pragma unroll
     for (int q = 0; q < RR; ++q) {

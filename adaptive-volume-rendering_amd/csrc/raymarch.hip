@@ -92,7 +92,8 @@ __global__ void __launch_bounds__(256) raymarch_kernel(View v, const float* __re
 // per step the point, h, c and the four gate activations. Backward, one ray per 16 lanes in reverse step order:
 //   dsd = rd . dx;  dh = clamp(w_out dsd + W_hh^T dg_next, -10, 10)   (the reference's hook on state[0])
 //   LSTMCell backward -> dg (64 gate pre-activations)
-//   d table[texel] += w_corner dg (atomics: W_ih's gradient is then dT^T latent, the latent's W_ih^T dT)
+//   d table[texel] += w_corner dg (fixed-point int64 sums, below: W_ih's gradient is then dT^T latent, the
+//   latent's W_ih^T dT)
 //   dx += R^T d(xc) of the bilinear lookup's position gradient (grid_sample border / align_corners=True
 //         backward: zero where the coordinate was clipped)
 // with W_hh, the biases and out_layer's gradients summed per workgroup.
@@ -216,12 +217,29 @@ __global__ void __launch_bounds__(256) raymarch_train_kernel(MarchScenes sc, con
 constexpr int kMarchGrads = kGates * kHid + kGates + kHid + 1;
 constexpr int kMarchRays = 256 / kHid;   // rays per workgroup
 
-// Deterministic backward (round 5): the table gradient is summed in fp64 atomics (order-independent to ~1e-16
-// relative, so its fp32 image is the same bits run after run), and the parameter gradients are summed in a fixed
-// order -- the 4 rays of a wave by two xor shuffles (commutative adds: every lane ends with the same bits), the 4
-// waves of a workgroup in wave order through LDS, the workgroups in block order by raymarch_grads_reduce_kernel.
-// With float atomics in both places two identical train.py steps differed in the LSTM gradients' last bits, and
-// one Adam step turned that into different parameters (tests/test_gpu_poison.py).
+// Bit-deterministic backward (ABI 15): no floating-point atomics anywhere.
+//  * raymarch_bwd_kernel runs the reverse recursion per ray and stores, per step and ray, the 64 gate-gradient
+//    values dg and the lookup's 4 texels and weights (instead of scattering them), plus max |dg| over the finite
+//    values (an unsigned max of the float bits: order-independent) and a flag for non-finite ones. The parameter
+//    gradients are summed in a fixed order -- the 4 rays of a wave by two xor shuffles (commutative adds: every
+//    lane ends with the same bits), the 4 waves of a workgroup in wave order through LDS, the workgroups in block
+//    order by raymarch_grads_reduce_kernel.
+//  * raymarch_table_scatter_kernel adds every contribution w_corner * dg to the table gradient as an int64 fixed-
+//    point value under one power-of-two scale 2^s per launch, chosen from max |dg| and the number of contributions
+//    so no sum can overflow. Integer addition is associative: the sums are the same bits in any atomic order.
+//    Each contribution is the exact double product w * dg rounded once to the fixed-point grid (an error of at
+//    most 2^(cbits - 62) of max |dg|, 2^-45 with the 2^17 contributions of a train.py step): far below fp32
+//    resolution relative to the largest gradient, which is how the table gradient is consumed (W_ih's gradient
+//    sums over every texel; the latent's is compared at that scale).
+//  * raymarch_table_finish_kernel converts the sums to fp32 (ldexp(sum, -s), rounded once); an entry that a
+//    non-finite dg reached is NaN (the reference's scatter would carry the NaN there too).
+// Round 5 summed the table gradient in fp64 atomics instead: order-dependent at 2^-53, so one fp32 rounding in a
+// great many could differ run to run, and one Adam step amplifies such a bit.
+struct MarchCtl {
+  unsigned max_bits;   // max |dg| over finite values, float bits
+  unsigned bad;        // nonzero if some dg was NaN / inf
+};
+
 __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const float* __restrict__ tables,
                                                            int64_t table_stride, const float* __restrict__ w_hh,
                                                            const float* __restrict__ w_out,
@@ -230,7 +248,8 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
                                                            const float* __restrict__ state,
                                                            const float* __restrict__ grad_world, int64_t n_per_scene,
                                                            int64_t n_rays, int steps, int pos_grad,
-                                                           double* __restrict__ d_tables,
+                                                           float* __restrict__ dg_rows, float* __restrict__ lk_rows,
+                                                           MarchCtl* __restrict__ ctl,
                                                            float* __restrict__ grad_partials) {
   // W_hh^T dg per step: red (ray, unit k, column j); after the loop the same LDS holds the per-wave parameter
   // sums wsum (the loop's last barrier ends every read of red)
@@ -245,7 +264,6 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
   const int scene = (int)(ray / n_per_scene);
   const View& v = sc.v[scene];
   const float* table = tables + scene * table_stride;
-  double* dtab = d_tables + scene * table_stride;
   float wr[4][kHid];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -261,6 +279,8 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
 #pragma unroll
     for (int j = 0; j < kHid; ++j) dWhh[q][j] = 0.f;
   float dh_next = 0.f, dc_next = 0.f;
+  float dg_max = 0.f;
+  bool dg_bad = false;
   for (int s = steps - 1; s >= 0; --s) {
     const float* st = state + ((int64_t)s * n_rays + ray) * kMarchState;
     const float h = st[k], c = st[kHid + k];
@@ -299,10 +319,12 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
     }
 #pragma unroll
     for (int j = 0; j < kHid; ++j) red[rl][k][j] = part[j];
-    // the lookup at x_s: table gradient and the position gradient
+    // the lookup at x_s: its table gradient is scattered later (dg and the lookup stored), the position gradient
+    // here
     const float* xs = trace + (int64_t)s * n_rays * 3 + 3 * ray;
     const LookupGrad L = lookup_grad(v, xs[0], xs[1], xs[2]);
     float gix = 0.f, giy = 0.f;
+    const int64_t rs = (int64_t)s * n_rays + ray;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int row = q * kHid + k;
@@ -311,11 +333,13 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
       gix += dg[q] * (L.wy0 * (tne - tnw) + L.wy1 * (tse - tsw));
       giy += dg[q] * (L.wx0 * (tsw - tnw) + L.wx1 * (tse - tne));
       if (live) {
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc)
-          atomicAdd(dtab + (int64_t)L.bl.tex[cc] * kGates + row, (double)(L.bl.w[cc] * dg[q]));
+        dg_rows[rs * kGates + row] = dg[q];
+        const float a = fabsf(dg[q]);
+        if (a <= 3.402823466e38f) dg_max = fmaxf(dg_max, a);   // finite (a NaN fails the compare)
+        else dg_bad = true;
       }
     }
+    if (live && k < 8) lk_rows[rs * 8 + k] = k < 4 ? __int_as_float(L.bl.tex[k]) : L.bl.w[k - 4];
 #pragma unroll
     for (int d = kHid / 2; d > 0; d >>= 1) {
       gix += __shfl_xor(gix, d, kHid);
@@ -337,6 +361,16 @@ __global__ void __launch_bounds__(256) raymarch_bwd_kernel(MarchScenes sc, const
     for (int kk = 0; kk < kHid; ++kk) acc += red[rl][kk][k];
     dh_next = acc;
     __syncthreads();   // red read before the next step overwrites it
+  }
+  // max |dg| and the non-finite flag of the wave: one unsigned max / or per wave (order-independent)
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    dg_max = fmaxf(dg_max, __shfl_xor(dg_max, d));
+    dg_bad = __shfl_xor((int)dg_bad, d) | (int)dg_bad;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&ctl->max_bits, __float_as_uint(dg_max));
+    if (dg_bad) atomicOr(&ctl->bad, 1u);
   }
   // this workgroup's parameter gradients (dead rays contribute nothing), summed in a fixed order
   if (!live) {
@@ -385,6 +419,59 @@ __global__ void __launch_bounds__(256) raymarch_grads_reduce_kernel(const float*
   d_grads[i] = s;
 }
 
+// The fixed-point exponent: every |w * dg| <= max |dg| < 2^e, so |w * dg * 2^s| < 2^(62 - cbits) and a sum of
+// at most 2^cbits contributions stays below 2^62.
+__device__ __forceinline__ int march_fixed_exp(const MarchCtl* ctl, int cbits) {
+  const float m = __uint_as_float(ctl->max_bits);
+  if (!(m > 0.f)) return 0;
+  int e;
+  frexpf(m, &e);   // m = f 2^e, f in [0.5, 1)
+  return 62 - cbits - e;
+}
+
+// One wave per (step, ray): lane r adds w_c * dg[r] into the 4 corner texels' row r (64 consecutive int64 per
+// corner: coalesced atomics).
+__global__ void __launch_bounds__(256) raymarch_table_scatter_kernel(const float* __restrict__ dg_rows,
+                                                                     const float* __restrict__ lk_rows,
+                                                                     const MarchCtl* __restrict__ ctl,
+                                                                     int64_t n_rays, int64_t n_per_scene,
+                                                                     int64_t table_stride, int64_t n_rs, int cbits,
+                                                                     unsigned long long* __restrict__ acc,
+                                                                     float* __restrict__ d_tables) {
+  const int64_t rs = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (rs >= n_rs) return;
+  const int r = threadIdx.x & 63;
+  const int64_t ray = rs % n_rays;
+  const int64_t base = (ray / n_per_scene) * table_stride;
+  const int sc = march_fixed_exp(ctl, cbits);
+  const float g = dg_rows[rs * kGates + r];
+  const bool finite = fabsf(g) <= 3.402823466e38f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int tex = __float_as_int(lk_rows[rs * 8 + c]);
+    const float w = lk_rows[rs * 8 + 4 + c];
+    const int64_t i = base + (int64_t)tex * kGates + r;
+    if (finite) {
+      const double prod = (double)w * (double)g;                 // exact (two fp32 factors)
+      const long long q = (long long)rint(ldexp(prod, sc));     // one rounding onto the fixed-point grid
+      if (q != 0) atomicAdd(acc + i, (unsigned long long)q);    // two's complement: signed sums
+    } else {
+      d_tables[i] = __int_as_float(0x7fc00000);                 // NaN marker (every writer stores the same bits)
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) raymarch_table_finish_kernel(const unsigned long long* __restrict__ acc,
+                                                                    const MarchCtl* __restrict__ ctl, int64_t n,
+                                                                    int cbits, float* __restrict__ d_tables) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int sc = march_fixed_exp(ctl, cbits);
+  const bool bad = ctl->bad != 0u;
+  if (bad && d_tables[i] != d_tables[i]) return;               // a non-finite contribution reached this entry
+  d_tables[i] = (float)ldexp((double)(long long)acc[i], -sc);
+}
+
 }  // namespace avr
 
 using namespace avr;
@@ -422,18 +509,45 @@ extern "C" int avr_raymarch_train(const avr_view_desc* views, int n_scenes, cons
   return check_launch("raymarch_train_kernel");
 }
 
-extern "C" int avr_raymarch_bwd_scratch_floats(int64_t n_rays, int64_t* n_floats) {
-  AVR_REQUIRE(n_rays >= 0 && n_floats, "avr_raymarch_bwd_scratch_floats: bad arguments");
-  *n_floats = ((n_rays + kMarchRays - 1) / kMarchRays) * kMarchGrads;
+// scratch regions of avr_raymarch_bwd, 256-B aligned: the int64 table accumulators, dg rows, lookup rows,
+// the workgroups' parameter partials, the control words
+struct MarchScratch {
+  int64_t acc, dg, lk, partials, ctl, total;
+};
+
+static MarchScratch march_scratch(int64_t n_rays, int steps, int64_t table_entries) {
+  const auto up = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  MarchScratch m;
+  m.acc = 0;
+  m.dg = m.acc + up(table_entries * 8);
+  m.lk = m.dg + up((int64_t)steps * n_rays * kGates * 4);
+  m.partials = m.lk + up((int64_t)steps * n_rays * 8 * 4);
+  m.ctl = m.partials + up(((n_rays + kMarchRays - 1) / kMarchRays) * kMarchGrads * 4);
+  m.total = m.ctl + up(sizeof(MarchCtl));
+  return m;
+}
+
+extern "C" int avr_raymarch_bwd_scratch_bytes(int64_t n_rays, int steps, int64_t table_entries, int64_t* n_bytes) {
+  AVR_REQUIRE(n_rays >= 0 && steps >= 0 && table_entries >= 0 && n_bytes,
+              "avr_raymarch_bwd_scratch_bytes: bad arguments");
+  *n_bytes = march_scratch(n_rays, steps, table_entries).total;
   return AVR_OK;
 }
 
 extern "C" int avr_raymarch_bwd(const avr_view_desc* views, int n_scenes, const float* gate_tables,
                                 const float* w_hh, const float* w_out, const float* rd, const float* trace,
                                 const float* state, const float* grad_world, int64_t n_per_scene, int steps,
-                                int lookup_grad, double* d_tables, float* d_grads, float* scratch, void* stream) {
+                                int lookup_grad, float* d_tables, float* d_grads, void* scratch,
+                                int64_t scratch_bytes, void* stream) {
   AVR_REQUIRE(n_per_scene >= 0 && steps >= 0, "avr_raymarch_bwd: negative size");
-  if (n_per_scene == 0 || steps == 0) return AVR_OK;
+  if (n_per_scene == 0 || steps == 0) {   // nothing marched: every gradient is zero (written whole, as below)
+    hipStream_t s = as_stream(stream);
+    bool ok = !d_grads || hipMemsetAsync(d_grads, 0, kMarchGrads * sizeof(float), s) == hipSuccess;
+    if (d_tables && views && n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES)
+      ok = ok && hipMemsetAsync(d_tables, 0, (size_t)views[0].latent_h * views[0].latent_w * kGates * n_scenes *
+                                                 sizeof(float), s) == hipSuccess;
+    return ok ? AVR_OK : fail(AVR_E_HIP, "avr_raymarch_bwd: memset");
+  }
   MarchScenes sc;
   int rc = march_scenes(views, n_scenes, &sc, "avr_raymarch_bwd");
   if (rc) return rc;
@@ -441,16 +555,42 @@ extern "C" int avr_raymarch_bwd(const avr_view_desc* views, int n_scenes, const 
               "avr_raymarch_bwd: null pointer");
   const int64_t n = n_per_scene * n_scenes;
   const int64_t stride = (int64_t)views[0].latent_h * views[0].latent_w * kGates;
+  const int64_t entries = stride * n_scenes;
   const int64_t blocks = (n + kMarchRays - 1) / kMarchRays;
-  AVR_REQUIRE(blocks < (1ll << 31), "avr_raymarch_bwd: too many rays");
-  raymarch_bwd_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(
-      sc, gate_tables, stride, w_hh, w_out, rd, trace, state, grad_world, n_per_scene, n, steps, lookup_grad ? 1 : 0,
-      d_tables, scratch);
+  const int64_t n_rs = (int64_t)steps * n;
+  AVR_REQUIRE(blocks < (1ll << 31) && (n_rs + 3) / 4 < (1ll << 31), "avr_raymarch_bwd: too many rays");
+  // every table entry receives at most n_rs * 4 contributions (4 corners per lookup)
+  int cbits = 0;
+  while (cbits < 40 && (1ll << cbits) < n_rs * 4) ++cbits;
+  AVR_REQUIRE(cbits <= 30, "avr_raymarch_bwd: too many ray steps for the fixed-point sums");
+  const MarchScratch m = march_scratch(n, steps, entries);
+  AVR_REQUIRE(scratch_bytes >= m.total, "avr_raymarch_bwd: scratch of %lld bytes < %lld",
+              (long long)scratch_bytes, (long long)m.total);
+  char* sb = static_cast<char*>(scratch);
+  auto* acc = reinterpret_cast<unsigned long long*>(sb + m.acc);
+  auto* dg_rows = reinterpret_cast<float*>(sb + m.dg);
+  auto* lk_rows = reinterpret_cast<float*>(sb + m.lk);
+  auto* partials = reinterpret_cast<float*>(sb + m.partials);
+  auto* ctl = reinterpret_cast<MarchCtl*>(sb + m.ctl);
+  hipStream_t s = as_stream(stream);
+  if (hipMemsetAsync(acc, 0, (size_t)entries * 8, s) != hipSuccess ||
+      hipMemsetAsync(ctl, 0, sizeof(MarchCtl), s) != hipSuccess ||
+      hipMemsetAsync(d_tables, 0, (size_t)entries * 4, s) != hipSuccess)
+    return fail(AVR_E_HIP, "avr_raymarch_bwd: memset");
+  raymarch_bwd_kernel<<<(unsigned)blocks, 256, 0, s>>>(sc, gate_tables, stride, w_hh, w_out, rd, trace, state,
+                                                       grad_world, n_per_scene, n, steps, lookup_grad ? 1 : 0,
+                                                       dg_rows, lk_rows, ctl, partials);
   rc = check_launch("raymarch_bwd_kernel");
   if (rc) return rc;
-  raymarch_grads_reduce_kernel<<<(kMarchGrads + 255) / 256, 256, 0, as_stream(stream)>>>(scratch, (int)blocks,
-                                                                                         d_grads);
-  return check_launch("raymarch_grads_reduce_kernel");
+  raymarch_grads_reduce_kernel<<<(kMarchGrads + 255) / 256, 256, 0, s>>>(partials, (int)blocks, d_grads);
+  rc = check_launch("raymarch_grads_reduce_kernel");
+  if (rc) return rc;
+  raymarch_table_scatter_kernel<<<(unsigned)((n_rs + 3) / 4), 256, 0, s>>>(dg_rows, lk_rows, ctl, n, n_per_scene,
+                                                                            stride, n_rs, cbits, acc, d_tables);
+  rc = check_launch("raymarch_table_scatter_kernel");
+  if (rc) return rc;
+  raymarch_table_finish_kernel<<<(unsigned)((entries + 255) / 256), 256, 0, s>>>(acc, ctl, entries, cbits, d_tables);
+  return check_launch("raymarch_table_finish_kernel");
 }
 
 extern "C" int avr_raymarch(const avr_view_desc* view, const float* gate_table, const float* w_hh, const float* b_ih,

@@ -406,7 +406,7 @@ def cpu_baseline(c3_rays=384, c1_rays=4096):
             "wall_s": round(time.perf_counter() - t0, 1)}
 
 
-def run_train(args, device):
+def run_train(args, device, train_pmc=None):
     """--mode train: one train.py step (train.py:50-114) per step — SB = 4
     scenes x 512 rays (train.py defaults batch_size 4, ray_batch_size 512),
     the conf/default.conf renderer (64 coarse + 32 fine of which 16 depth
@@ -505,6 +505,12 @@ def run_train(args, device):
         if "torch" in nonfinite:
             line["torch_autograd"]["nonfinite_loss"] = nonfinite["torch"]
         line["speedup_vs_torch_autograd"] = round(res["torch"] / res["hip"], 3)
+    if train_pmc is not None:
+        kern, note = train_pmc
+        line["pmc"] = kern if kern is not None else {"note": note}
+        line["pmc_source"] = ("rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE over a child bench.py "
+                              "--pmc-child of this train step (1 warm-up + 1 step): mfma_busy = busy cycles / "
+                              "(1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), clock = GRBM_GUI_ACTIVE / 8 / dispatch time")
     print(json.dumps(line), flush=True)
 
 
@@ -650,14 +656,16 @@ def _run_killable(cmd, timeout, env):
     return p.returncode, out, err
 
 
-def pmc_traffic(args, timeout=240):
-    """The `roofline.traffic` leg, measured in this run: two rocprofv3 --pmc
-    passes (FETCH_SIZE; WRITE_SIZE + TCC_HIT/MISS -- counter groups that fit
-    one pass each, MI355X_MICROARCH.md) over a child `bench.py --pmc-child`
-    (the same C3 workload: one warm-up + one timed step), started BEFORE this
-    process touches the GPU. Per field_x3_kernel dispatch: L2->fabric bytes =
-    2 x FETCH_SIZE (gfx950 counts half of 16-B-per-lane reads) + WRITE_SIZE,
-    Infinity-Cache hits included. Returns (dict or None, note)."""
+def _short_kernel(name):
+    import re
+    return re.sub(r"\(.*", "", name).replace("void ", "").strip()
+
+
+def pmc_passes(child_args, groups, match, timeout=240):
+    """rocprofv3 --pmc passes over a child `bench.py --pmc-child <child_args>`, one pass per counter group (each
+    group within one pass's limits, MI355X_MICROARCH.md), started BEFORE this process touches the GPU. Returns
+    ({kernel: {counter: mean per dispatch, "dispatches": n, "mean_ns": mean dispatch time}} over the kernels
+    whose name contains one of `match`, note)."""
     import csv
     import glob
     import shutil
@@ -668,44 +676,102 @@ def pmc_traffic(args, timeout=240):
     tmp = tempfile.mkdtemp(prefix="avr_pmc_", dir=os.environ.get("TMPDIR") or "/tmp")
     env = dict(os.environ)
     env.setdefault("TMPDIR", "/tmp")
-    per = {}
+    vals, durs = {}, {}
     try:
-        durs = []
-        for counters in (["FETCH_SIZE", "GRBM_GUI_ACTIVE"], ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"]):
+        for counters in groups:
             d = os.path.join(tmp, counters[0])
             cmd = [prof, "--pmc", *counters, "-f", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
-                   os.path.abspath(__file__), "--pmc-child", "--precision", args.precision,
-                   "--rays", str(args.rays), "--n-coarse", str(args.n_coarse), "--n-fine", str(args.n_fine)]
+                   os.path.abspath(__file__), "--pmc-child", *child_args]
             print(f"bench.py: rocprofv3 --pmc {' '.join(counters)} pass ...", file=sys.stderr, flush=True)
             rc, _, err = _run_killable(cmd, timeout, env)
             if rc != 0:
                 return None, f"rocprofv3 --pmc {counters[0]} pass failed ({rc}): {err.strip()[-300:]}"
-            rows = []
             for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 with open(path) as fh:
-                    rows += [r for r in csv.DictReader(fh) if "field_x3_kernel" in r["Kernel_Name"]
-                             or "field_fwd_kernel" in r["Kernel_Name"]]
-            for c in counters:
-                vals = {}
-                for r in rows:
-                    if r["Counter_Name"] == c:
-                        vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-                        if c == "GRBM_GUI_ACTIVE" and "End_Timestamp" in r:
-                            durs.append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
-                if not vals:
-                    return None, f"no {c} rows for the field kernel"
-                per[c] = (sum(vals.values()) / len(vals), len(vals))
+                    for r in csv.DictReader(fh):
+                        if not any(m in r["Kernel_Name"] for m in match):
+                            continue
+                        k = _short_kernel(r["Kernel_Name"])
+                        key = (counters[0], r["Dispatch_Id"])
+                        per = vals.setdefault(k, {}).setdefault(r["Counter_Name"], {})
+                        per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+                        if "End_Timestamp" in r:
+                            durs.setdefault(k, {})[key] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    fetch, n = per["FETCH_SIZE"]
-    write, _ = per["WRITE_SIZE"]
-    hit, miss = per["TCC_HIT_sum"][0], per["TCC_MISS_sum"][0]
-    # the shader clock the field kernel ran at: GRBM_GUI_ACTIVE (summed over the 8 XCDs) per dispatch time
-    clock = None
-    if durs and per.get("GRBM_GUI_ACTIVE"):
-        clock = per["GRBM_GUI_ACTIVE"][0] / 8.0 / (sum(durs) / len(durs))   # cycles per ns = GHz
-    return {"bytes_per_launch": int((2 * fetch + write) * 1024), "fetch_size_kb_raw": fetch, "write_size_kb": write,
-            "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None, "dispatches": n, "clock_ghz": clock}, "ok"
+    out = {}
+    for k, cs in vals.items():
+        e = {c: sum(v.values()) / len(v) for c, v in cs.items()}
+        e["dispatches"] = max(len(v) for v in cs.values())
+        dk = durs.get(k, {})
+        e["mean_ns"] = sum(dk.values()) / max(len(dk), 1)
+        # each counter's own dispatches' mean time (a clock is cycles of one pass over that pass's times)
+        e["mean_ns_of"] = {c: sum(dk.get(key, 0.0) for key in v) / len(v) for c, v in cs.items()}
+        out[k] = e
+    return out, "ok"
+
+
+def pmc_derived(e):
+    """Clock and MFMA-busy of one kernel's pass averages: GRBM_GUI_ACTIVE is summed over the 8 XCDs; MFMA busy =
+    SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over the 1024 SIMDs) / (1024 x GRBM_GUI_ACTIVE / 8)."""
+    d = {}
+    g = e.get("GRBM_GUI_ACTIVE")
+    if g:
+        ns = e.get("mean_ns_of", {}).get("GRBM_GUI_ACTIVE") or e.get("mean_ns")
+        if ns:
+            d["clock_ghz"] = g / 8.0 / ns
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in e:
+            d["mfma_busy"] = e["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * g / 8.0)
+    return d
+
+
+def pmc_traffic(args, timeout=240):
+    """The `roofline.traffic` and `roofline.mfma_busy` leg, measured in this run: two rocprofv3 --pmc passes
+    (FETCH_SIZE + GRBM_GUI_ACTIVE + SQ_VALU_MFMA_BUSY_CYCLES; WRITE_SIZE + TCC_HIT/MISS) over a child
+    `bench.py --pmc-child` (the same C3 workload: one warm-up + one timed step). Per field dispatch: L2->fabric
+    bytes = 2 x FETCH_SIZE (gfx950 counts half of 16-B-per-lane reads) + WRITE_SIZE, Infinity-Cache hits
+    included; the clock it ran at and its MFMA-busy fraction. Returns (dict or None, note)."""
+    child = ["--precision", args.precision, "--rays", str(args.rays), "--n-coarse", str(args.n_coarse),
+             "--n-fine", str(args.n_fine)]
+    groups = (["FETCH_SIZE", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"],
+              ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"])
+    per, note = pmc_passes(child, groups, ("field_x3_kernel", "field_fwd_kernel"), timeout)
+    if per is None:
+        return None, note
+    if len(per) != 1:
+        return None, f"expected one field kernel instantiation, found {sorted(per)}"
+    (kname, e), = per.items()
+    for c in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
+        if c not in e:
+            return None, f"no {c} rows for the field kernel"
+    hit, miss = e["TCC_HIT_sum"], e["TCC_MISS_sum"]
+    der = pmc_derived(e)
+    return {"kernel": kname, "bytes_per_launch": int((2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024),
+            "fetch_size_kb_raw": e["FETCH_SIZE"], "write_size_kb": e["WRITE_SIZE"],
+            "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None, "dispatches": e["dispatches"],
+            "clock_ghz": der.get("clock_ghz"), "mfma_busy": der.get("mfma_busy")}, "ok"
+
+
+TRAIN_PMC_KERNELS = ("field_x3_kernel", "field_bwd_x3_kernel", "weight_grad_kernel", "bn_layer_kernel",
+                     "lin_out_", "raymarch_")
+
+
+def pmc_train(args, timeout=300):
+    """--mode train --pmc-train: MFMA busy and clock per training kernel (the SAVE forward, the backward chain,
+    the weight gradients, the layer-by-layer GEMMs) in one rocprofv3 --pmc pass over a child train step
+    (SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE). Returns ({kernel: {...}} or None, note)."""
+    child = ["--mode", "train", "--train-modes", "hip", "--conf", args.conf, "--views", str(args.views),
+             "--renderer", args.renderer] + (["--bn"] if args.bn else []) + (["--spade"] if args.spade else [])
+    per, note = pmc_passes(child, (["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"],), TRAIN_PMC_KERNELS, timeout)
+    if per is None:
+        return None, note
+    res = {}
+    for k, e in sorted(per.items(), key=lambda kv: -kv[1]["mean_ns"] * kv[1]["dispatches"]):
+        der = pmc_derived(e)
+        res[k] = {"dispatches": e["dispatches"], "mean_us": round(e["mean_ns"] / 1e3, 2),
+                  "mfma_busy": None if der.get("mfma_busy") is None else round(der["mfma_busy"], 4),
+                  "clock_ghz": None if der.get("clock_ghz") is None else round(der["clock_ghz"], 3)}
+    return res, note
 
 
 def _comm_device(device):
@@ -916,6 +982,8 @@ def main():
     ap.add_argument("--config5-steps", type=int, default=2, help="N=1: timed steps of the config-4 / 5 legs")
     ap.add_argument("--fp32-steps", type=int, default=3, help="N=1: timed steps of the strict-fp32 leg")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-train", action="store_true",
+                    help="--mode train: one rocprofv3 --pmc pass (MFMA busy + clock per training kernel) first")
     ap.add_argument("--dist", action="store_true",
                     help="initialise the RCCL process group even at one rank (the N > 1 code path on one GPU)")
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=None,
@@ -946,6 +1014,7 @@ def main():
     args = ap.parse_args()
     if args.pmc_child:
         args.steps, args.warmup, args.no_cpu_baseline, args.no_pmc, args.no_legs = 1, 1, True, True, True
+        args.pmc_train, args.train_modes = False, "hip"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
@@ -966,6 +1035,9 @@ def main():
     pmc, pmc_note = None, "skipped"
     if (world == 1 and args.mode == "render" and config == 3 and not args.no_pmc):
         pmc, pmc_note = pmc_traffic(args)
+    train_pmc = None
+    if world == 1 and args.mode == "train" and args.pmc_train:
+        train_pmc = pmc_train(args)
 
     if use_dist:
         import torch.distributed as dist
@@ -988,7 +1060,7 @@ def main():
     from avr.renderers import VolumeRenderer
     avr.load_library()
     if args.mode == "train":
-        return run_train(args, device)
+        return run_train(args, device, train_pmc)
 
     # N > 1: ranks > 0 build a scene of the same architecture and receive rank 0's (broadcast_scene)
     net = build_scene(device, seed=0 if rank == 0 else 1000 + rank, sigma_bias=args.sigma_bias)
@@ -1073,9 +1145,11 @@ def main():
     hbm.on = False
     field_ms = timer.total_ms()
     field_launches = len(timer.events)
+    field_spread = None
     if use_dist:
-        t = torch.tensor([field_ms], device=_comm_device(device), dtype=torch.float64)
+        t = torch.tensor([field_ms, -field_ms], device=_comm_device(device), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        field_spread = {"min": round(-float(t[1]), 3), "max": round(float(t[0]), 3)}
         field_ms = float(t[0])
     assert bool(torch.isfinite(out).all())
     if args.pmc_child:
@@ -1159,6 +1233,11 @@ def main():
             "Infinity-Cache hits")
         line["roofline"]["traffic_over_algorithmic"] = round(pmc["bytes_per_launch"] / alg_bytes, 1)
         line["roofline"]["l2_hit_rate"] = None if pmc["l2_hit_rate"] is None else round(pmc["l2_hit_rate"], 4)
+        if pmc.get("mfma_busy") is not None:
+            line["roofline"]["mfma_busy"] = round(pmc["mfma_busy"], 4)
+            line["roofline"]["mfma_busy_source"] = (
+                f"the --pmc pass of this run over {pmc['kernel']}: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x "
+                "GRBM_GUI_ACTIVE / 8 XCDs), the fraction of the kernel's cycles the matrix cores were busy")
         if pmc.get("clock_ghz"):
             # the MFMA peak scales with the clock the board's power limit allows (2.4 GHz nominal)
             c = pmc["clock_ghz"]
@@ -1179,6 +1258,10 @@ def main():
         line["scene_checksum"] = scene_checksum(net)
     if config == 5 and use_dist:
         line["shard_phases"] = shard_phases(stimer, args.steps, device, R)
+    if field_spread is not None:
+        # every rank's field kernel time over the timed steps (HIP events around its field launches): a slow
+        # rank or an uneven tile split shows as max >> min
+        line["field_ms_per_rank"] = dict(field_spread, steps=args.steps, launches_per_rank=field_launches)
     if config == 4:
         line["config"]["fine_samples_evaluated_fraction"] = round(
             fine_evaluated[0] / (args.steps * R * (args.n_coarse + args.n_fine)), 4)

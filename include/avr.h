@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 14
+#define AVR_ABI_VERSION 15
 #define AVR_MAX_BLOCKS 8
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
@@ -436,8 +436,8 @@ int avr_bn_grad_rows(int64_t n_rows, int n_cols, const float* g, const float* pr
  * (a multiple of 64), every pointer 16-B aligned, weight (4, d_hidden) and bias (4) as nn.Linear holds them:
  * avr_lin_out_fwd_rows: out (n_rows, 4) = [sigmoid(raw[0:3]), relu(raw[3])], raw = relu(x) . weight^T + bias,
  *   x (n_rows, ld_x); x_max (or NULL): max relu(x) as float bits, max with what is there.
- * avr_lin_out_bwd_rows: d_raw (n_rows, 4) = grad_out * [y (1 - y) rgb, (y > 0) sigma] with y = out (torch's
- *   sigmoid / relu backward), g (n_rows, d_hidden) = d_raw . weight where pre > 0, else 0 (aten
+ * avr_lin_out_bwd_rows: d_raw (n_rows, 4) = [(grad_out (1 - y)) y rgb, sigma: grad_out where y > 0 else 0] with
+ *   y = out (aten's sigmoid_backward and ReluBackward's threshold_backward, bit for bit), g (n_rows, d_hidden) = d_raw . weight where pre > 0, else 0 (aten
  *   threshold_backward; pre (n_rows, ld_pre) = lin_out's input before its relu); d_raw_max (or NULL): max |d_raw|
  *   as float bits, max with what is there. */
 /* The spade product rule's backward (ABI 14; avr.layer_train, models.py:585-587: X' = S * X + T): over n values
@@ -489,12 +489,16 @@ int avr_raymarch(const avr_view_desc* view, const float* gate_table, const float
  * (renderers.py:413-432, :320-343). n_scenes (<= AVR_MAX_SCENES) scenes of n_per_scene rays each (ray r in
  * scene r / n_per_scene, its view and gate table; gate_tables (n_scenes, H*W, 64)). Forward: world (n, 3),
  * trace ((steps + 1), n, 3) = every point, state (steps, n, 96) = h, c, i, f, g, o per step (the backward's
- * input). Backward, given grad_world (n, 3): d_tables (n_scenes, H*W, 64), fp64, += d loss / d gate table
- * (zero it first; W_ih's gradient is then sum_s d_tables[s]^T latent_s^T, the latent's W_ih^T d_tables[s]),
+ * input). Backward, given grad_world (n, 3): d_tables (n_scenes, H*W, 64), fp32, = d loss / d gate table
+ * (written whole; W_ih's gradient is then sum_s d_tables[s]^T latent_s^T, the latent's W_ih^T d_tables[s]),
  * d_grads (64*16 + 64 + 16 + 1) = d W_hh, d (b_ih = b_hh), d w_out, d b_out, with the reference's clamp(-10, 10)
  * of every h gradient (state[0].register_hook) and grid_sample's border / align_corners=True position gradient.
- * ABI 13: deterministic -- the table gradient in fp64 atomics, the parameter gradients summed in a fixed order
- * through `scratch` (avr_raymarch_bwd_scratch_floats(n) floats, n = n_scenes * n_per_scene); lookup_grad 1 =
+ * ABI 15: bit-deterministic by construction, no floating-point atomics -- the table gradient summed as int64
+ * fixed-point values under one power-of-two scale per call (chosen from max |dg| so no sum can overflow; integer
+ * sums do not depend on the order), then rounded once to fp32 (an entry a NaN / inf gate gradient reached is
+ * NaN); the parameter gradients summed in a fixed order. `scratch` holds avr_raymarch_bwd_scratch_bytes(n, steps,
+ * n_scenes * H*W * 64) bytes (n = n_scenes * n_per_scene; the accumulators, the stored gate gradients and
+ * lookups, the workgroups' partials), scratch_bytes its size; lookup_grad 1 =
  * the lookup's position gradient flows into the points (models.py:753-823 with stop_encoder_grad False), 0 = it
  * does not (stop_encoder_grad True detaches the looked-up latent, models.py:810-811: W_ih, the LSTM and
  * out_layer still get theirs, the points only through x += rd * sd).                                          */
@@ -502,11 +506,11 @@ int avr_raymarch_train(const avr_view_desc* views, int n_scenes, const float* ga
                        const float* b_ih, const float* b_hh, const float* w_out, const float* b_out, const float* ro,
                        const float* rd, const float* init_dist, int64_t n_per_scene, int steps, float* world,
                        float* trace, float* state, void* stream);
-int avr_raymarch_bwd_scratch_floats(int64_t n_rays, int64_t* n_floats);
+int avr_raymarch_bwd_scratch_bytes(int64_t n_rays, int steps, int64_t table_entries, int64_t* n_bytes);
 int avr_raymarch_bwd(const avr_view_desc* views, int n_scenes, const float* gate_tables, const float* w_hh,
                      const float* w_out, const float* rd, const float* trace, const float* state,
-                     const float* grad_world, int64_t n_per_scene, int steps, int lookup_grad, double* d_tables,
-                     float* d_grads, float* scratch, void* stream);
+                     const float* grad_world, int64_t n_per_scene, int steps, int lookup_grad, float* d_tables,
+                     float* d_grads, void* scratch, int64_t scratch_bytes, void* stream);
 
 /* ------------------------------------------------------------ measurement
  * Streaming device copy dst[0, n_bytes) = src[0, n_bytes) (16-B aligned,

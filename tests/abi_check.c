@@ -236,16 +236,21 @@ int main(void) {
                             NULL), AVR_E_INVALID);
   expect("raymarch_train null", avr_raymarch_train(&v, 1, buf, NULL, buf, buf, buf, buf, buf, buf, buf, 4, 10, buf, buf,
                                                    buf, NULL), AVR_E_INVALID);
-  expect("raymarch_bwd null", avr_raymarch_bwd(&v, 1, buf, buf, buf, buf, buf, buf, NULL, 4, 10, 1, (double*)buf, buf,
-                                               buf, NULL), AVR_E_INVALID);
-  expect("raymarch_bwd no scratch", avr_raymarch_bwd(&v, 1, buf, buf, buf, buf, buf, buf, buf, 4, 10, 1, (double*)buf,
-                                                     buf, NULL, NULL), AVR_E_INVALID);
+  expect("raymarch_bwd null", avr_raymarch_bwd(&v, 1, buf, buf, buf, buf, buf, buf, NULL, 4, 10, 1, buf, buf,
+                                               buf, 1 << 20, NULL), AVR_E_INVALID);
+  expect("raymarch_bwd no scratch", avr_raymarch_bwd(&v, 1, buf, buf, buf, buf, buf, buf, buf, 4, 10, 1, buf,
+                                                     buf, NULL, 1 << 20, NULL), AVR_E_INVALID);
+  expect("raymarch_bwd scratch too small", avr_raymarch_bwd(&v, 1, buf, buf, buf, buf, buf, buf, buf, 4, 10, 1, buf,
+                                                            buf, buf, 64, NULL), AVR_E_INVALID);
   expect("raymarch_bwd no steps", avr_raymarch_bwd(&v, 1, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 4, 0, 1, NULL,
-                                                   NULL, NULL, NULL), AVR_OK);
+                                                   NULL, NULL, 0, NULL), AVR_OK);
   {
-    int64_t nf = 0;
-    expect("raymarch_bwd scratch size", avr_raymarch_bwd_scratch_floats(33, &nf), AVR_OK);
-    check("raymarch_bwd scratch = 3 workgroups", nf == 3 * (64 * 16 + 64 + 16 + 1));
+    /* ABI 15: int64 accumulators (8 B per table entry), dg rows (64 floats per ray step), lookups (8 floats per
+       ray step), 3 workgroups' partials, the control words; each region rounded up to 256 B */
+    int64_t nb = 0;
+    expect("raymarch_bwd scratch size", avr_raymarch_bwd_scratch_bytes(33, 10, 4096, &nb), AVR_OK);
+    check("raymarch_bwd scratch layout", nb == 32768 + 84480 + 10752 + 13312 + 256);
+    expect("raymarch_bwd scratch bad", avr_raymarch_bwd_scratch_bytes(-1, 10, 4096, &nb), AVR_E_INVALID);
   }
 
   /* measurement */

@@ -49,47 +49,80 @@ def _grads(net, xyz, vd, w, coarse, hip, latent_grad):
     return out.detach(), gr
 
 
-def _near_tie_points(net, xyz, vd, coarse, rel_max=1e-4, rel_relu=1e-5):
-    """Points where the gradient is discontinuous within fp32 noise, in float64: a relu input within `rel_relu` of
-    zero (of that layer's largest |value|; relu masks that fp32 rounding may flip, in any fp32 implementation) or,
-    with the max combine, a feature whose two largest views are within `rel_max` (the view a max's gradient goes
-    to). Seen on the MI355X: one fc_0 input of (64, 3, cl 2, SB 2, NS 2, spade) sits 4.8e-7 from zero, the x3 path
-    flips its mask where PyTorch fp32 did not, and block 0's input gradient moves by 2e-3 of its max."""
+def _capture_forward(layer_train, store):
+    """Wrap _FieldTrainLayers.forward so each call appends what the HIP forward decided: its stored fp32 rows
+    (Xpre[b]: block b's residual stream before lin_z / spade / combine, Xin[b]: block b's input, N[b]: fc_0's
+    output) and its output. The relu masks and the max-combine's winning views of the HIP run are read from these
+    exactly as its backward reads them (layer_train.py:205-242). Returns the original forward."""
+    orig = layer_train._FieldTrainLayers.forward
+
+    def forward(ctx, fused, coarse, *rest):
+        out = orig(ctx, fused, coarse, *rest)
+        Xpre, Xin, N = ctx.keep[:3]
+        store.append(([t.clone() for t in Xpre], [t.clone() for t in Xin], [t.clone() for t in N], out.clone()))
+        return out
+
+    layer_train._FieldTrainLayers.forward = staticmethod(forward)
+    return orig
+
+
+def _hip_masks(cap, mlp, SB, NS, B):
+    """The branch of the piecewise-linear MLP the HIP forward took: relu masks [rows > 0] of every fc_0 / fc_1 /
+    lin_out operand and of sigma (the backward's masks, layer_train.py:205-233), and with the max combine the view
+    torch.max(dim) picks on the HIP rows (the one its adjoint, layer_train.py:238-242, sends the gradient to)."""
+    Xpre, Xin, N, out = cap
+    nb = mlp.n_blocks
+    m = {"x": [x > 0 for x in Xin], "n": [n > 0 for n in N], "out": Xpre[nb] > 0,
+         "sigma": out.reshape(-1, 4)[:, 3:] > 0}
+    cl = mlp.combine_layer
+    if NS > 1 and cl < nb and mlp.combine_type == "max":
+        idx = Xpre[cl].reshape(SB, NS, B, -1).max(1).indices
+        m["win"] = torch.nn.functional.one_hot(idx, NS).permute(0, 3, 1, 2)       # (SB, NS, B, H)
+    return m
+
+
+def _masked_forward(net, mlp, prm, xyz, vd, lat, m):
+    """NewPixelNeRFNet.forward (models.py:739-863; ResnetFC models.py:541-592 with ResnetBlockFC models.py:454-470,
+    spade models.py:585-587, the views' combine utils.py:71-81) with every relu replaced by its input times the HIP
+    run's mask and the max combine by the HIP run's winning view: the same function as the reference's on the
+    branch the HIP forward took, so its float64 gradient needs no excluded points."""
+    F = torch.nn.functional
+    SB, B, _ = xyz.shape
+    NS = net.num_views_per_obj
+    feat, zft = net.mlp_inputs(xyz, vd, latent=lat)
+    dt = zft.dtype
+
+    def lin(v, n):
+        return F.linear(v, prm[n + ".weight"], prm[n + ".bias"])
+
+    x = lin(zft, "lin_in")
+    for b in range(mlp.n_blocks):
+        if b == mlp.combine_layer and NS > 1:
+            v = x.reshape(SB, NS, B, -1)
+            x = ((v * m["win"].to(dt)).sum(1) if "win" in m else v.mean(1)).reshape(SB * B, -1)
+        if b < mlp.combine_layer:
+            tz = lin(feat, f"lin_z.{b}")
+            x = lin(feat, f"scale_z.{b}") * x + tz if mlp.use_spade else x + tz
+        h = lin(x * m["x"][b].to(dt), f"blocks.{b}.fc_0")
+        x = x + lin(h * m["n"][b].to(dt), f"blocks.{b}.fc_1")
+    raw = lin(x * m["out"].to(dt), "lin_out")
+    return torch.cat([torch.sigmoid(raw[:, :3]), raw[:, 3:] * m["sigma"].to(dt)], -1).reshape(SB, B, 4)
+
+
+def _masked_grads(net, xyz, vd, w, coarse, m, latent_grad):
+    """Every parameter, point and (unless stop_encoder_grad) latent-map gradient of _masked_forward, in the
+    net's current dtype (fp32, or float64 inside _fp64)."""
     mlp = net.mlp_coarse if coarse else net.mlp_fine
-    NS, (SB, B, _) = net.num_views_per_obj, xyz.shape
-    near = torch.zeros(SB, B, dtype=torch.bool, device=xyz.device)
-
-    def mark(v):   # v: (SB * NS * B or SB * B, H) pre-activation rows
-        small = v.abs() < rel_relu * v.abs().max()
-        near.logical_or_(small.reshape(SB, -1, B, small.shape[-1]).any(1).any(-1))
-
-    with torch.no_grad():
-        net.double()
-        try:
-            feat, zft = net.mlp_inputs(xyz.double(), vd.double())
-            x = mlp.lin_in(zft)
-            for b in range(mlp.n_blocks):
-                if b == mlp.combine_layer and NS > 1:
-                    v = x.reshape(SB, NS, B, -1)
-                    if mlp.combine_type == "max":
-                        top2 = v.topk(2, dim=1).values
-                        gap = (top2[:, 0] - top2[:, 1]) / v.abs().amax(dim=(0, 1, 2)).clamp_min(1e-30)
-                        near |= (gap < rel_max).any(-1)
-                    x = v.mean(1).reshape(SB * B, -1) if mlp.combine_type == "average" else v.amax(1).reshape(SB * B, -1)
-                if b < mlp.combine_layer:
-                    tz = mlp.lin_z[b](feat)
-                    x = mlp.scale_z[b](feat) * x + tz if mlp.use_spade else x + tz
-                mark(x)
-                blk = mlp.blocks[b]
-                n = blk.fc_0(torch.relu(x))
-                mark(n)
-                x = x + blk.fc_1(torch.relu(n))
-            mark(x)
-            out = mlp.lin_out(torch.relu(x))
-            mark(out[:, 3:4])
-        finally:
-            net.float()
-    return near
+    prm = {n: p.detach().clone().requires_grad_(True) for n, p in mlp.named_parameters()}
+    lat = net.encoder.latent.detach().clone().requires_grad_(latent_grad)
+    x = xyz.clone().requires_grad_(True)
+    out = _masked_forward(net, mlp, prm, x, vd, lat, m)
+    (out * w).sum().backward()
+    gr = {n: p.grad.detach().clone() for n, p in prm.items() if p.grad is not None}
+    gr["xyz"] = x.grad.detach().clone()
+    if latent_grad:
+        gr["latent"] = lat.grad.detach().clone()
+    return out.detach(), gr
 
 
 CASES = [  # d_hidden, n_blocks, d_latent, combine_layer, SB, NS, spade, combine_type
@@ -104,55 +137,81 @@ CASES = [  # d_hidden, n_blocks, d_latent, combine_layer, SB, NS, spade, combine
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=lambda c: f"h{c[0]}-nb{c[1]}-cl{c[3]}-sb{c[4]}-ns{c[5]}"
-                                                     f"{'-spade' if c[6] else ''}-{c[7]}")
-def test_layer_train_grads_match_fp64(case):
+def _check_case(case, stop=False):
     from avr import layer_train
     d_hidden, n_blocks, d_latent, cl, SB, NS, spade, ctype = case
     hw = (16, 16) if d_hidden == 512 else (8, 8)
     net = _views_net(d_hidden, n_blocks, d_latent, hw, cl, SB, NS, spade, ctype)
+    net.stop_encoder_grad = stop
+    latent_grad = not stop        # a detached lookup (models.py:810-811) leaves the map without a gradient
     g = torch.Generator().manual_seed(17)
     B = 333
     xyz = ((torch.rand(SB, B, 3, generator=g) - 0.5) * 0.8).to(DEV)
     vd = torch.nn.functional.normalize(torch.randn(SB, B, 3, generator=g), dim=-1).to(DEV)
     w = torch.randn(SB, B, 4, generator=g).to(DEV)
     assert net.can_train_layers(xyz, vd) and not net.can_train_fused(xyz, vd)
-    calls = []
+    calls, caps = [], []
     orig = layer_train._FieldTrainLayers.apply
+    orig_fwd = _capture_forward(layer_train, caps)
     layer_train._FieldTrainLayers.apply = lambda *a: calls.append(1) or orig(*a)
     try:
         for coarse in (True, False):
-            # points at a discontinuity of the gradient within fp32 noise (relu inputs next to zero, max ties:
-            # any two fp32 implementations may take different sides) carry no loss, so the comparison measures the
-            # arithmetic, not which side of a tie the rounding fell on
-            tie = _near_tie_points(net, xyz, vd, coarse)
-            wc = w * (~tie).unsqueeze(-1).float()
-            print(f"{case} coarse={coarse}: {int(tie.sum())} of {tie.numel()} points next to a relu / max tie")
-            out_h, g_h = _grads(net, xyz, vd, wc, coarse, hip=True, latent_grad=True)
+            mlp = net.mlp_coarse if coarse else net.mlp_fine
+            caps.clear()
+            out_h, g_h = _grads(net, xyz, vd, w, coarse, hip=True, latent_grad=latent_grad)
             n_hip = len(calls)
-            out_t, g_t = _grads(net, xyz, vd, wc, coarse, hip=False, latent_grad=True)
-            assert n_hip >= 1 and len(calls) == n_hip, "the HIP run must take the layer path, torch's must not"
+            out_t, g_t = _grads(net, xyz, vd, w, coarse, hip=False, latent_grad=latent_grad)
+            assert n_hip >= 1 and len(calls) == n_hip and len(caps) == 1, \
+                "the HIP run must take the layer path (once), torch's must not"
             np.testing.assert_allclose(out_h.cpu().numpy(), out_t.cpu().numpy(), atol=2e-4)
             if spade:
                 assert any(k.startswith("scale_z.") for k in g_h)
-            _, g_d = _fp64(net, lambda: _grads(net, xyz.double(), vd.double(), wc.double(), coarse, hip=False,
-                                               latent_grad=True))
-            for k in g_d:   # every key's errors first (the assertion below names only the first failing one)
-                ref = g_d[k].double()
+            # the reference gradient on the branch the HIP forward took: every point carries its loss
+            m = _hip_masks(caps[0], mlp, SB, NS, B)
+            out_m, g_tm = _masked_grads(net, xyz, vd, w, coarse, m, latent_grad)
+            np.testing.assert_allclose(out_m.cpu().numpy(), out_h.cpu().numpy(), atol=2e-4)
+            _, g_dm = _fp64(net, lambda: _masked_grads(net, xyz.double(), vd.double(), w.double(), coarse,
+                                                       m, latent_grad))
+            # the unconditioned float64 reference, printed for the record (the relu / max flips of either fp32 run)
+            _, g_d = _fp64(net, lambda: _grads(net, xyz.double(), vd.double(), w.double(), coarse, hip=False,
+                                               latent_grad=latent_grad))
+            assert set(g_h) == set(g_tm) == set(g_dm) == set(g_d), sorted(set(g_h) ^ set(g_dm))
+            for k in g_dm:   # every key's errors first (the assertion below names only the first failing one)
+                ref, ref_u = g_dm[k].double(), g_d[k].double()
                 sc = float(ref.abs().max()) or 1.0
                 print(f"   {k}: HIP {float((g_h[k].double() - ref).abs().max()) / sc:.2e} "
-                      f"torch32 {float((g_t[k].double() - ref).abs().max()) / sc:.2e}")
-            worst = _compare64(g_h, g_t, g_d)
-            print(f"{case} coarse={coarse}: worst HIP gradient error vs float64 {worst:.2e} of max |grad|")
+                      f"torch32 {float((g_tm[k].double() - ref).abs().max()) / sc:.2e} under the HIP masks; "
+                      f"unconditioned: HIP {float((g_h[k].double() - ref_u).abs().max()) / sc:.2e} "
+                      f"torch32 {float((g_t[k].double() - ref_u).abs().max()) / sc:.2e}")
+            worst = _compare64(g_h, g_tm, g_dm)
+            print(f"{case} stop={stop} coarse={coarse}: 0 points excluded; worst HIP gradient error vs float64 "
+                  f"under the HIP masks {worst:.2e} of max |grad|")
     finally:
         layer_train._FieldTrainLayers.apply = orig
+        layer_train._FieldTrainLayers.forward = staticmethod(orig_fwd)
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"h{c[0]}-nb{c[1]}-cl{c[3]}-sb{c[4]}-ns{c[5]}"
+                                                     f"{'-spade' if c[6] else ''}-{c[7]}")
+def test_layer_train_grads_match_fp64(case):
+    """Every parameter, point and latent-map gradient of every point (none excluded) within twice fp32's own
+    error of the float64 gradient on the HIP forward's branch."""
+    _check_case(case)
+
+
+@pytest.mark.parametrize("case", [(64, 3, 64, 2, 2, 2, True, "average"), (128, 4, 128, 2, 1, 3, False, "max")],
+                         ids=["spade-ns2", "ns3-max"])
+def test_layer_train_stop_encoder_grad_point_gradient(case):
+    """stop_encoder_grad with points that need a gradient (the detached lookup has no grad_fn): the
+    points get z_feature's gradient alone, as torch's autograd of the module gives."""
+    _check_case(case, stop=True)
 
 
 @pytest.mark.parametrize("H,n,pad", [(64, 1, 0), (192, 5, 4), (512, 1003, 0), (512, 40000, 8)])
 def test_lin_out_rows_vs_fp64(H, n, pad):
     """avr_lin_out_fwd_rows / avr_lin_out_bwd_rows (the layer-by-layer paths' output layer) against float64 torch:
-    out and g within 1e-5 of their scale, d_raw bit-equal to torch's fp32 activation backward (same two
-    roundings), g exactly 0 where pre <= 0, both maxima exact; rows with a leading dimension past d_hidden."""
+    out and g within 1e-5 of their scale, d_raw bit-equal to torch's own activation backward kernels
+    (aten sigmoid_backward / threshold_backward), g exactly 0 where pre <= 0, both maxima exact; rows with a leading dimension past d_hidden."""
     from avr import ops
     g = torch.Generator().manual_seed(H + n)
     xw = torch.randn(n, H + pad, generator=g).to(DEV)
@@ -166,7 +225,9 @@ def test_lin_out_rows_vs_fp64(H, n, pad):
     assert int(xmax) == int(torch.relu(x).max().reshape(1).view(torch.int32))
     go = torch.randn(n, 4, generator=g).to(DEV)
     d4, gr, dmax = ops.lin_out_rows_bwd(go, out, W, x)
-    d4_ref = torch.cat([go[:, :3] * ((1.0 - out[:, :3]) * out[:, :3]), go[:, 3:] * (out[:, 3:] > 0)], -1)
+    # torch's own activation backward kernels (SigmoidBackward0 / ReluBackward0), bit for bit
+    d4_ref = torch.cat([torch.ops.aten.sigmoid_backward(go[:, :3], out[:, :3]),
+                        torch.ops.aten.threshold_backward(go[:, 3:], out[:, 3:], 0.0)], -1)
     assert torch.equal(d4, d4_ref)
     assert int(dmax) == int(d4_ref.abs().max().reshape(1).view(torch.int32))
     g_ref = (d4.double() @ W.double()) * (x > 0)

@@ -199,3 +199,31 @@ def test_adaptive_renderer_training_step_hip_vs_torch():
         worst = max(worst, err / s)
         assert err <= 3.0 * noise_k + 2e-2 * s + 1e-7, f"{k}: {err:.3e} (torch's own spread {noise_k:.3e}) of {s:.3e}"
     print(f"adaptive step: worst HIP gradient difference {worst:.2e} of max |grad|")
+
+
+def test_march_table_gradient_order_independent():
+    """ABI 15: the gate-table gradient is summed as int64 fixed-point values (no floating-point atomics), so it
+    does not depend on the order its contributions arrive in. Permuting the rays inside each scene changes the
+    workgroups every contribution comes from and the order of the atomic adds: the latent's and W_ih's gradients
+    (both computed from the table gradient alone) must come out bit for bit the same, the world points permuted
+    with the rays; and a second identical backward gives every gradient bit for bit."""
+    sb, R = 2, 300
+    net = _net(64, 2, 64, (8, 8), sb=sb)
+    rend = _renderer(64, 10)
+    ros, rds, init, *_ = _march_inputs(sb, R, seed=21)
+    w = 300.0 * torch.randn(sb, R, 3, generator=torch.Generator().manual_seed(22)).to(DEV)
+    wa, ga, path = _march_grads(rend, net, ros, rds, init, w, hip=True)
+    assert path == "hip_train"
+    wb, gb, _ = _march_grads(rend, net, ros, rds, init, w, hip=True)
+    assert torch.equal(wa, wb)
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), f"{k} differs between two identical backward passes"
+    perm = torch.randperm(R, generator=torch.Generator().manual_seed(23)).to(DEV)
+    wp, gp, _ = _march_grads(rend, net, ros[:, perm], rds[:, perm], init[:, perm], w[:, perm], hip=True)
+    assert torch.equal(wp, wa[:, perm])
+    for k in ("latent", "lstm.weight_ih"):
+        assert torch.equal(gp[k], ga[k]), (k, float((gp[k] - ga[k]).abs().max()))
+    assert float(ga["latent"].abs().max()) > 0 and float(ga["lstm.weight_ih"].abs().max()) > 0
+    for k in gp:   # the parameter sums follow the ray order (fixed-order float sums): equal to rounding only
+        s = float(ga[k].abs().max()) or 1.0
+        assert float((gp[k] - ga[k]).abs().max()) <= 1e-5 * s, k

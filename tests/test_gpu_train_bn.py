@@ -193,3 +193,31 @@ def test_bn_training_renderer_step():
     for k in gt_:   # fc_0's bias has an exactly zero gradient under batch statistics (see _compare64)
         s = max(float(gt_[k].abs().max()), 1e-4 * glob)
         assert float((gh[k] - gt_[k]).abs().max()) <= 2e-3 * s, k
+
+
+def test_bn_training_stop_encoder_grad_point_gradient():
+    """stop_encoder_grad with points that need a gradient (the detached lookup, models.py:810-811, has
+    no grad_fn, so the backward must not ask autograd for it): the points get z_feature's gradient alone, and every
+    parameter and point gradient is within twice PyTorch fp32's own error against float64."""
+    net = _bn_net(128, 3, combine_layer=2, hw=(8, 8))
+    net.stop_encoder_grad = True
+    xyz, vd, w = _points(1, 512, seed=21)
+    start = _running(net)
+
+    def grads(x0, v0, w0, hip):
+        _set_running(net, start)
+        net.hip_backward = hip
+        net.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        out = net(x, coarse=True, viewdirs=v0)
+        (out * w0).sum().backward()
+        gr = {n: p.grad.detach().clone() for n, p in net.mlp_coarse.named_parameters() if p.grad is not None}
+        gr["xyz"] = x.grad.detach().clone()
+        return gr
+
+    assert net.can_train_bn(xyz, vd)
+    g_h = grads(xyz, vd, w, True)
+    g_t = grads(xyz, vd, w, False)
+    g_d = _fp64(net, lambda: grads(xyz.double(), vd.double(), w.double(), False))
+    assert float(g_h["xyz"].abs().max()) > 0
+    _compare64(g_h, g_t, g_d, floor=1e-4)

@@ -137,7 +137,8 @@ def _install(monkeypatch, net):
 
     def lin_out_rows_bwd(grad_out, out, weight, pre, g=None):
         """avr_lin_out_bwd_rows' contract."""
-        d4 = torch.cat([grad_out[:, :3] * ((1.0 - out[:, :3]) * out[:, :3]), grad_out[:, 3:] * (out[:, 3:] > 0)], -1)
+        d4 = torch.cat([torch.ops.aten.sigmoid_backward(grad_out[:, :3], out[:, :3]),
+                        torch.ops.aten.threshold_backward(grad_out[:, 3:], out[:, 3:], 0.0)], -1)
         gr = torch.ops.aten.threshold_backward(d4 @ weight, pre, 0.0)
         if g is not None:
             g.copy_(gr)
