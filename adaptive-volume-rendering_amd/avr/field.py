@@ -8,7 +8,9 @@ parameter or the latent changes (tensor version counters), so an inference
 loop over many frames of one scene pays for them once, as the reference pays
 for encode() once.
 """
+import collections
 import ctypes
+import weakref
 
 import torch
 
@@ -125,14 +127,27 @@ class _precision:
         return False
 
 
-# Submodule (re)registrations anywhere in the process: FusedField._state's cached slots are rebuilt after one, so a
-# module replaced in an MLP (mlp.lin_in = nn.Linear(...)) is seen; parameters and buffers replaced in place are read
-# through their owners' dicts anyway.
+# Submodule (re)registrations anywhere in the process, numbered, with the id of the module that registered: a
+# FusedField._state slot is rebuilt after a registration under its MLP, so a module replaced in an MLP
+# (mlp.lin_in = nn.Linear(...)) is seen, and only then (modules built elsewhere, e.g. per training step, leave it
+# alone); parameters and buffers replaced in place are read through their owners' dicts anyway.
 _MODULE_GEN = [0]
+_REG_LOG = collections.deque(maxlen=4096)   # (generation, id(parent module))
 
 
 def _module_registered(module, name, submodule):
     _MODULE_GEN[0] += 1
+    _REG_LOG.append((_MODULE_GEN[0], id(module)))
+
+
+def _slot_current(gen, module_ids):
+    """No registration since generation `gen` under a module of module_ids (the log must still cover them all;
+    a reused id only costs a rebuild)."""
+    if gen == _MODULE_GEN[0]:
+        return True
+    if not _REG_LOG or _REG_LOG[0][0] > gen + 1:
+        return False
+    return not any(pid in module_ids for g, pid in _REG_LOG if g > gen)
 
 
 torch.nn.modules.module.register_module_module_registration_hook(_module_registered)
@@ -142,12 +157,40 @@ def _version_key(tensors):
     return tuple((t.data_ptr(), t._version) for t in tensors)
 
 
+def _stamp(t):
+    """(stream, event) marking the current stream's work that filled the cached device tensor t (None on the CPU
+    or while a HIP graph is being captured: one stream then, nothing to join)."""
+    if t is None or not t.is_cuda or torch.cuda.is_current_stream_capturing():
+        return None
+    s = torch.cuda.current_stream(t.device)
+    ev = torch.cuda.Event()
+    ev.record(s)
+    return s, ev
+
+
+def _join(stamp, *tensors):
+    """A cached value read from another stream than the one that made it (the adaptive renderer's side stream,
+    avr.renderers): that stream waits for the maker's work, and the tensors' memory is kept from reuse under the
+    maker's later allocations until this stream's work on them is done."""
+    if stamp is None:
+        return
+    s = torch.cuda.current_stream(stamp[0].device)
+    if s == stamp[0]:
+        return
+    s.wait_event(stamp[1])
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            t.record_stream(s)
+
+
 class _Packed:
     def __init__(self, dims, packed, table_keys):
         self.dims = dims
         self.packed = packed
         self.tables = {}
         self.bwd = None
+        self.bwd_stamp = None
+        self.stamp = None
 
 
 PRECISIONS = {"fp32": _lib.FIELD_FP32, "x3": _lib.FIELD_X3}
@@ -170,7 +213,8 @@ class FusedField:
         self._packed = {}     # coarse(bool) -> (key, _Packed)
         self._view_cache = {}
         self._latent_cache = {}   # per latent version: channels-last copies, max |latent| (both MLPs share them)
-        self._slots = {}          # id(mlp) -> (mlp, [(name, owner dict, key)] params, [...] float buffers)
+        # mlp (weakly) -> ([(name, owner dict, key)] params, [...] float buffers, generation, ids of its modules)
+        self._slots = weakref.WeakKeyDictionary()
 
     def invalidate(self):
         """Drop every cached blob, table and view descriptor (avr.parallel.broadcast_scene calls it after
@@ -198,9 +242,11 @@ class FusedField:
         key = (latent.data_ptr(), latent._version, tuple(latent.shape))
         hit = self._latent_cache.get(what)
         if hit is not None and hit[0] == key:
+            _join(hit[3], hit[1])
             return hit[1]
         val = make()
-        self._latent_cache[what] = (key, val, latent)   # holding `latent` keeps its address from being reused
+        # holding `latent` keeps its address from being reused
+        self._latent_cache[what] = (key, val, latent, _stamp(val))
         return val
 
     def latent_hwc(self, latent, s):
@@ -226,17 +272,21 @@ class FusedField:
         read through each owning module's dict: the module tree is walked once per mlp and again after any
         submodule registration (a walk per call was a large part of the adaptive step's host time), and a
         parameter or buffer replaced later is still seen."""
-        hit = self._slots.get(id(mlp))
-        if hit is None or hit[0] is not mlp or hit[3] != _MODULE_GEN[0]:
+        hit = self._slots.get(mlp)
+        if hit is not None and hit[2] != _MODULE_GEN[0]:
+            hit = (hit[0], hit[1], _MODULE_GEN[0], hit[3]) if _slot_current(hit[2], hit[3]) else None
+            if hit is not None:
+                self._slots[mlp] = hit
+        if hit is None:
             mods = list(mlp.named_modules())
             ps = [(f"{mn}.{n}" if mn else n, m._parameters, n) for mn, m in mods
                   for n, t in m._parameters.items() if t is not None]
             bs = [(f"{mn}.{n}" if mn else n, m._buffers, n) for mn, m in mods
                   for n, t in m._buffers.items() if t is not None and t.is_floating_point()]
-            hit = (mlp, ps, bs, _MODULE_GEN[0])
-            self._slots[id(mlp)] = hit
-        named = {full: d[k] for full, d, k in hit[1]}
-        return named, list(named.values()), [d[k] for _, d, k in hit[2]]
+            hit = (ps, bs, _MODULE_GEN[0], frozenset(id(m) for _, m in mods))
+            self._slots[mlp] = hit
+        named = {full: d[k] for full, d, k in hit[0]}
+        return named, list(named.values()), [d[k] for _, d, k in hit[1]]
 
     def _mlp(self, coarse):
         net = self.net
@@ -261,6 +311,7 @@ class FusedField:
         key = (id(mlp), self.precision if bn_fold else "x3", _version_key(params))
         hit = self._packed.get(slot)
         if hit is not None and hit[0] == key:
+            _join(hit[1].stamp, hit[1].packed)
             return hit[1]
         dims = self.dims(mlp)
         if not bn_fold:
@@ -302,6 +353,7 @@ class FusedField:
         entry = _Packed(dims, packed, None)
         entry._keep = keep
         entry.weights = w
+        entry.stamp = _stamp(packed)
         self._packed[slot] = (key, entry)
         return entry
 
@@ -316,7 +368,9 @@ class FusedField:
                        "avr_field_bwd_packed_floats")
             bwd = torch.empty(n.value, device=entry.packed.device, dtype=F32)
             call("avr_field_pack_bwd", ctypes.byref(dims), ctypes.byref(entry.weights), ptr(bwd), stream_of(bwd))
-            entry.bwd = bwd
+            entry.bwd, entry.bwd_stamp = bwd, _stamp(bwd)
+        else:
+            _join(entry.bwd_stamp, entry.bwd)
         return entry.bwd
 
     def table(self, coarse, sb=0):
@@ -325,6 +379,7 @@ class FusedField:
         key = (sb, lat.data_ptr(), lat._version, tuple(lat.shape))
         hit = entry.tables.get(sb)
         if hit is not None and hit[0] == key:
+            _join(hit[3], hit[1])
             return hit[1]
         dims = entry.dims
         L, H, W = lat.shape[1:]
@@ -334,7 +389,7 @@ class FusedField:
         with _precision(dims, _lib.FIELD_FP32):   # inference: exact fp32 tables, computed once per latent map
             call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W, ptr(table),
                  stream_of(table))
-        entry.tables[sb] = (key, table, lat)  # holding `lat` keeps its address from being reused
+        entry.tables[sb] = (key, table, lat, _stamp(table))  # holding `lat` keeps its address from being reused
         return table
 
     def tables_batch(self, coarse, n_scenes, fast=False, bn_fold=True):
@@ -349,6 +404,7 @@ class FusedField:
         cache = entry.__dict__.setdefault("batch_tables", {})
         hit = cache.get(bool(fast))
         if hit is not None and hit[0] == key:
+            _join(hit[3], hit[1])
             return hit[1]
         dims = entry.dims
         L, H, W = lat.shape[1:]
@@ -363,7 +419,7 @@ class FusedField:
                     latent = lat[min(sb, lat.shape[0] - 1)].detach().to(F32).contiguous()
                     call("avr_field_latent_table", ctypes.byref(dims), ptr(entry.packed), ptr(latent), H, W,
                          ptr(out[sb]), stream_of(out))
-        cache[bool(fast)] = (key, out, lat)
+        cache[bool(fast)] = (key, out, lat, _stamp(out))
         return out
 
     def view(self, sb=0, ns=1):

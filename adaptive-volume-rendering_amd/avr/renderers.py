@@ -283,6 +283,20 @@ class _LSTMMarch(nn.Module):
             return d.to(device)
         return d.pin_memory().to(device, non_blocking=True)
 
+    def _side_stream(self, phi, world):
+        """A second stream of world's device for the marched point's field pass (AdaptiveVolumeRenderer training on
+        the HIP path; None otherwise: CPU, inference, the module path, or AVR_ADAPTIVE_SIDE_STREAM=0)."""
+        import os
+        if not (world.is_cuda and torch.is_grad_enabled() and getattr(phi, "use_fused", False)
+                and getattr(phi, "hip_backward", False)) or os.environ.get("AVR_ADAPTIVE_SIDE_STREAM") == "0":
+            return None
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        key = world.device
+        if getattr(self, "_side", None) is None or self._side[0] != key:
+            self._side = (key, torch.cuda.Stream(device=key))
+        return self._side[1]
+
     def _gate_table(self, phi):
         lat = phi.encoder.latent
         w = self.lstm.weight_ih
@@ -464,11 +478,24 @@ class AdaptiveVolumeRenderer(_LSTMMarch):
         ros, rds, c2w_info = ops.world_rays(xy_pix, intrinsics, cam2world)
         init = self._initial_distance(SB, num_rays, dev, noise)
         world = self.march(ros, rds, init, phi)
-        # coarse image at the marched point
-        output_coarse = phi(world.reshape(SB, -1, 3), viewdirs=rds.reshape(SB, -1, 3), coarse=True,
-                            return_features=False)
-        rgb_coarse = output_coarse[..., :3].reshape(SB, num_rays, 3)
-        depth_coarse = ops.depth_of_points(world, c2w_info).reshape(SB, num_rays, -1)
+        # coarse image at the marched point. In training on the HIP path it runs on a side stream, beside the band
+        # pass: its field launches cover 64 samples per workgroup, so SB x R points fill a tenth of the chip, and
+        # autograd runs each backward on its forward's stream, so the two passes overlap in the backward too. The
+        # kernels and their results are the same; only their order on the device changes.
+        side = self._side_stream(phi, world)
+        if side is not None:
+            main = torch.cuda.current_stream(dev)
+            side.wait_stream(main)
+            for t in (world, rds) + tuple(x for x in c2w_info if torch.is_tensor(x)):
+                t.record_stream(side)
+            with torch.cuda.stream(side):
+                output_coarse = phi(world.reshape(SB, -1, 3), viewdirs=rds.reshape(SB, -1, 3), coarse=True,
+                                    return_features=False)
+                depth_coarse = ops.depth_of_points(world, c2w_info).reshape(SB, num_rays, -1)
+        else:
+            output_coarse = phi(world.reshape(SB, -1, 3), viewdirs=rds.reshape(SB, -1, 3), coarse=True,
+                                return_features=False)
+            depth_coarse = ops.depth_of_points(world, c2w_info).reshape(SB, num_rays, -1)
         # band around the marched distance (renderers.py:490-496); the sort is a no-op on stratified z
         final_distance = (world[..., 0] - ros[..., 0]) / rds[..., 0]
         u = None if noise is None else noise.get("band")
@@ -488,6 +515,11 @@ class AdaptiveVolumeRenderer(_LSTMMarch):
         rgb, distance_map, _ = volume_integral(z_vals_sorted, field[..., 3:], field[..., :3],
                                                white_back=self.white_back)
         depth_map = ops.depth_from_world(ros, rds, distance_map.reshape(SB, num_rays), c2w_info)
+        if side is not None:   # join: the coarse outputs are read on the caller's stream from here on
+            main.wait_stream(side)
+            for t in (output_coarse, depth_coarse):
+                t.record_stream(main)
+        rgb_coarse = output_coarse[..., :3].reshape(SB, num_rays, 3)
         return rgb_coarse, rgb, depth_coarse, depth_map
 
     @classmethod

@@ -232,13 +232,25 @@ def test_fused_field_parameter_slots_follow_replacements():
     assert list(named) == list(ref) and all(named[k] is ref[k] for k in ref)
     assert [id(t) for t in ps] == [id(t) for t in mlp.parameters()]
     assert [id(b) for b in bs] == [id(b) for b in mlp.buffers() if b.is_floating_point()]
-    slots = fused._slots[id(mlp)]
+    slots = fused._slots[mlp]
     fused._state(mlp)
-    assert fused._slots[id(mlp)] is slots                      # cached
+    assert fused._slots[mlp] is slots                          # cached
+    # modules built elsewhere (with submodules) register children, but not under this MLP: no rebuild
+    nn.Sequential(nn.Linear(3, 3), nn.ReLU())
+    fused._state(mlp)
+    assert fused._slots[mlp][0] is slots[0] and fld._MODULE_GEN[0] == fused._slots[mlp][2]
     mlp.lin_out.weight = nn.Parameter(torch.zeros_like(mlp.lin_out.weight))
     assert fused._state(mlp)[0]["lin_out.weight"] is mlp.lin_out.weight
     old = mlp.lin_in
     mlp.lin_in = nn.Linear(old.in_features, old.out_features)
     named = fused._state(mlp)[0]
     assert named["lin_in.weight"] is mlp.lin_in.weight and named["lin_in.weight"] is not old.weight
-    assert fld._MODULE_GEN[0] == fused._slots[id(mlp)][3]
+    assert fused._slots[mlp][0] is not slots[0] and fld._MODULE_GEN[0] == fused._slots[mlp][2]
+    # the slots hold the MLP weakly: a dropped module's entry goes with it
+    import gc
+    tmp = nn.Sequential(nn.Linear(2, 2))
+    fused._state(tmp)
+    n = len(fused._slots)
+    del tmp
+    gc.collect()
+    assert len(fused._slots) == n - 1
