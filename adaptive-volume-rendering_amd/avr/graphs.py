@@ -26,7 +26,7 @@ import torch
 
 from . import anomaly
 
-__all__ = ["GraphedRenderer"]
+__all__ = ["GraphedRenderer", "GraphedTrainStep"]
 
 
 class GraphedRenderer:
@@ -114,4 +114,102 @@ class GraphedRenderer:
         self.graph.replay()
         if anomaly.is_enabled():   # the captured launches were not checked at capture time (avr/anomaly.py)
             anomaly.check_outputs("GraphedRenderer replay", self.out)
+        return self.out
+
+
+class GraphedTrainStep:
+    """One training step -- the renderer and net forward, the loss, loss.backward() and optimizer.step()
+    (train.py:108-114) -- captured into one HIP graph for fixed shapes and replayed, for training loops whose step
+    is bound by launch overhead (the AdaptiveVolumeRenderer step: ~190 launches of a few to a few hundred
+    microseconds each).
+
+    step_fn() runs one step on tensors the caller keeps at fixed addresses (refill them in place between calls)
+    and returns what the caller reads after the step (e.g. the loss); it may call optimizer.zero_grad() (the
+    default set_to_none: a host-only no-op once captured: the captured backward writes the gradients). The
+    optimizer must be capturable (torch.optim.Adam(..., capturable=True)).
+
+    Calls 1 .. warmup run step_fn eagerly (real steps, on a side stream, so the graph's memory pool starts clean);
+    the next call captures it (the capture records launches without running them) and replays it once; later
+    calls replay. Every call is one training step.
+
+    Host-side inputs: each marcher in `renderers` (Raymarcher / AdaptiveVolumeRenderer) draws its start distances
+    on the CPU generator in an eager step (renderers.py:322 / :402); before every replay stage_host_draws() makes
+    the same draw and copies it into the buffer the captured march reads, so the random stream matches eager steps.
+    The band's torch.rand draws advance on device per replay as eager calls would (PyTorch's graph-safe generator).
+
+    State: the captured kernels take the source-view descriptors (poses, focal, principal point, latent map
+    shape) as launch arguments, and read the latent map through its address: like GraphedRenderer, every call
+    checks the nets' view tensors (a new latent or pose tensor, or an in-place update of one) and the field
+    precision, and captures again when one changed; refill the latent in place for a new scene of one shape and
+    the capture stays valid only if the poses did not change. Parameters are updated by the captured optimizer
+    step itself. The nets' FusedField caches are dropped before a capture, so every blob and lin_z table the
+    step reads is rebuilt inside the graph from the current parameters.
+    """
+
+    @staticmethod
+    def _detach(out):
+        """The caller's view of a step's outputs, without the autograd graph (kept alive it would hold the
+        parameters' AccumulateGrad nodes, and their streams, into the next step)."""
+        if isinstance(out, torch.Tensor):
+            return out.detach()
+        if isinstance(out, (list, tuple)):
+            return type(out)(GraphedTrainStep._detach(o) for o in out)
+        if isinstance(out, dict):
+            return {k: GraphedTrainStep._detach(v) for k, v in out.items()}
+        return out
+
+    def __init__(self, step_fn, nets=(), renderers=(), warmup=3):
+        self.step_fn = step_fn
+        self.nets = [n for n in nets if n is not None]
+        self.renderers = [r for r in renderers if r is not None]
+        self.warmup = warmup
+        self.calls = 0
+        self.captures = 0
+        self.graph = None
+        self.out = None
+
+    def _views(self):
+        out = []
+        for net in self.nets:
+            enc = getattr(net, "encoder", None)
+            out += [getattr(enc, "latent", None), getattr(enc, "latent_scaling", None)]
+            out += [getattr(net, a, None) for a in ("poses", "focal", "c", "image_shape")]
+        return [t for t in out if isinstance(t, torch.Tensor)]
+
+    def _stale(self):
+        views = self._views()
+        return (len(views) != len(self._held) or any(a is not b or a._version != v
+                                                       for a, (b, v) in zip(views, self._held))
+                or [getattr(n, "field_precision", None) for n in self.nets] != self._held_precision)
+
+    def _capture(self):
+        self.graph = self.out = None
+        for net in self.nets:
+            fused = getattr(net, "_fused", None)
+            if fused is not None:
+                fused.invalidate()   # every blob / table the step reads is made inside the graph
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self.step_fn()
+        self.graph, self.out = graph, self._detach(out)
+        self._held = [(t, t._version) for t in self._views()]
+        self._held_precision = [getattr(n, "field_precision", None) for n in self.nets]
+        self.captures += 1
+
+    def __call__(self):
+        self.calls += 1
+        if self.calls <= self.warmup:
+            stream = torch.cuda.Stream()
+            stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(stream):
+                out = self._detach(self.step_fn())
+            torch.cuda.current_stream().wait_stream(stream)
+            return out
+        if self.graph is None or self._stale():
+            self._capture()
+        for r in self.renderers:
+            r.stage_host_draws()
+        self.graph.replay()
+        if anomaly.is_enabled():
+            anomaly.check_outputs("GraphedTrainStep replay", self.out)
         return self.out

@@ -272,16 +272,45 @@ class _LSTMMarch(nn.Module):
         self.counter = 0
         self._gate_cache = None
         self.last_path = None
+        self._graph_init = None   # start distances read by a captured training step (stage_host_draws)
 
     def _initial_distance(self, SB, num_rays, device, noise):
         if noise is not None and "initial_distance" in noise:
             return noise["initial_distance"].reshape(SB, num_rays, 1).to(device)
+        if torch.device(device).type == "cuda" and torch.cuda.is_current_stream_capturing():
+            # inside a HIP-graph capture (avr.graphs.GraphedTrainStep): a static device buffer that
+            # stage_host_draws() refills before every replay with the same CPU draw an eager step makes
+            buf = self._graph_init
+            if buf is None or buf.shape != (SB, num_rays, 1) or buf.device != torch.device(device):
+                buf = self._graph_init = torch.empty((SB, num_rays, 1), device=device)
+            return buf
         # renderers.py:322 / :402: drawn on the CPU generator, then moved -- through pinned memory, asynchronously:
         # a pageable host-to-device copy waits for the stream to drain, a bubble in every training step
         d = torch.zeros((SB, num_rays, 1)).normal_(mean=0.8, std=5e-2)
         if torch.device(device).type != "cuda":
             return d.to(device)
         return d.pin_memory().to(device, non_blocking=True)
+
+    def stage_host_draws(self):
+        """Before a replay of a captured training step (avr.graphs.GraphedTrainStep): the start distances an eager
+        step draws on the CPU generator (renderers.py:322 / :402, same call, same values), copied into the buffer
+        the captured march reads, on the current stream. Two pinned slots alternate; a slot is refilled only after
+        the copy that last read it has run."""
+        buf = self._graph_init
+        if buf is None:
+            return
+        ring = getattr(self, "_graph_ring", None)
+        if ring is None or ring[0][0].shape != buf.shape:
+            ring = self._graph_ring = [[torch.empty(buf.shape).pin_memory(), None] for _ in range(2)]
+            self._graph_slot = 0
+        slot = ring[self._graph_slot]
+        self._graph_slot ^= 1
+        if slot[1] is not None:
+            slot[1].synchronize()
+        slot[0].normal_(mean=0.8, std=5e-2)
+        buf.copy_(slot[0], non_blocking=True)
+        slot[1] = torch.cuda.Event()
+        slot[1].record(torch.cuda.current_stream(buf.device))
 
     def _side_stream(self, phi, world):
         """A second stream of world's device for the marched point's field pass (AdaptiveVolumeRenderer training on
@@ -290,7 +319,7 @@ class _LSTMMarch(nn.Module):
         if not (world.is_cuda and torch.is_grad_enabled() and getattr(phi, "use_fused", False)
                 and getattr(phi, "hip_backward", False)) or os.environ.get("AVR_ADAPTIVE_SIDE_STREAM") == "0":
             return None
-        if torch.cuda.is_current_stream_capturing():
+        if torch.cuda.is_current_stream_capturing() and os.environ.get("AVR_ADAPTIVE_SIDE_STREAM_IN_GRAPH") == "0":
             return None
         key = world.device
         if getattr(self, "_side", None) is None or self._side[0] != key:
@@ -479,23 +508,21 @@ class AdaptiveVolumeRenderer(_LSTMMarch):
         init = self._initial_distance(SB, num_rays, dev, noise)
         world = self.march(ros, rds, init, phi)
         # coarse image at the marched point. In training on the HIP path it runs on a side stream, beside the band
-        # pass: its field launches cover 64 samples per workgroup, so SB x R points fill a tenth of the chip, and
-        # autograd runs each backward on its forward's stream, so the two passes overlap in the backward too. The
-        # kernels and their results are the same; only their order on the device changes.
+        # pass: its field launches cover 64 samples per workgroup, so SB x R points fill a tenth of the chip. It is
+        # issued after the band pass, so autograd (which runs each backward on its forward's stream, later nodes
+        # first) starts its backward first, on the side stream, and the band's backward fills the rest of the chip.
+        # The kernels and their results are the same (no random draws in it); only their order on the device changes.
+        def coarse_pass():
+            out = phi(world.reshape(SB, -1, 3), viewdirs=rds.reshape(SB, -1, 3), coarse=True, return_features=False)
+            return out, ops.depth_of_points(world, c2w_info).reshape(SB, num_rays, -1)
+
         side = self._side_stream(phi, world)
-        if side is not None:
+        if side is None:
+            output_coarse, depth_coarse = coarse_pass()
+        else:   # the march's outputs are ready at this point of the caller's stream
             main = torch.cuda.current_stream(dev)
-            side.wait_stream(main)
-            for t in (world, rds) + tuple(x for x in c2w_info if torch.is_tensor(x)):
-                t.record_stream(side)
-            with torch.cuda.stream(side):
-                output_coarse = phi(world.reshape(SB, -1, 3), viewdirs=rds.reshape(SB, -1, 3), coarse=True,
-                                    return_features=False)
-                depth_coarse = ops.depth_of_points(world, c2w_info).reshape(SB, num_rays, -1)
-        else:
-            output_coarse = phi(world.reshape(SB, -1, 3), viewdirs=rds.reshape(SB, -1, 3), coarse=True,
-                                return_features=False)
-            depth_coarse = ops.depth_of_points(world, c2w_info).reshape(SB, num_rays, -1)
+            marched = torch.cuda.Event()
+            marched.record(main)
         # band around the marched distance (renderers.py:490-496); the sort is a no-op on stratified z
         final_distance = (world[..., 0] - ros[..., 0]) / rds[..., 0]
         u = None if noise is None else noise.get("band")
@@ -512,6 +539,12 @@ class AdaptiveVolumeRenderer(_LSTMMarch):
                 pts = ros.unsqueeze(-2) + rds.unsqueeze(-2) * z_vals_sorted.unsqueeze(-1)
             field = phi(pts.reshape(SB, -1, 3), coarse=False, viewdirs=vd.reshape(SB, -1, 3),
                         return_features=False).reshape(SB, num_rays, self.n_coarse, 4)
+        if side is not None:   # fork (issued after the band's field launch, waiting only for the march)
+            side.wait_event(marched)
+            for t in (world, rds) + tuple(x for x in c2w_info if torch.is_tensor(x)):
+                t.record_stream(side)
+            with torch.cuda.stream(side):
+                output_coarse, depth_coarse = coarse_pass()
         rgb, distance_map, _ = volume_integral(z_vals_sorted, field[..., 3:], field[..., :3],
                                                white_back=self.white_back)
         depth_map = ops.depth_from_world(ros, rds, distance_map.reshape(SB, num_rays), c2w_info)

@@ -460,15 +460,35 @@ def run_train(args, device, train_pmc=None):
 
     res, nonfinite = {}, {}
     for mode in args.train_modes.split(","):
-        net.hip_backward = mode == "hip"
-        for _ in range(args.warmup):
-            step()
+        net.hip_backward = mode in ("hip", "hip_graph")
+        run = step
+        if mode == "hip_graph":
+            # the same step captured into one HIP graph (avr.graphs.GraphedTrainStep) with a capturable Adam; the
+            # VolumeRenderer's in-kernel Philox draws would be keyed by the capture-time offset, so the adaptive
+            # renderer only (its draws: the CPU start distances, staged per replay, and torch.rand on device)
+            from avr.graphs import GraphedTrainStep
+            if args.renderer != "adaptive":
+                raise SystemExit("bench.py: --train-modes hip_graph needs --renderer adaptive")
+            opt_g = torch.optim.Adam(params, lr=1e-4, capturable=True)
+
+            def step_g():
+                rgb_c, rgb_f, _, _ = rend(c2w, K, x_pix, net)
+                loss = ((rgb_c - gt) ** 2).mean() + ((rgb_f - gt) ** 2).mean()
+                opt_g.zero_grad()
+                loss.backward()
+                opt_g.step()
+                return loss
+            run = GraphedTrainStep(step_g, nets=[net], renderers=[rend], warmup=3)
+        for _ in range(max(args.warmup, 5 if mode == "hip_graph" else 0)):
+            run()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            loss = step()
+            loss = run()
         torch.cuda.synchronize()
         res[mode] = (time.perf_counter() - t0) / args.steps
+        if mode == "hip_graph":
+            assert run.captures == 1 and bool(torch.isfinite(loss)), (run.captures, float(loss))
         if mode == "hip":
             assert bool(torch.isfinite(loss)), f"{mode}: non-finite loss {float(loss)} after the timed steps"
         elif not bool(torch.isfinite(loss)):
@@ -485,11 +505,12 @@ def run_train(args, device, train_pmc=None):
         spr = rend.n_coarse + rend.n_coarse + rend.n_fine
         wl = (f"train.py defaults: {SB} scenes x {R} rays, {rend.n_coarse} coarse + {rend.n_fine} fine "
               f"({rend.n_fine_depth} depth) samples, Adam lr 1e-4")
+    hip_t = res["hip"] if "hip" in res else res["hip_graph"]
     line = {
         "metric": "training rays/s (train.py step: forward + loss.backward() + Adam through "
                   + ("AdaptiveVolumeRenderer)" if args.renderer == "adaptive" else "VolumeRenderer)"),
-        "value": round(SB * R / res["hip"], 1), "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(res["hip"] * 1e3, 3), "higher_is_better": True,
+        "value": round(SB * R / hip_t, 1), "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(hip_t * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (field products as 3 fp16 MFMA terms)",
         "data": f"synthetic: random-init {args.conf}.conf field{' with --bn (training-mode BatchNorm)' if args.bn else ''}"
                 f"{' with use_spade' if args.spade else ''}, {SB * NS} random 512x64x64 latents"
@@ -500,11 +521,16 @@ def run_train(args, device, train_pmc=None):
                                   ", layer by layer: avr.layer_train)" if (args.spade or NS > 1) else ")"),
                    "field_samples_per_step": SB * R * spr},
     }
+    if "hip_graph" in res:
+        line["hip_graph"] = {"value": round(SB * R / res["hip_graph"], 1), "ms_per_step": round(res["hip_graph"] * 1e3, 3),
+                             "note": "the same step captured once into a HIP graph and replayed (avr.graphs."
+                                     "GraphedTrainStep; Adam(capturable=True)); the CPU start distances are drawn "
+                                     "and staged per replay as an eager step draws them"}
     if "torch" in res:
         line["torch_autograd"] = {"value": round(SB * R / res["torch"], 1), "ms_per_step": round(res["torch"] * 1e3, 3)}
         if "torch" in nonfinite:
             line["torch_autograd"]["nonfinite_loss"] = nonfinite["torch"]
-        line["speedup_vs_torch_autograd"] = round(res["torch"] / res["hip"], 3)
+        line["speedup_vs_torch_autograd"] = round(res["torch"] / hip_t, 3)
     if train_pmc is not None:
         kern, note = train_pmc
         line["pmc"] = kern if kern is not None else {"note": note}

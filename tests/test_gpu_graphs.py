@@ -143,3 +143,39 @@ def test_graph_survives_eager_calls_that_replace_caches():
     gr()
     assert gr.captures == captures + 1          # a precision change re-captures
     net.field_precision = "x3"
+
+
+@pytest.mark.parametrize("side", ["1", "0"])
+def test_graphed_train_step_matches_eager_adaptive(side, monkeypatch):
+    """avr.graphs.GraphedTrainStep: bench.run_train's AdaptiveVolumeRenderer train.py step (default_mv field,
+    4 scenes x 512 rays, capturable Adam) captured once and replayed gives the eager step's losses and parameters
+    bit for bit over several steps -- the CPU start distances staged per replay draw the same values, the band's
+    device draws advance as eager ones do -- with the marched point's pass on its side stream inside the graph or
+    not."""
+    from test_gpu_poison import _setup
+    from avr.graphs import GraphedTrainStep
+    monkeypatch.setenv("AVR_ADAPTIVE_SIDE_STREAM_IN_GRAPH", side)
+    runs = []
+    for graphed in (False, True):
+        net, rend, named, (c2w, K, x_pix, gt), _ = _setup("adaptive", False)
+        opt = torch.optim.Adam([p for _, p in named], lr=1e-4, capturable=True)
+
+        def step():
+            rgb_c, rgb_f, _, _ = rend(c2w, K, x_pix, net)
+            loss = ((rgb_c - gt) ** 2).mean() + ((rgb_f - gt) ** 2).mean()
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            return loss
+        run = GraphedTrainStep(step, nets=[net], renderers=[rend], warmup=2) if graphed else step
+        torch.manual_seed(123)
+        losses = [float(run()) for _ in range(6)]
+        assert rend.last_path == "hip_train"
+        if graphed:
+            assert run.captures == 1 and run.calls == 6
+        runs.append((losses, {n: p.detach().clone() for n, p in named}))
+    (le, pe), (lg, pg) = runs
+    assert all(torch.isfinite(torch.tensor(le)))
+    assert le == lg, (le, lg)
+    for n in pe:
+        assert torch.equal(pe[n], pg[n]), n
