@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so")
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
+AVR_LOOKUP_GRAD_TERMS = 8
 ABI_VERSION = 15
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -101,6 +102,8 @@ _SIGS = {
     "avr_raymarch_train": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_raymarch_bwd_scratch_bytes": [i64, c_int, i64, ctypes.POINTER(i64)],
+    "avr_latent_tables_grad_points": [ctypes.POINTER(ViewDesc), c_int, c_void_p, i64, i64, c_int, c_int, c_void_p, i64,
+                                      c_void_p, i64, c_void_p, c_void_p],
     "avr_raymarch_bwd": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, i64, c_int, c_int, c_void_p, c_void_p, c_void_p, i64, c_void_p],
     "avr_march_state_bytes": [i64, ctypes.POINTER(i64)],

@@ -10,6 +10,7 @@ for encode() once.
 """
 import collections
 import ctypes
+import os
 import weakref
 
 import torch
@@ -216,11 +217,14 @@ class FusedField:
         # mlp (weakly) -> ([(name, owner dict, key)] params, [...] float buffers, generation, ids of its modules)
         self._slots = weakref.WeakKeyDictionary()
 
-    def invalidate(self):
-        """Drop every cached blob, table and view descriptor (avr.parallel.broadcast_scene calls it after
-        writing a scene into the net; the (data_ptr, _version) keys would catch that too)."""
+    def invalidate(self, views=True):
+        """Drop every cached blob, table and (views=True) view descriptor (avr.parallel.broadcast_scene calls it
+        after writing a scene into the net; the (data_ptr, _version) keys would catch that too). views=False keeps
+        the host-side view descriptors (avr.graphs.GraphedTrainStep before a capture: building one reads the poses
+        back to the host, which a capture cannot do)."""
         self._packed.clear()
-        self._view_cache.clear()
+        if views:
+            self._view_cache.clear()
         self._latent_cache.clear()
 
     def cache_tensors(self):
@@ -653,6 +657,7 @@ class _FieldTrain(torch.autograd.Function):
         entry.dims.precision = PRECISIONS[fused.precision]
         ctx.fused, ctx.coarse, ctx.names, ctx.entry = fused, coarse, names, entry
         ctx.act, ctx.act_max, ctx.masks, ctx.zf = act, act_max, masks, zf
+        ctx.tables = tables
         ctx.save_for_backward(xyz, viewdirs, latent, out, *params)
         return out
 
@@ -747,15 +752,33 @@ class _FieldTrain(torch.autograd.Function):
             d_look = None
             if not net.stop_encoder_grad:
                 with torch.no_grad():
-                    g_feat = _feat_grad(fused, entry, bwd, Gz, P, Mt)
                     d_look = torch.empty(Mt, 3, device=dev, dtype=F32)
-                    hwc = fused.latent_hwc_all(latent)
                     p = xyz.detach().to(F32).contiguous()
-                    for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
-                        n = min(_lib.AVR_MAX_SCENES, SB - g0)
-                        views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
-                        call("avr_latent_features_grad_points", views, n, ptr(hwc[g0]), net.d_latent, ptr(p[g0]),
-                             B, ptr(g_feat[g0 * B]), ptr(d_look[g0 * B]), stream_of(d_look))
+                    tabs = ctx.tables
+                    via_tables = (not dims.spade and nz <= _lib.AVR_LOOKUP_GRAD_TERMS and tabs.shape[0] == SB
+                                  and os.environ.get("AVR_POINT_GRAD_VIA_FEATURES") != "1")
+                    if via_tables:
+                        # sum_b Gz[b] . lin_z[b](interp(latent, p)) = sum_b Gz[b] . interp(table_b, p): the corner
+                        # differences of the forward's per-texel tables against each Gz row (ABI 15), no
+                        # d_hidden x d_latent product per point for the feature gradient
+                        ld = Gz[0].stride(0)
+                        assert all(g.stride(0) == ld and g.stride(1) == 1 for g in Gz)
+                        gptr = [g.data_ptr() for g in Gz]
+                        for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
+                            n = min(_lib.AVR_MAX_SCENES, SB - g0)
+                            views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+                            gr = (ctypes.c_void_p * nz)(*[g + g0 * B * ld * 4 for g in gptr])
+                            call("avr_latent_tables_grad_points", views, n, ptr(tabs[g0]), tabs.stride(0),
+                                 tabs.stride(1), nz, H, ptr(p[g0]), B, gr, ld, ptr(d_look[g0 * B]),
+                                 stream_of(d_look))
+                    else:
+                        g_feat = _feat_grad(fused, entry, bwd, Gz, P, Mt)
+                        hwc = fused.latent_hwc_all(latent)
+                        for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
+                            n = min(_lib.AVR_MAX_SCENES, SB - g0)
+                            views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+                            call("avr_latent_features_grad_points", views, n, ptr(hwc[g0]), net.d_latent,
+                                 ptr(p[g0]), B, ptr(g_feat[g0 * B]), ptr(d_look[g0 * B]), stream_of(d_look))
             with torch.enable_grad():
                 x = xyz.detach().requires_grad_(True)
                 zft = net.z_features(x, viewdirs.detach())

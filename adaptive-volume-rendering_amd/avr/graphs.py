@@ -130,7 +130,9 @@ class GraphedTrainStep:
 
     Calls 1 .. warmup run step_fn eagerly (real steps, on a side stream, so the graph's memory pool starts clean);
     the next call captures it (the capture records launches without running them) and replays it once; later
-    calls replay. Every call is one training step.
+    calls replay. Every call is one training step. The outputs returned are detached; drop any reference to an
+    earlier step's autograd graph (a loss kept from an eager step) before the first call: it would keep the
+    parameters' AccumulateGrad nodes, created on the streams of that step, alive into the capture.
 
     Host-side inputs: each marcher in `renderers` (Raymarcher / AdaptiveVolumeRenderer) draws its start distances
     on the CPU generator in an eager step (renderers.py:322 / :402); before every replay stage_host_draws() makes
@@ -140,10 +142,10 @@ class GraphedTrainStep:
     State: the captured kernels take the source-view descriptors (poses, focal, principal point, latent map
     shape) as launch arguments, and read the latent map through its address: like GraphedRenderer, every call
     checks the nets' view tensors (a new latent or pose tensor, or an in-place update of one) and the field
-    precision, and captures again when one changed; refill the latent in place for a new scene of one shape and
-    the capture stays valid only if the poses did not change. Parameters are updated by the captured optimizer
-    step itself. The nets' FusedField caches are dropped before a capture, so every blob and lin_z table the
-    step reads is rebuilt inside the graph from the current parameters.
+    precision; when one changed, that call runs eagerly (rebuilding the view descriptors on the host, which a
+    capture cannot) and the next one captures again. Parameters are updated by the captured optimizer step
+    itself. The nets' FusedField blob and table caches are dropped before a capture, so every blob and lin_z
+    table the step reads is rebuilt inside the graph from the current parameters.
     """
 
     @staticmethod
@@ -187,7 +189,7 @@ class GraphedTrainStep:
         for net in self.nets:
             fused = getattr(net, "_fused", None)
             if fused is not None:
-                fused.invalidate()   # every blob / table the step reads is made inside the graph
+                fused.invalidate(views=False)   # every blob / table the step reads is made inside the graph
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             out = self.step_fn()
@@ -198,14 +200,19 @@ class GraphedTrainStep:
 
     def __call__(self):
         self.calls += 1
-        if self.calls <= self.warmup:
+        if self.graph is not None and self._stale():
+            # new views: this step runs eagerly (it rebuilds the host-side view descriptors, which a capture
+            # cannot), the next one captures again
+            self.graph = self.out = None
+            self._eager_until = self.calls
+        if self.calls <= max(self.warmup, getattr(self, "_eager_until", 0)):
             stream = torch.cuda.Stream()
             stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(stream):
                 out = self._detach(self.step_fn())
             torch.cuda.current_stream().wait_stream(stream)
             return out
-        if self.graph is None or self._stale():
+        if self.graph is None:
             self._capture()
         for r in self.renderers:
             r.stage_host_draws()

@@ -108,18 +108,27 @@ __device__ __forceinline__ float lane_sum(float v) {
   return v;
 }
 
-__global__ void __launch_bounds__(256) latent_features_grad_points_kernel(LatBatch vb, const float* __restrict__ lat_hwc,
-                                                                          int64_t lat_stride, int C,
+// The summed rows: term t contributes sum_c g_t[c] (corner differences of map_t)[c], map_t (H*W, C) of scene s at
+// map[t] + s * map_scene_stride, g_t the point's row at g[t] + row * ldg[t]. One term (the looked-up latent and
+// its feature gradient: avr_latent_features_grad_points) or one per linear layer fed by the lookup with that
+// layer's per-texel table and output gradient (avr_latent_tables_grad_points).
+struct GradTerms {
+  const float* map[AVR_LOOKUP_GRAD_TERMS];
+  const float* g[AVR_LOOKUP_GRAD_TERMS];
+  int64_t ldg[AVR_LOOKUP_GRAD_TERMS];
+  int64_t map_scene_stride;
+  int n;
+};
+
+__global__ void __launch_bounds__(256) latent_features_grad_points_kernel(LatBatch vb, GradTerms T, int C,
                                                                           const float* __restrict__ xyz,
                                                                           int64_t n_points,
-                                                                          const float* __restrict__ gfeat,
                                                                           float* __restrict__ gxyz) {
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= n_points) return;
   const int s = blockIdx.y;
   const View& v = vb.v[s];
-  lat_hwc += s * lat_stride;
   const int64_t row = s * n_points + m;
   const float x0 = xyz[3 * row], x1 = xyz[3 * row + 1], x2 = xyz[3 * row + 2];
   const float xr[3] = {dot3(v.R + 0, x0, x1, x2), dot3(v.R + 3, x0, x1, x2), dot3(v.R + 6, x0, x1, x2)};
@@ -136,17 +145,20 @@ __global__ void __launch_bounds__(256) latent_features_grad_points_kernel(LatBat
   const float wx1 = fsub(ix, fx0), wy1 = fsub(iy, fy0);
   const float wx0 = fsub(fadd(fx0, 1.0f), ix), wy0 = fsub(fadd(fy0, 1.0f), iy);
   float sx = 0.f, sy = 0.f;
-  const float* g = gfeat + row * C;
-  for (int c = 4 * lane; c < C; c += 256) {
-    const floatx4 gv = *reinterpret_cast<const floatx4*>(g + c);
-    const floatx4 nw = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[0] * C + c);
-    const floatx4 ne = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[1] * C + c);
-    const floatx4 sw = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[2] * C + c);
-    const floatx4 se = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[3] * C + c);
+  for (int t = 0; t < T.n; ++t) {
+    const float* lat_hwc = T.map[t] + s * T.map_scene_stride;
+    const float* g = T.g[t] + row * T.ldg[t];
+    for (int c = 4 * lane; c < C; c += 256) {
+      const floatx4 gv = *reinterpret_cast<const floatx4*>(g + c);
+      const floatx4 nw = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[0] * C + c);
+      const floatx4 ne = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[1] * C + c);
+      const floatx4 sw = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[2] * C + c);
+      const floatx4 se = *reinterpret_cast<const floatx4*>(lat_hwc + (int64_t)bl.tex[3] * C + c);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sx += gv[t] * ((ne[t] - nw[t]) * wy0 + (se[t] - sw[t]) * wy1);
-      sy += gv[t] * ((sw[t] - nw[t]) * wx0 + (se[t] - ne[t]) * wx1);
+      for (int q = 0; q < 4; ++q) {
+        sx += gv[q] * ((ne[q] - nw[q]) * wy0 + (se[q] - sw[q]) * wy1);
+        sy += gv[q] * ((sw[q] - nw[q]) * wx0 + (se[q] - ne[q]) * wx1);
+      }
     }
   }
   sx = lane_sum(sx);
@@ -172,6 +184,17 @@ __global__ void __launch_bounds__(256) latent_features_grad_points_kernel(LatBat
 
 }  // namespace avr
 
+static int lookup_views(const avr_view_desc* views, int n_scenes, LatBatch* vb, const char* what) {
+  AVR_REQUIRE(n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES, "%s: 1..%d scenes per call", what, AVR_MAX_SCENES);
+  for (int s = 0; s < n_scenes; ++s) {
+    AVR_REQUIRE(views[s].latent_h == views[0].latent_h && views[s].latent_w == views[0].latent_w &&
+                    views[s].latent_h > 0 && views[s].latent_w > 0,
+                "%s: scenes need latent maps of one (positive) size", what);
+    view_from_desc(&views[s], &vb->v[s]);
+  }
+  return AVR_OK;
+}
+
 extern "C" int avr_latent_features_grad_points(const avr_view_desc* views, int n_scenes, const float* latent_hwc,
                                                int channels, const float* xyz, int64_t n_points,
                                                const float* grad_features, float* grad_xyz, void* stream) {
@@ -181,15 +204,46 @@ extern "C" int avr_latent_features_grad_points(const avr_view_desc* views, int n
   if (n_points == 0) return AVR_OK;
   AVR_REQUIRE(views && latent_hwc && xyz && grad_features && grad_xyz, "avr_latent_features_grad_points: null pointer");
   LatBatch vb;
-  for (int s = 0; s < n_scenes; ++s) {
-    AVR_REQUIRE(views[s].latent_h == views[0].latent_h && views[s].latent_w == views[0].latent_w &&
-                    views[s].latent_h > 0 && views[s].latent_w > 0,
-                "avr_latent_features_grad_points: scenes need latent maps of one (positive) size");
-    view_from_desc(&views[s], &vb.v[s]);
-  }
-  const int64_t stride = (int64_t)views[0].latent_h * views[0].latent_w * channels;
+  int rc = lookup_views(views, n_scenes, &vb, "avr_latent_features_grad_points");
+  if (rc) return rc;
+  GradTerms T{};
+  T.n = 1;
+  T.map[0] = latent_hwc;
+  T.g[0] = grad_features;
+  T.ldg[0] = channels;
+  T.map_scene_stride = (int64_t)views[0].latent_h * views[0].latent_w * channels;
   latent_features_grad_points_kernel<<<dim3((unsigned)((n_points + 3) / 4), (unsigned)n_scenes), 256, 0,
-                                       as_stream(stream)>>>(vb, latent_hwc, stride, channels, xyz, n_points,
-                                                            grad_features, grad_xyz);
+                                       as_stream(stream)>>>(vb, T, channels, xyz, n_points, grad_xyz);
+  return check_launch("latent_features_grad_points_kernel");
+}
+
+extern "C" int avr_latent_tables_grad_points(const avr_view_desc* views, int n_scenes, const float* tables,
+                                             int64_t table_scene_stride, int64_t table_stride, int n_tables,
+                                             int channels, const float* xyz, int64_t n_points,
+                                             const float* const* grads, int64_t ld_grad, float* grad_xyz,
+                                             void* stream) {
+  AVR_REQUIRE(n_points >= 0 && channels > 0 && channels % 4 == 0 && ld_grad >= channels && ld_grad % 4 == 0 &&
+                  n_tables >= 1 && n_tables <= AVR_LOOKUP_GRAD_TERMS && table_stride >= 0 && table_scene_stride >= 0,
+              "avr_latent_tables_grad_points: bad sizes");
+  if (n_points == 0) return AVR_OK;
+  AVR_REQUIRE(views && tables && xyz && grads && grad_xyz, "avr_latent_tables_grad_points: null pointer");
+  LatBatch vb;
+  int rc = lookup_views(views, n_scenes, &vb, "avr_latent_tables_grad_points");
+  if (rc) return rc;
+  const int64_t hw = (int64_t)views[0].latent_h * views[0].latent_w;
+  AVR_REQUIRE((table_stride >= hw * channels || n_tables == 1) && (table_scene_stride >= n_tables * hw * channels ||
+                                                                    n_scenes == 1),
+              "avr_latent_tables_grad_points: overlapping tables");
+  GradTerms T{};
+  T.n = n_tables;
+  T.map_scene_stride = table_scene_stride;
+  for (int t = 0; t < n_tables; ++t) {
+    AVR_REQUIRE(grads[t], "avr_latent_tables_grad_points: null gradient rows %d", t);
+    T.map[t] = tables + t * table_stride;
+    T.g[t] = grads[t];
+    T.ldg[t] = ld_grad;
+  }
+  latent_features_grad_points_kernel<<<dim3((unsigned)((n_points + 3) / 4), (unsigned)n_scenes), 256, 0,
+                                       as_stream(stream)>>>(vb, T, channels, xyz, n_points, grad_xyz);
   return check_launch("latent_features_grad_points_kernel");
 }

@@ -487,6 +487,9 @@ def run_train(args, device, train_pmc=None):
             loss = run()
         torch.cuda.synchronize()
         res[mode] = (time.perf_counter() - t0) / args.steps
+        # no autograd graph of this mode outlives it (its AccumulateGrad nodes would carry their streams into the
+        # next mode's steps, and into a capture)
+        loss = loss.detach()
         if mode == "hip_graph":
             assert run.captures == 1 and bool(torch.isfinite(loss)), (run.captures, float(loss))
         if mode == "hip":

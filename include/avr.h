@@ -26,6 +26,7 @@ extern "C" {
 
 #define AVR_ABI_VERSION 15
 #define AVR_MAX_BLOCKS 8
+#define AVR_LOOKUP_GRAD_TERMS 8   /* tables per avr_latent_tables_grad_points call */
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
 
 enum {
@@ -469,6 +470,19 @@ int avr_latent_features_batch(const avr_view_desc* views, int n_scenes, const fl
 int avr_latent_features_grad_points(const avr_view_desc* views, int n_scenes, const float* latent_hwc, int channels,
                                     const float* xyz, int64_t n_points, const float* grad_features, float* grad_xyz,
                                     void* stream);
+/* ABI 15: the same position gradient where the looked-up features feed only linear maps whose per-texel images are
+ * at hand -- the lin_z tables (avr_field_latent_table: table_b = lin_z[b].weight @ latent, no bias): sum_b
+ * grad_b . lin_z[b](interp(latent, p)) = sum_b grad_b . interp(table_b, p) (both linear), so the gradient through
+ * the lookup needs no d loss / d features = sum_b grad_b W_z[b] (a d_hidden x d_latent product per point per
+ * table) -- the corner differences of each table dotted with its row of grad_b. tables: scene s, table b at
+ * tables + s * table_scene_stride + b * table_stride, (H*W, channels) each; grads[b] (n_scenes * n_points, ld_grad)
+ * the gradient at lin_z[b]'s output (d loss / d block-b input); grad_xyz (n_scenes * n_points, 3) written.
+ * 1 <= n_tables <= AVR_LOOKUP_GRAD_TERMS. Replaces the torch autograd of SpatialEncoder.index for points whose
+ * latent map needs no gradient (the adaptive renderer's band, renderers.py:492-508). */
+int avr_latent_tables_grad_points(const avr_view_desc* views, int n_scenes, const float* tables,
+                                  int64_t table_scene_stride, int64_t table_stride, int n_tables, int channels,
+                                  const float* xyz, int64_t n_points, const float* const* grads, int64_t ld_grad,
+                                  float* grad_xyz, void* stream);
 
 /* --------------------------------------------------------- LSTM ray marcher
  * Raymarcher / AdaptiveVolumeRenderer march (renderers.py:313-351, :380-432):

@@ -2,7 +2,8 @@
 blocks of STEPS steps alternate between arms (environment switches read per call), ROUNDS times, so box jitter
 hits both arms alike; prints each arm's per-block ms and median.
 
-usage: python scripts/adaptive_ab.py [ROUNDS] [STEPS] ARM_A_ENV ARM_B_ENV   (an arm: "NAME=VALUE,..." or "-")"""
+usage: python scripts/adaptive_ab.py [ROUNDS] [STEPS] ARM_A ARM_B   (an arm: "NAME=VALUE,..." environment
+switches, or "-"; a leading "graph:" runs that arm through avr.graphs.GraphedTrainStep with a capturable Adam)"""
 import os
 import statistics
 import sys
@@ -36,23 +37,34 @@ def main():
         p.requires_grad_(True)
     torch.manual_seed(11)
     rend = AdaptiveVolumeRenderer.from_conf(default_conf()["adaptive_renderer"]).to(dev)
-    opt = torch.optim.Adam(list(net.parameters()) + list(rend.parameters()), lr=1e-4)
+    params = list(net.parameters()) + list(rend.parameters())
+    opt = torch.optim.Adam(params, lr=1e-4)
+    opt_g = torch.optim.Adam(params, lr=1e-4, capturable=True)
     x_pix = torch.rand(SB, R, 2, generator=g).to(dev)
     c2w = torch.stack([bench.orbit_c2w(0.3 + 0.9 * b) for b in range(SB)]).to(dev)
     c2w = c2w.reshape(SB, 1, 4, 4).expand(SB, R, 4, 4)
     K = torch.tensor([[[1.0254, 0.0, 0.5], [0.0, 1.0254, 0.5], [0.0, 0.0, 1.0]]] * SB, device=dev)
     gt = torch.rand(SB, R, 3, generator=g).to(dev)
 
-    def step():
-        rgb_c, rgb_f, _, _ = rend(c2w, K, x_pix, net)
-        loss = ((rgb_c - gt) ** 2).mean() + ((rgb_f - gt) ** 2).mean()
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
-        return loss
+    def make_step(o):
+        def step():
+            rgb_c, rgb_f, _, _ = rend(c2w, K, x_pix, net)
+            loss = ((rgb_c - gt) ** 2).mean() + ((rgb_f - gt) ** 2).mean()
+            o.zero_grad()
+            loss.backward()
+            o.step()
+            return loss.detach()
+        return step
+
+    from avr.graphs import GraphedTrainStep
+    runners = {}
+    for a in arms:
+        runners[a] = (GraphedTrainStep(make_step(opt_g), nets=[net], renderers=[rend], warmup=2)
+                      if a.startswith("graph:") else make_step(opt))
 
     def setenv(arm):
-        if arm == "-":
+        arm = arm[len("graph:"):] if arm.startswith("graph:") else arm
+        if arm in ("-", ""):
             return
         for kv in arm.split(","):
             k, v = kv.split("=", 1)
@@ -62,11 +74,12 @@ def main():
     for a in arms:
         setenv(a)
         for _ in range(5):
-            step()
+            runners[a]()
     torch.cuda.synchronize()
     for r in range(rounds):
         for a in arms:
             setenv(a)
+            step = runners[a]
             step()
             torch.cuda.synchronize()
             t0 = time.perf_counter()

@@ -357,6 +357,71 @@ def test_latent_features_grad_points_vs_autograd():
     print(f"grad points: HIP err {eh / s:.2e}, torch fp32 err {et / s:.2e} of max {s:.3e}")
 
 
+@pytest.mark.parametrize("n_tables", [1, 3])
+def test_latent_tables_grad_points_vs_fp64(n_tables):
+    """avr_latent_tables_grad_points (ABI 15): the lookup's position gradient from the per-texel lin_z tables, sum_b
+    Gz[b] . interp(W_z[b] latent, p), against float64 autograd of the module's lookup with the feature gradient
+    sum_b Gz[b] W_z[b] (the same quantity: both maps are linear); two scenes, points in and outside the image,
+    gradient rows with a leading dimension past d_hidden. The fp32 autograd of the feature path is the yardstick."""
+    from avr import _lib
+    from avr._lib import ViewDesc
+    H, C, M = 256, 512, 700
+    net = _net(128, 2, C, (16, 16), sb=2)
+    xyz, vd, _ = _points(2, M, seed=23)
+    xyz = xyz * torch.where(torch.arange(M, device=DEV) % 3 == 0, 3.0, 1.0).reshape(1, M, 1)
+    g = torch.Generator().manual_seed(6)
+    Wz = [torch.randn(H, C, generator=g).to(DEV) * 0.05 for _ in range(n_tables)]
+    ld = H + 8
+    Gbuf = [torch.randn(2 * M, ld, generator=g).to(DEV) for _ in range(n_tables)]
+    Gz = [b[:, :H] for b in Gbuf]
+    lat = net.encoder.latent                                    # (2, C, h, w)
+    tabs = torch.stack([torch.stack([(Wz[b] @ lat[s].reshape(C, -1)).t() for b in range(n_tables)])
+                        for s in range(2)]).contiguous()        # (2, n_tables, h*w, H)
+    fused = net.fused()
+    views = (ViewDesc * 2)(*[fused.view(sb) for sb in range(2)])
+    got = torch.empty(2 * M, 3, device=DEV)
+    grads = (ctypes.c_void_p * n_tables)(*[t.data_ptr() for t in Gz])
+    _lib.call("avr_latent_tables_grad_points", views, 2, _lib.ptr(tabs), tabs.stride(0), tabs.stride(1), n_tables, H,
+              _lib.ptr(xyz.contiguous()), M, grads, ld, _lib.ptr(got), _lib.stream_of(got))
+
+    def autograd(dtype):
+        x = xyz.to(dtype).clone().requires_grad_(True)
+        feat, _ = net.mlp_inputs(x, vd.to(dtype))
+        gfeat = sum(Gz[b].to(dtype) @ Wz[b].to(dtype) for b in range(n_tables))
+        return torch.autograd.grad(feat, x, gfeat)[0].reshape(-1, 3)
+
+    ref32 = autograd(torch.float32)
+    with torch.no_grad():
+        net.double()
+    try:
+        ref64 = autograd(torch.float64)
+    finally:
+        net.float()
+    s = float(ref64.abs().max())
+    eh = float((got.double() - ref64).abs().max())
+    et = float((ref32.double() - ref64).abs().max())
+    assert eh <= 2.0 * et + 1e-6 * s, (eh, et, s)
+    print(f"tables grad points ({n_tables}): HIP err {eh / s:.2e}, torch fp32 err {et / s:.2e} of max {s:.3e}")
+
+
+@pytest.mark.parametrize("via", ["tables", "features"])
+def test_field_train_point_gradient_paths(via, monkeypatch):
+    """The band points' lookup gradient on the fused training path both ways (ABI 15's tables path, the default,
+    and the feature-gradient path it replaced, AVR_POINT_GRAD_VIA_FEATURES=1) against float64 autograd."""
+    monkeypatch.setenv("AVR_POINT_GRAD_VIA_FEATURES", "1" if via == "features" else "0")
+    net = _net(512, 5, 512, (16, 16), 3)
+    xyz0, vd, w = _points(1, 700, seed=19)
+    res = {}
+    for hip in (True, False, "fp64"):
+        def run(hip=hip):
+            xyz = (xyz0.double() if hip == "fp64" else xyz0.clone()).requires_grad_(True)
+            v, ww = (vd.double(), w.double()) if hip == "fp64" else (vd, w)
+            _, g, _ = _grads(net, xyz, v, ww, True, hip=hip is True)
+            return dict(g, xyz=xyz.grad.detach().clone())
+        res[hip] = _fp64(net, run) if hip == "fp64" else run()
+    _compare64(res[True], res[False], res["fp64"])
+
+
 def test_latent_features_grad_points_on_source_camera_plane():
     """A point on the source camera's plane (camera z = 0: the projection is infinite, the lookup clipped to the
     border) gets exactly the clip's zero position gradient from the lookup, not 0 * inf = NaN. The r04q adaptive
