@@ -55,7 +55,7 @@ if has tprof; then
   head -6 $OUT/train_kernel_stats.csv | cut -c1-160
 fi
 if has trainx; then
-  for x in "bn:--bn" "adaptive:--renderer adaptive" "views2:--views 2" "spade_views2:--spade --views 2"; do
+  for x in "bn:--bn" "adaptive:--renderer adaptive --train-modes hip,hip_graph,torch" "views2:--views 2" "spade_views2:--spade --views 2"; do
     timeout -k 10 300 python -u bench.py --mode train --conf default_mv ${x#*:} --steps 20 --warmup 5 > $OUT/bench_train_${x%%:*}_mv.log 2>&1
     rc=$?; tail -1 $OUT/bench_train_${x%%:*}_mv.log | cut -c1-300; echo; [ $rc -eq 0 ] || { echo "train ${x%%:*} rc=$rc"; exit $rc; }
   done

@@ -86,6 +86,12 @@ def test_bench_dist_path_at_one_rank():
     assert line["n_gpus"] == 1 and line["scaling"] == "strong"
     assert "RCCL gather" in line["config"]["parallelism"]
     assert line["config"]["rays_per_gpu"] == 4 * 160 * 160 and line["value"] > 0
+    # the N > 1 attribution every config-5 line with a process group carries: per-rank
+    # shard phases, the scene broadcast, and every rank's field time (min / max over ranks)
+    assert {"render_ms_per_step", "all_gather_ms_per_step", "reassembly_ms_per_step"} <= set(line["shard_phases"])
+    assert "scene_broadcast" in line
+    fr = line["field_ms_per_rank"]
+    assert 0 < fr["min"] <= fr["max"] and fr["steps"] == 2 and fr["launches_per_rank"] > 0
 
 
 def test_broadcast_scene_over_rccl_world1(nccl_world1):
