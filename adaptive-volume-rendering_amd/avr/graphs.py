@@ -126,7 +126,8 @@ class GraphedTrainStep:
     step_fn() runs one step on tensors the caller keeps at fixed addresses (refill them in place between calls)
     and returns what the caller reads after the step (e.g. the loss); it may call optimizer.zero_grad() (the
     default set_to_none: a host-only no-op once captured: the captured backward writes the gradients). The
-    optimizer must be capturable (torch.optim.Adam(..., capturable=True)).
+    optimizer must be capturable: torch.optim.Adam(..., capturable=True, fused=True) (the fused form is one
+    multi-tensor kernel; the capturable foreach form adds many small launches).
 
     Calls 1 .. warmup run step_fn eagerly (real steps, on a side stream, so the graph's memory pool starts clean);
     the next call captures it (the capture records launches without running them) and replays it once; later

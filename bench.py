@@ -469,7 +469,10 @@ def run_train(args, device, train_pmc=None):
             from avr.graphs import GraphedTrainStep
             if args.renderer != "adaptive":
                 raise SystemExit("bench.py: --train-modes hip_graph needs --renderer adaptive")
-            opt_g = torch.optim.Adam(params, lr=1e-4, capturable=True)
+            # the optimizer a captured step needs: capturable (its step counts on the device); fused (one
+            # multi-tensor kernel: the capturable foreach form adds ~0.7 ms of small launches to this step,
+            # profiles/r06l_adaptive_graph_fused_adam_ab.txt)
+            opt_g = torch.optim.Adam(params, lr=1e-4, capturable=True, fused=True)
 
             def step_g():
                 rgb_c, rgb_f, _, _ = rend(c2w, K, x_pix, net)
@@ -527,8 +530,9 @@ def run_train(args, device, train_pmc=None):
     if "hip_graph" in res:
         line["hip_graph"] = {"value": round(SB * R / res["hip_graph"], 1), "ms_per_step": round(res["hip_graph"] * 1e3, 3),
                              "note": "the same step captured once into a HIP graph and replayed (avr.graphs."
-                                     "GraphedTrainStep; Adam(capturable=True)); the CPU start distances are drawn "
-                                     "and staged per replay as an eager step draws them"}
+                                     "GraphedTrainStep; Adam(capturable=True, fused=True) -- the eager legs use "
+                                     "train.py's default Adam); the CPU start distances are drawn and staged per "
+                                     "replay as an eager step draws them"}
     if "torch" in res:
         line["torch_autograd"] = {"value": round(SB * R / res["torch"], 1), "ms_per_step": round(res["torch"] * 1e3, 3)}
         if "torch" in nonfinite:

@@ -3,7 +3,8 @@ blocks of STEPS steps alternate between arms (environment switches read per call
 hits both arms alike; prints each arm's per-block ms and median.
 
 usage: python scripts/adaptive_ab.py [ROUNDS] [STEPS] ARM_A ARM_B   (an arm: "NAME=VALUE,..." environment
-switches, or "-"; a leading "graph:" runs that arm through avr.graphs.GraphedTrainStep with a capturable Adam)"""
+switches, or "-"; a leading "graph:" runs that arm through avr.graphs.GraphedTrainStep with a capturable Adam,
+"graphf:" with a capturable fused Adam)"""
 import os
 import statistics
 import sys
@@ -40,6 +41,7 @@ def main():
     params = list(net.parameters()) + list(rend.parameters())
     opt = torch.optim.Adam(params, lr=1e-4)
     opt_g = torch.optim.Adam(params, lr=1e-4, capturable=True)
+    opt_gf = torch.optim.Adam(params, lr=1e-4, capturable=True, fused=True)
     x_pix = torch.rand(SB, R, 2, generator=g).to(dev)
     c2w = torch.stack([bench.orbit_c2w(0.3 + 0.9 * b) for b in range(SB)]).to(dev)
     c2w = c2w.reshape(SB, 1, 4, 4).expand(SB, R, 4, 4)
@@ -59,11 +61,14 @@ def main():
     from avr.graphs import GraphedTrainStep
     runners = {}
     for a in arms:
-        runners[a] = (GraphedTrainStep(make_step(opt_g), nets=[net], renderers=[rend], warmup=2)
-                      if a.startswith("graph:") else make_step(opt))
+        if a.startswith("graph:") or a.startswith("graphf:"):
+            o = opt_gf if a.startswith("graphf:") else opt_g
+            runners[a] = GraphedTrainStep(make_step(o), nets=[net], renderers=[rend], warmup=2)
+        else:
+            runners[a] = make_step(opt)
 
     def setenv(arm):
-        arm = arm[len("graph:"):] if arm.startswith("graph:") else arm
+        arm = arm.split(":", 1)[1] if arm.startswith(("graph:", "graphf:")) else arm
         if arm in ("-", ""):
             return
         for kv in arm.split(","):

@@ -148,7 +148,7 @@ def test_graph_survives_eager_calls_that_replace_caches():
 @pytest.mark.parametrize("side", ["1", "0"])
 def test_graphed_train_step_matches_eager_adaptive(side, monkeypatch):
     """avr.graphs.GraphedTrainStep: bench.run_train's AdaptiveVolumeRenderer train.py step (default_mv field,
-    4 scenes x 512 rays, capturable Adam) captured once and replayed gives the eager step's losses and parameters
+    4 scenes x 512 rays, capturable fused Adam) captured once and replayed gives the eager step's losses and parameters
     bit for bit over several steps -- the CPU start distances staged per replay draw the same values, the band's
     device draws advance as eager ones do -- with the marched point's pass on its side stream inside the graph or
     not."""
@@ -158,7 +158,7 @@ def test_graphed_train_step_matches_eager_adaptive(side, monkeypatch):
     runs = []
     for graphed in (False, True):
         net, rend, named, (c2w, K, x_pix, gt), _ = _setup("adaptive", False)
-        opt = torch.optim.Adam([p for _, p in named], lr=1e-4, capturable=True)
+        opt = torch.optim.Adam([p for _, p in named], lr=1e-4, capturable=True, fused=True)
 
         def step():
             rgb_c, rgb_f, _, _ = rend(c2w, K, x_pix, net)
