@@ -14,6 +14,7 @@ import os
 import weakref
 
 import torch
+from torch.optim.optimizer import register_optimizer_step_post_hook
 
 from . import _lib
 from ._lib import FieldDims, ResnetFCWeights, ViewDesc, call, ptr, require_device, stream_of
@@ -154,8 +155,34 @@ def _slot_current(gen, module_ids):
 torch.nn.modules.module.register_module_module_registration_hook(_module_registered)
 
 
-def _version_key(tensors):
-    return tuple((t.data_ptr(), t._version) for t in tensors)
+# Every optimizer step anywhere in the process, counted: a fused optimizer (torch.optim.Adam(fused=True)) updates
+# the parameters in one multi-tensor kernel without advancing their version counters, so the (data_ptr, _version)
+# keys of the caches below would not see it (the blob would keep the old weights). The count is part of every key;
+# GraphedTrainStep advances it after each replay (a captured optimizer step runs no host hook).
+_PARAM_GEN = [0]
+
+
+def _optimizer_stepped(optimizer, args, kwargs):
+    _PARAM_GEN[0] += 1
+
+
+register_optimizer_step_post_hook(_optimizer_stepped)
+
+
+def bump_param_generation():
+    """Invalidate every FusedField cache entry derived from parameters or the latent map (after an update the
+    version counters do not record: a replayed optimizer step, a write through .data)."""
+    _PARAM_GEN[0] += 1
+
+
+def param_generation():
+    return _PARAM_GEN[0]
+
+
+def _version_key(tensors, gen=True):
+    """(data_ptr, _version) of each tensor, with the optimizer-step generation for anything an optimizer may
+    update (gen=False: the source views -- poses, focal, principal point -- which none does)."""
+    return ((_PARAM_GEN[0],) if gen else ()) + tuple((t.data_ptr(), t._version) for t in tensors)
 
 
 def _stamp(t):
@@ -243,7 +270,7 @@ class FusedField:
         return out
 
     def _latent_cached(self, what, latent, make):
-        key = (latent.data_ptr(), latent._version, tuple(latent.shape))
+        key = (_PARAM_GEN[0], latent.data_ptr(), latent._version, tuple(latent.shape))
         hit = self._latent_cache.get(what)
         if hit is not None and hit[0] == key:
             _join(hit[3], hit[1])
@@ -380,7 +407,7 @@ class FusedField:
     def table(self, coarse, sb=0):
         entry = self.packed(coarse)
         lat = self.net.encoder.latent
-        key = (sb, lat.data_ptr(), lat._version, tuple(lat.shape))
+        key = (sb, _PARAM_GEN[0], lat.data_ptr(), lat._version, tuple(lat.shape))
         hit = entry.tables.get(sb)
         if hit is not None and hit[0] == key:
             _join(hit[3], hit[1])
@@ -404,7 +431,7 @@ class FusedField:
         cache holds them (packed())."""
         entry = self.packed(coarse, bn_fold)
         lat = self.net.encoder.latent
-        key = (n_scenes, bool(fast), lat.data_ptr(), lat._version, tuple(lat.shape))
+        key = (n_scenes, bool(fast), _PARAM_GEN[0], lat.data_ptr(), lat._version, tuple(lat.shape))
         cache = entry.__dict__.setdefault("batch_tables", {})
         hit = cache.get(bool(fast))
         if hit is not None and hit[0] == key:
@@ -431,7 +458,7 @@ class FusedField:
         object sb // ns, as models.py:796-801 repeat_interleaves them)."""
         net = self.net
         srcs = [net.poses, net.focal, net.c, net.image_shape, net.encoder.latent_scaling]
-        key = (sb, ns, _version_key(srcs), tuple(net.encoder.latent.shape))
+        key = (sb, ns, _version_key(srcs, gen=False), tuple(net.encoder.latent.shape))
         hit = self._view_cache.get((sb, ns))
         if hit is not None and hit[0] == key:
             return hit[1]

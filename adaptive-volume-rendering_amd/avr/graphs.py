@@ -25,6 +25,7 @@ after that. Warm-ups and re-captures leave the renderer's Philox offset where it
 import torch
 
 from . import anomaly
+from .field import bump_param_generation, param_generation
 
 __all__ = ["GraphedRenderer", "GraphedTrainStep"]
 
@@ -66,7 +67,8 @@ class GraphedRenderer:
         # held references: no address is reused while compared
         return any(t._version != v for t, v in self._held) or \
             any(a is not b for a, b in zip(self._views(), self._held_views)) or \
-            getattr(self.net, "field_precision", None) != self._held_precision
+            getattr(self.net, "field_precision", None) != self._held_precision or \
+            param_generation() != self._held_gen   # an optimizer step (fused ones leave versions alone)
 
     def refresh(self):
         """Capture again (after replacing a Parameter object of the net, which the per-call check does not see)."""
@@ -100,6 +102,7 @@ class GraphedRenderer:
         views = self._views()
         self._held_views = views
         self._held = [(t, t._version) for t in self._params() + views if isinstance(t, torch.Tensor)]
+        self._held_gen = param_generation()
         self.captures += 1
 
     def __call__(self, cam2world=None, intrinsics=None, x_pix=None):
@@ -218,6 +221,7 @@ class GraphedTrainStep:
         for r in self.renderers:
             r.stage_host_draws()
         self.graph.replay()
+        bump_param_generation()   # the replayed optimizer step ran no host hook: eager calls must repack
         if anomaly.is_enabled():
             anomaly.check_outputs("GraphedTrainStep replay", self.out)
         return self.out

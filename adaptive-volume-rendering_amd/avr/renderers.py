@@ -25,6 +25,7 @@ import torch
 from torch import nn
 
 from . import _lib, ops
+from .field import param_generation
 
 
 def _noise(shape, like, kind):
@@ -329,7 +330,7 @@ class _LSTMMarch(nn.Module):
     def _gate_table(self, phi):
         lat = phi.encoder.latent
         w = self.lstm.weight_ih
-        key = (lat.data_ptr(), lat._version, tuple(lat.shape), w.data_ptr(), w._version)
+        key = (param_generation(), lat.data_ptr(), lat._version, tuple(lat.shape), w.data_ptr(), w._version)
         if self._gate_cache is not None and self._gate_cache[0] == key:
             return self._gate_cache[1]
         C = lat.shape[1]

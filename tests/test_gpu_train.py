@@ -636,3 +636,26 @@ def test_training_forward_stores_z_feature():
     assert bool((zf[:, d_in:] == 0).all())
     zmax = act_max[2 * nb + 1:].view(torch.float32)
     assert float(zmax) == float(zf[:, :d_in].abs().max())
+
+
+def test_fused_optimizer_step_reaches_the_field():
+    """A fused optimizer (torch.optim.Adam(fused=True)) updates the parameters in one kernel without advancing
+    their version counters: the packed blobs and tables must still be rebuilt after its step (the optimizer-step
+    generation in FusedField's cache keys), on the training path and the inference path alike -- checked against
+    PyTorch's forward of the same module after two large steps."""
+    net = _net(64, 3, 64, (8, 8))
+    xyz, vd, w = _points(1, 300, seed=29)
+    opt = torch.optim.Adam(net.mlp_coarse.parameters(), lr=5e-2, fused=True)
+    for _ in range(3):
+        opt.zero_grad()
+        out = net(xyz, coarse=True, viewdirs=vd)
+        with torch.no_grad():
+            ref = net.forward_torch(xyz, True, vd)
+        np.testing.assert_allclose(out.detach().cpu().numpy(), ref.cpu().numpy(), atol=1e-4)
+        (out * w).sum().backward()
+        opt.step()
+    with torch.no_grad():
+        assert net.can_fuse(xyz)
+        a = net(xyz, coarse=True, viewdirs=vd)
+        b = net.forward_torch(xyz, True, vd)
+    np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), atol=1e-4)

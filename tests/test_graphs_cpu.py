@@ -7,6 +7,7 @@ import torch
 
 def _graphed_state():
     from avr.conf import default_conf
+    from avr.field import param_generation
     from avr.graphs import GraphedRenderer
     from avr.models import NewPixelNeRFNet
     with warnings.catch_warnings():
@@ -23,6 +24,7 @@ def _graphed_state():
         g._held_views = views
         g._held = [(t, t._version) for t in g._params() + views if isinstance(t, torch.Tensor)]
         g._held_precision = net.field_precision
+        g._held_gen = param_generation()
     hold()
     return g, net, hold
 
@@ -48,3 +50,26 @@ def test_state_check_sees_updates():
     assert g._stale()
     hold()
     assert not g._stale()
+    p = net.mlp_coarse.lin_out.bias                 # a fused optimizer: no version bump, a generation step
+    p.grad = torch.ones_like(p)
+    torch.optim.Adam([p], lr=1e-3, fused=True).step()
+    assert g._stale()
+    hold()
+    assert not g._stale()
+
+
+def test_optimizer_steps_advance_the_param_generation():
+    """Every torch.optim step (fused ones too, which leave the parameters' version counters alone) advances the
+    generation FusedField's cache keys carry; GraphedTrainStep advances it per replay."""
+    import torch
+    from avr.field import bump_param_generation, param_generation
+    p = torch.nn.Parameter(torch.randn(8))
+    for opt in (torch.optim.Adam([p], lr=1e-2, fused=True), torch.optim.SGD([p], lr=1e-2)):
+        p.grad = torch.randn(8)
+        g0, v0 = param_generation(), p._version
+        opt.step()
+        assert param_generation() == g0 + 1
+    assert p._version >= v0
+    g0 = param_generation()
+    bump_param_generation()
+    assert param_generation() == g0 + 1
