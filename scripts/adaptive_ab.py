@@ -76,6 +76,7 @@ def main():
             os.environ[k] = v
 
     res = {a: [] for a in arms}
+    host = {}
     for a in arms:
         setenv(a)
         for _ in range(5):
@@ -90,9 +91,12 @@ def main():
             t0 = time.perf_counter()
             for _ in range(steps):
                 loss = step()
+            t_host = time.perf_counter() - t0          # the host's enqueue time (the GPU may still be running)
             torch.cuda.synchronize()
             res[a].append((time.perf_counter() - t0) / steps * 1e3)
-        print(f"round {r}: " + "  ".join(f"{a}: {res[a][-1]:.3f} ms" for a in arms), flush=True)
+            host.setdefault(a, []).append(t_host / steps * 1e3)
+        print(f"round {r}: " + "  ".join(f"{a}: {res[a][-1]:.3f} ms (host {host[a][-1]:.3f})" for a in arms),
+              flush=True)
     assert bool(torch.isfinite(loss))
     for a in arms:
         print(f"{a}: median {statistics.median(res[a]):.3f} ms per step over {rounds} blocks of {steps} "

@@ -179,3 +179,35 @@ def test_graphed_train_step_matches_eager_adaptive(side, monkeypatch):
     assert le == lg, (le, lg)
     for n in pe:
         assert torch.equal(pe[n], pg[n]), n
+
+
+def test_graphed_train_step_recaptures_after_view_change():
+    """GraphedTrainStep with new source views between steps (poses updated in place, as a new batch of scenes
+    would): the call that sees the change runs eagerly (it rebuilds the host-side view descriptors), the next
+    one captures again, and every step's loss equals the eager run's with the same change."""
+    from test_gpu_poison import _setup
+    from avr.graphs import GraphedTrainStep
+    runs = []
+    for graphed in (False, True):
+        net, rend, named, (c2w, K, x_pix, gt), _ = _setup("adaptive", False)
+        opt = torch.optim.Adam([p for _, p in named], lr=1e-4, capturable=True, fused=True)
+
+        def step():
+            rgb_c, rgb_f, _, _ = rend(c2w, K, x_pix, net)
+            loss = ((rgb_c - gt) ** 2).mean() + ((rgb_f - gt) ** 2).mean()
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            return loss
+        run = GraphedTrainStep(step, nets=[net], renderers=[rend], warmup=1) if graphed else step
+        torch.manual_seed(321)
+        losses = []
+        for i in range(7):
+            if i == 4:
+                with torch.no_grad():
+                    net.poses[:, 0, 3] += 0.02      # new source views, same shapes
+            losses.append(float(run()))
+        if graphed:
+            assert run.captures == 2, run.captures
+        runs.append(losses)
+    assert runs[0] == runs[1], runs
