@@ -221,3 +221,20 @@ def test_bn_training_stop_encoder_grad_point_gradient():
     g_d = _fp64(net, lambda: grads(xyz.double(), vd.double(), w.double(), False))
     assert float(g_h["xyz"].abs().max()) > 0
     _compare64(g_h, g_t, g_d, floor=1e-4)
+
+
+def test_bn_training_512_two_scenes_ragged_lin_z():
+    """d_hidden 512 (the width whose forward layers run bn_layer_kernel<4, 8, FWD, 512>): two scenes, in-kernel lin_z
+    rows (combine_layer 3) and a row count that is not a multiple of 64 -- the forward and every gradient within
+    twice PyTorch fp32's own error against float64. (Round 6 ran the rejected two-half kernels through this case,
+    profiles/r06v_bn_h2_ab.txt.)"""
+    net = _bn_net(512, 3, combine_layer=3, sb=2, hw=(8, 8))
+    xyz, vd, w = _points(2, 333, seed=31)
+    start = _running(net)
+    out_h, g_h, _ = _grads_bn(net, xyz, vd, w, True, hip=True)
+    _set_running(net, start)
+    out_t, g_t, _ = _grads_bn(net, xyz, vd, w, True, hip=False)
+    _set_running(net, start)
+    _, g_d, _ = _fp64(net, lambda: _grads_bn(net, xyz.double(), vd.double(), w.double(), True, hip=False))
+    np.testing.assert_allclose(out_h.cpu().numpy(), out_t.cpu().numpy(), atol=2e-4)
+    _compare64(g_h, g_t, g_d, floor=1e-4)
