@@ -24,7 +24,7 @@ cnt = collections.defaultdict(int)
 import cProfile  # noqa: E402
 import pstats  # noqa: E402
 
-PROF = cProfile.Profile() if os.environ.get("PROFILE_FN") else None   # e.g. PROFILE_FN=FieldTrain.backward
+PROF = cProfile.Profile() if os.environ.get("PROFILE_FN") else None   # e.g. PROFILE_FN=FieldTrain.backward or step_forward
 
 
 def wrap(cls, name):
@@ -62,8 +62,12 @@ phase = collections.defaultdict(float)
 t_all = time.perf_counter()
 for _ in range(steps):
     t0 = time.perf_counter()
+    if PROF is not None and os.environ.get("PROFILE_FN") == "step_forward":   # the main thread's forward + loss
+        PROF.enable()
     rgb_c, rgb_f, _, _ = tp.rend(tp.c2w, tp.K, tp.x_pix, tp.net)
     loss = ((rgb_c - tp.gt) ** 2).mean() + ((rgb_f - tp.gt) ** 2).mean()
+    if PROF is not None and os.environ.get("PROFILE_FN") == "step_forward":
+        PROF.disable()
     t1 = time.perf_counter()
     tp.opt.zero_grad()
     loss.backward()
@@ -83,3 +87,4 @@ for k, v in sorted(acc.items(), key=lambda kv: -kv[1]):
     print(f"  {k:28s} {v / steps * 1e3:8.3f} ms / step ({cnt[k] // steps} calls)")
 if PROF is not None:
     pstats.Stats(PROF).sort_stats("tottime").print_stats(30)
+    pstats.Stats(PROF).sort_stats("cumulative").print_stats(45)
