@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("AVR_LIB_PATH") or os.path.join(_HERE, "libavr_hip.so"
 AVR_MAX_BLOCKS = 8
 AVR_MAX_SCENES = 16
 AVR_LOOKUP_GRAD_TERMS = 8
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -104,6 +104,8 @@ _SIGS = {
     "avr_raymarch_bwd_scratch_bytes": [i64, c_int, i64, ctypes.POINTER(i64)],
     "avr_latent_tables_grad_points": [ctypes.POINTER(ViewDesc), c_int, c_void_p, i64, i64, c_int, c_int, c_void_p, i64,
                                       c_void_p, i64, c_void_p, c_void_p],
+    "avr_zfeature_grad_points": [ctypes.POINTER(ViewDesc), c_int, c_void_p, i64, c_void_p, i64, c_int, ctypes.c_float,
+                                 c_int, c_void_p, c_void_p],
     "avr_raymarch_bwd": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, i64, c_int, c_int, c_void_p, c_void_p, c_void_p, i64, c_void_p],
     "avr_march_state_bytes": [i64, ctypes.POINTER(i64)],
@@ -154,6 +156,7 @@ _SIGS = {
     "avr_lin_out_fwd_rows": [i64, c_int, c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_lin_out_bwd_rows": [i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, c_void_p, c_void_p,
                              c_void_p],
+    "avr_lin_out_act_bwd_rows": [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_spade_bwd_rows": [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_stream_copy": [c_void_p, c_void_p, i64, c_void_p],
     "avr_stream_fill": [c_void_p, i64, c_uint32, c_void_p],

@@ -690,7 +690,7 @@ class _FieldTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
-        from .ops import _max_bits, latent_features, sum_of_products, weight_grads
+        from .ops import latent_features, lin_out_act_bwd, weight_grads
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         fused, entry, names = ctx.fused, ctx.entry, ctx.names
         net = fused.net
@@ -739,21 +739,16 @@ class _FieldTrain(torch.autograd.Function):
                                     hwc=fused.latent_hwc(latent, s))
         lat_max = fused.latent_max_bits(latent)   # |interpolated latent| <= max |latent| (convex blend)
         zf_max = act_max[n_l:n_l + 1]
-        Gz = [G[2 * b - 1] if b > 0 else G[2 * nb] for b in range(nz)]
-        layers = []
-        for b in range(nb):
-            layers.append((G[2 * b], act[2 * b], g_max[2 * b:2 * b + 1], act_max[2 * b:2 * b + 1], True))
-            layers.append((G[2 * b + 1], act[2 * b + 1], g_max[2 * b + 1:2 * b + 2], act_max[2 * b + 1:2 * b + 2], True))
+        # every layer's views in one call each (a slice per layer and operand was ~0.1 ms of host time per call)
+        Gl, Al, gm, am = G.unbind(0), act.unbind(0), g_max.split(1), act_max.split(1)
+        Gz = [Gl[2 * b - 1] if b > 0 else Gl[2 * nb] for b in range(nz)]
+        layers = [(Gl[k], Al[k], gm[k], am[k], True) for k in range(2 * nb)]
         for b in range(nz):
-            gi = 2 * b - 1 if b > 0 else 2 * nb
-            layers.append((Gz[b], lat_feat, g_max[gi:gi + 1], lat_max, False))
-        layers.append((G[2 * nb], zf, g_max[2 * nb:2 * nb + 1], zf_max, True))
-        # lin_out (4 outputs): d out through sigmoid / relu (torch: g * (1 - y) * y, g * (y > 0))
-        y = out.reshape(Mt, 4)
-        go = grad_out.reshape(Mt, 4)
-        d4 = torch.cat([torch.ops.aten.sigmoid_backward(go[:, :3], y[:, :3]),
-                        torch.ops.aten.threshold_backward(go[:, 3:], y[:, 3:], 0.0)], -1).contiguous()
-        layers.append((d4, act[2 * nb], _max_bits(d4), act_max[2 * nb:2 * nb + 1], True))
+            layers.append((Gz[b], lat_feat, gm[2 * b - 1 if b > 0 else 2 * nb], lat_max, False))
+        layers.append((Gl[2 * nb], zf, gm[2 * nb], zf_max, True))
+        # lin_out (4 outputs): d out through sigmoid / relu (torch: g * (1 - y) * y, g * (y > 0)), with its max
+        d4, d4_max = lin_out_act_bwd(grad_out, out)
+        layers.append((d4, Al[2 * nb], d4_max, am[2 * nb], True))
         res = weight_grads(layers, Mt)
         grads = {"lin_out.weight": res[-1][0], "lin_out.bias": res[-1][1]}
         res = res[:-1]
@@ -773,7 +768,7 @@ class _FieldTrain(torch.autograd.Function):
         want_xyz = ctx.needs_input_grad[3]
         if want_xyz and not want_latent and (net.stop_encoder_grad or (nz > 0 and SB <= latent.shape[0])):
             # the points alone (the adaptive renderer's band, fixed latent): the lookup's adjoint on HIP
-            # (avr_latent_features_grad_points), the cheap z_feature path through torch autograd. With
+            # (avr_latent_tables_grad_points / avr_latent_features_grad_points), then z_feature's. With
             # stop_encoder_grad the looked-up latent is detached (models.py:810-811), so no gradient reaches the
             # points through the lookup: z_feature's part alone.
             d_look = None
@@ -806,11 +801,29 @@ class _FieldTrain(torch.autograd.Function):
                             views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
                             call("avr_latent_features_grad_points", views, n, ptr(hwc[g0]), net.d_latent,
                                  ptr(p[g0]), B, ptr(g_feat[g0 * B]), ptr(d_look[g0 * B]), stream_of(d_look))
-            with torch.enable_grad():
-                x = xyz.detach().requires_grad_(True)
-                zft = net.z_features(x, viewdirs.detach())
-                d_z, = torch.autograd.grad(zft, x, G[2 * nb] @ P["lin_in.weight"].detach())
-            d_xyz = (d_z if d_look is None else d_look.reshape(SB, B, 3) + d_z).to(xyz.dtype)
+            # z_feature's part (ABI 16): d loss / d z_feature = G_in W_in (its positional-encoded columns only), then
+            # the encoding's and the rotation's adjoint per point in one launch, added to the lookup's part
+            # (AVR_POINT_ZF_VIA_AUTOGRAD=1: torch autograd of z_features instead, the round-5 path, for A/B)
+            n_pe = 3 + 6 * dims.num_freqs
+            if os.environ.get("AVR_POINT_ZF_VIA_AUTOGRAD") == "1":
+                with torch.enable_grad():
+                    x = xyz.detach().requires_grad_(True)
+                    zft = net.z_features(x, viewdirs.detach())
+                    d_z, = torch.autograd.grad(zft, x, G[2 * nb] @ P["lin_in.weight"].detach())
+                d_xyz = (d_z if d_look is None else d_look.reshape(SB, B, 3) + d_z).to(xyz.dtype)
+            else:
+                with torch.no_grad():
+                    d_zf = G[2 * nb] @ P["lin_in.weight"].detach()[:, :n_pe]
+                    if d_look is None:
+                        d_look = torch.empty(Mt, 3, device=dev, dtype=F32)
+                        p = xyz.detach().to(F32).contiguous()
+                    for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
+                        n = min(_lib.AVR_MAX_SCENES, SB - g0)
+                        views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+                        call("avr_zfeature_grad_points", views, n, ptr(p[g0]), B, ptr(d_zf[g0 * B]), d_zf.stride(0),
+                             dims.num_freqs, dims.freq_factor, int(not net.stop_encoder_grad), ptr(d_look[g0 * B]),
+                             stream_of(d_look))
+                d_xyz = d_look.reshape(SB, B, 3).to(xyz.dtype)
         elif want_latent or want_xyz:
             with torch.enable_grad():
                 lat = latent.detach().requires_grad_(want_latent)

@@ -405,6 +405,18 @@ def lin_out_rows_bwd(grad_out, out, weight, pre, g=None):
     return d_raw, g, dmax
 
 
+def lin_out_act_bwd(grad_out, out):
+    """The activations' backward of lin_out's outputs alone: (d_raw (n, 4) = [sigmoid_backward rgb,
+    threshold_backward sigma], max |d_raw| as int32 float bits) (avr_lin_out_act_bwd_rows; torch's
+    sigmoid_backward / threshold_backward bit for bit), over contiguous (..., 4) fp32 grad_out / out."""
+    go, y = _f32c(grad_out.reshape(-1, 4)), _f32c(out.reshape(-1, 4))
+    n = go.shape[0]
+    d_raw = torch.empty(n, 4, device=go.device, dtype=F32)
+    dmax = torch.zeros(1, device=go.device, dtype=torch.int32)
+    call("avr_lin_out_act_bwd_rows", n, ptr(go), ptr(y), ptr(d_raw), ptr(dmax), stream_of(go))
+    return d_raw, dmax
+
+
 def spade_bwd_rows(g, x, s):
     """The spade product rule's backward (avr_spade_bwd_rows): (g * x, s * g, max |g * x| as int32 float bits) in
     one pass over contiguous fp32 tensors of one shape, bit-identical to torch's two products."""

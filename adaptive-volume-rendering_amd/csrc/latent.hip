@@ -182,6 +182,37 @@ __global__ void __launch_bounds__(256) latent_features_grad_points_kernel(LatBat
   }
 }
 
+// z_feature's position adjoint for the fused family (models.py:753-794 with PositionalEncoding :41-87): z = R x
+// (normalize_z), zf = [z, sin(f_k z + 0), sin(f_k z + pi/2) for k < F (3 each), R d]; given g = d loss / d zf's
+// first 3 + 6F columns, d z_c = g_c + sum_j f_j cos(phase_j + f_j z_c) g[3 + 3j + c] (j < 2F, f_j = f_(j/2) =
+// freq_factor 2^(j/2)) and d x = R^T d z -- torch autograd's chain (sin', addcmul', bmm') in one thread per point.
+__global__ void __launch_bounds__(256) zfeature_grad_points_kernel(LatBatch vb, const float* __restrict__ xyz,
+                                                                   int64_t n_points, const float* __restrict__ g,
+                                                                   int64_t ldg, int F, float freq_factor,
+                                                                   int accumulate, float* __restrict__ gxyz) {
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= n_points) return;
+  const int s = blockIdx.y;
+  const View& v = vb.v[s];
+  const int64_t row = s * n_points + m;
+  const float x0 = xyz[3 * row], x1 = xyz[3 * row + 1], x2 = xyz[3 * row + 2];
+  const float z[3] = {dot3(v.R + 0, x0, x1, x2), dot3(v.R + 3, x0, x1, x2), dot3(v.R + 6, x0, x1, x2)};
+  const float* gr = g + row * ldg;
+  float dz[3] = {gr[0], gr[1], gr[2]};
+  constexpr float kHalfPi = 1.57079632679489662f;
+  for (int j = 0; j < 2 * F; ++j) {
+    const float f = ldexpf(freq_factor, j >> 1);   // freq_factor * 2^k exactly (models.py:45, fp32)
+    const float ph = (j & 1) ? kHalfPi : 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dz[c] += gr[3 + 3 * j + c] * cosf(ph + z[c] * f) * f;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float d = v.R[k] * dz[0] + v.R[3 + k] * dz[1] + v.R[6 + k] * dz[2];
+    gxyz[3 * row + k] = accumulate ? gxyz[3 * row + k] + d : d;
+  }
+}
+
 }  // namespace avr
 
 static int lookup_views(const avr_view_desc* views, int n_scenes, LatBatch* vb, const char* what) {
@@ -246,4 +277,21 @@ extern "C" int avr_latent_tables_grad_points(const avr_view_desc* views, int n_s
   latent_features_grad_points_kernel<<<dim3((unsigned)((n_points + 3) / 4), (unsigned)n_scenes), 256, 0,
                                        as_stream(stream)>>>(vb, T, channels, xyz, n_points, grad_xyz);
   return check_launch("latent_features_grad_points_kernel");
+}
+
+extern "C" int avr_zfeature_grad_points(const avr_view_desc* views, int n_scenes, const float* xyz, int64_t n_points,
+                                        const float* grad_zf, int64_t ld_grad, int num_freqs, float freq_factor,
+                                        int accumulate, float* grad_xyz, void* stream) {
+  AVR_REQUIRE(n_scenes >= 1 && n_scenes <= AVR_MAX_SCENES, "avr_zfeature_grad_points: 1..%d scenes per call",
+              AVR_MAX_SCENES);
+  AVR_REQUIRE(n_points >= 0 && num_freqs >= 0 && num_freqs <= 32 && ld_grad >= 3 + 6 * num_freqs,
+              "avr_zfeature_grad_points: bad sizes");
+  if (n_points == 0) return AVR_OK;
+  AVR_REQUIRE(views && xyz && grad_zf && grad_xyz, "avr_zfeature_grad_points: null pointer");
+  LatBatch vb;
+  for (int s = 0; s < n_scenes; ++s) view_from_desc(&views[s], &vb.v[s]);   // only R is read
+  avr::zfeature_grad_points_kernel<<<dim3((unsigned)((n_points + 255) / 256), (unsigned)n_scenes), 256, 0,
+                                     as_stream(stream)>>>(vb, xyz, n_points, grad_zf, ld_grad, num_freqs, freq_factor,
+                                                          accumulate ? 1 : 0, grad_xyz);
+  return check_launch("zfeature_grad_points_kernel");
 }

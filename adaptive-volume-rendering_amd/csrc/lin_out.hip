@@ -140,6 +140,29 @@ __global__ void __launch_bounds__(kLinOutThreads) lin_out_bwd_rows_kernel(
   }
 }
 
+// The activations' backward alone (the fused training path, whose chain kernel applies lin_out^T itself): d_raw
+// = [sigmoid_backward(go, y) rgb, threshold_backward(go, y, 0) sigma] per row as lin_out_bwd_rows_kernel computes
+// it, and max |d_raw| (the weight gradient's scale input). One thread per row.
+__global__ void __launch_bounds__(256) lin_out_act_bwd_kernel(int64_t M, const float* __restrict__ gout,
+                                                              const float* __restrict__ y, float* __restrict__ draw,
+                                                              unsigned* dmax) {
+  const int lane = threadIdx.x & 63;
+  float m = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < M; row += (int64_t)gridDim.x * 256) {
+    const floatx4 go = ld4g(gout + 4 * row), yv = ld4g(y + 4 * row);
+    floatx4 d;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d[k] = fmul(fmul(go[k], fsub(1.f, yv[k])), yv[k]);
+    d[3] = yv[3] > 0.f ? go[3] : 0.f;
+    *reinterpret_cast<floatx4*>(draw + 4 * row) = d;
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
+  }
+  if (dmax) {
+    m = max64(m, lane);
+    if (lane == 0) publish_max(dmax, m);
+  }
+}
+
 // rows per lane group per pass: the forward one, the backward two (scripts/lin_out_bench.py at 131 072 / 98 304
 // rows: forward 54 / 45 us with one row, 56 / 49 with two; backward 91 / 78 with one, 88 / 66 with two);
 // AVR_LIN_OUT_RR=1|2 sets both (A/B)
@@ -209,4 +232,17 @@ extern "C" int avr_lin_out_bwd_rows(int64_t n_rows, int d_hidden, const float* g
   const int H = d_hidden;
   AVR_LIN_OUT_DISPATCH(2, lin_out_bwd_rows_kernel, n_rows, grad_out, out, weight, pre, ld_pre, d_raw, g, d_raw_max)
   return check_launch("lin_out_bwd_rows_kernel");
+}
+
+extern "C" int avr_lin_out_act_bwd_rows(int64_t n_rows, const float* grad_out, const float* out, float* d_raw,
+                                        uint32_t* d_raw_max, void* stream) {
+  AVR_REQUIRE(n_rows >= 0, "avr_lin_out_act_bwd_rows: n_rows %lld", (long long)n_rows);
+  if (n_rows == 0) return AVR_OK;
+  AVR_REQUIRE(grad_out && out && d_raw, "avr_lin_out_act_bwd_rows: null pointer");
+  AVR_REQUIRE(aligned16(grad_out) && aligned16(out) && aligned16(d_raw),
+              "avr_lin_out_act_bwd_rows: 16-B aligned tensors");
+  const int64_t blocks = (n_rows + 255) / 256;
+  lin_out_act_bwd_kernel<<<(unsigned)(blocks < 2048 ? blocks : 2048), 256, 0, as_stream(stream)>>>(
+      n_rows, grad_out, out, d_raw, d_raw_max);
+  return check_launch("lin_out_act_bwd_kernel");
 }

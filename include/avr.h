@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 15
+#define AVR_ABI_VERSION 16
 #define AVR_MAX_BLOCKS 8
 #define AVR_LOOKUP_GRAD_TERMS 8   /* tables per avr_latent_tables_grad_points call */
 #define AVR_MAX_SCENES 16   /* scenes per training-forward launch */
@@ -450,6 +450,10 @@ int avr_lin_out_fwd_rows(int64_t n_rows, int d_hidden, const float* x, int64_t l
                          const float* bias, float* out, uint32_t* x_max, void* stream);
 int avr_lin_out_bwd_rows(int64_t n_rows, int d_hidden, const float* grad_out, const float* out, const float* weight,
                          const float* pre, int64_t ld_pre, float* d_raw, float* g, uint32_t* d_raw_max, void* stream);
+/* ABI 16: the activations' backward alone, d_raw (n_rows, 4) and d_raw_max as avr_lin_out_bwd_rows computes them
+ * (no lin_out^T: the fused training path's chain kernel applies it); 16-B aligned (n_rows, 4) rows. */
+int avr_lin_out_act_bwd_rows(int64_t n_rows, const float* grad_out, const float* out, float* d_raw,
+                             uint32_t* d_raw_max, void* stream);
 
 /* Latent features at points — SpatialEncoder.index (models.py:245-274) as
  * NewPixelNeRFNet.forward uses it (models.py:753-810): bilinear / border /
@@ -483,6 +487,14 @@ int avr_latent_tables_grad_points(const avr_view_desc* views, int n_scenes, cons
                                   int64_t table_scene_stride, int64_t table_stride, int n_tables, int channels,
                                   const float* xyz, int64_t n_points, const float* const* grads, int64_t ld_grad,
                                   float* grad_xyz, void* stream);
+/* ABI 16: the position gradient through z_feature for the fused family (use_xyz, normalize_z, PositionalEncoding
+ * with include_input on z = R xyz, raw view directions after it; models.py:753-794, :41-87): grad_zf (n_scenes *
+ * n_points rows of ld_grad >= 3 + 6 num_freqs) = d loss / d z_feature's first 3 + 6 num_freqs columns; grad_xyz
+ * (n_scenes * n_points, 3) = R_s^T d loss / d z, written (accumulate = 0) or added to (accumulate = 1: after the
+ * lookup's gradient). Replaces the torch autograd of z_feature for the adaptive renderer's band points.        */
+int avr_zfeature_grad_points(const avr_view_desc* views, int n_scenes, const float* xyz, int64_t n_points,
+                             const float* grad_zf, int64_t ld_grad, int num_freqs, float freq_factor, int accumulate,
+                             float* grad_xyz, void* stream);
 
 /* --------------------------------------------------------- LSTM ray marcher
  * Raymarcher / AdaptiveVolumeRenderer march (renderers.py:313-351, :380-432):

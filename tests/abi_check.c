@@ -185,6 +185,17 @@ int main(void) {
   expect("latent_grad_points null", avr_latent_features_grad_points(&v, 1, buf, 4, buf, 3, NULL, buf, NULL),
          AVR_E_INVALID);
   expect("latent_grad_points empty", avr_latent_features_grad_points(&v, 1, buf, 4, buf, 0, buf, buf, NULL), AVR_OK);
+  expect("zfeature_grad_points scenes", avr_zfeature_grad_points(&v, 0, buf, 3, buf, 39, 6, 3.14159f, 0, buf, NULL),
+         AVR_E_INVALID);
+  expect("zfeature_grad_points ld", avr_zfeature_grad_points(&v, 1, buf, 3, buf, 38, 6, 3.14159f, 0, buf, NULL),
+         AVR_E_INVALID);
+  expect("zfeature_grad_points null", avr_zfeature_grad_points(&v, 1, buf, 3, NULL, 39, 6, 3.14159f, 1, buf, NULL),
+         AVR_E_INVALID);
+  expect("lin_out_act_bwd null", avr_lin_out_act_bwd_rows(4, buf, NULL, buf, NULL, NULL), AVR_E_INVALID);
+  expect("lin_out_act_bwd rows", avr_lin_out_act_bwd_rows(-1, buf, buf, buf, NULL, NULL), AVR_E_INVALID);
+  expect("lin_out_act_bwd empty", avr_lin_out_act_bwd_rows(0, NULL, NULL, NULL, NULL, NULL), AVR_OK);
+  expect("zfeature_grad_points empty", avr_zfeature_grad_points(&v, 1, buf, 0, buf, 39, 6, 3.14159f, 0, buf, NULL),
+         AVR_OK);
   expect("latent_table_batch null", avr_field_latent_table_batch(&d, NULL, NULL, 2, 8, 8, NULL, NULL), AVR_E_INVALID);
   expect("latent_table_batch no scenes", avr_field_latent_table_batch(&d, buf, buf, 0, 8, 8, buf, NULL),
          AVR_E_INVALID);

@@ -74,6 +74,25 @@ def test_lin_out_rows_argument_checks():
     assert b(4, 256, None, None, None, None, 256, None, None, None, None) == 1001
 
 
+def test_round6_point_gradient_entry_points_argument_checks():
+    """avr_lin_out_act_bwd_rows and avr_zfeature_grad_points (ABI 16): zero rows is a no-op; null pointers, a scene
+    count outside 1..AVR_MAX_SCENES and gradient rows shorter than 3 + 6 num_freqs are refused before any HIP call."""
+    import ctypes
+    from avr import _lib
+    lib = _lib.load()
+    assert lib.avr_lin_out_act_bwd_rows(0, None, None, None, None, None) == 0
+    assert lib.avr_lin_out_act_bwd_rows(4, None, None, None, None, None) == 1001
+    assert b"null" in lib.avr_last_error_string()
+    v = (_lib.ViewDesc * 1)()
+    z = lib.avr_zfeature_grad_points
+    assert z(v, 1, None, 0, None, 39, 6, ctypes.c_float(3.14159), 0, None, None) == 0
+    assert z(v, 0, None, 3, None, 39, 6, ctypes.c_float(3.14159), 0, None, None) == 1001
+    assert z(v, 1, None, 3, None, 38, 6, ctypes.c_float(3.14159), 0, None, None) == 1001
+    assert b"bad sizes" in lib.avr_last_error_string()
+    assert z(v, 1, None, 3, None, 39, 6, ctypes.c_float(3.14159), 0, None, None) == 1001
+    assert b"null" in lib.avr_last_error_string()
+
+
 def test_spade_bwd_rows_argument_checks():
     """avr_spade_bwd_rows (ABI 14): zero values is a no-op; a count not a multiple of 4 and null pointers are
     refused before any HIP call."""

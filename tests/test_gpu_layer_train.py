@@ -209,7 +209,8 @@ def test_layer_train_stop_encoder_grad_point_gradient(case):
 
 @pytest.mark.parametrize("H,n,pad", [(64, 1, 0), (192, 5, 4), (512, 1003, 0), (512, 40000, 8)])
 def test_lin_out_rows_vs_fp64(H, n, pad):
-    """avr_lin_out_fwd_rows / avr_lin_out_bwd_rows (the layer-by-layer paths' output layer) against float64 torch:
+    """avr_lin_out_fwd_rows / avr_lin_out_bwd_rows (the layer-by-layer paths' output layer; and
+    avr_lin_out_act_bwd_rows, the activations' backward alone) against float64 torch:
     out and g within 1e-5 of their scale, d_raw bit-equal to torch's own activation backward kernels
     (aten sigmoid_backward / threshold_backward), g exactly 0 where pre <= 0, both maxima exact; rows with a leading dimension past d_hidden."""
     from avr import ops
@@ -233,6 +234,9 @@ def test_lin_out_rows_vs_fp64(H, n, pad):
     g_ref = (d4.double() @ W.double()) * (x > 0)
     assert float((gr.double() - g_ref).abs().max()) <= 1e-5 * max(float(g_ref.abs().max()), 1e-30)
     assert bool((gr[x <= 0] == 0).all())
+    # the activations' backward alone (ABI 16, the fused training path's d4): the same d_raw and max
+    d4b, dmaxb = ops.lin_out_act_bwd(go, out)
+    assert torch.equal(d4b, d4_ref) and int(dmaxb) == int(dmax)
 
 
 @pytest.mark.parametrize("H,nb,cl,M", [(64, 3, 2, 333), (256, 3, 3, 64), (512, 5, 3, 1000)])

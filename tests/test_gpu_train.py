@@ -404,11 +404,60 @@ def test_latent_tables_grad_points_vs_fp64(n_tables):
     print(f"tables grad points ({n_tables}): HIP err {eh / s:.2e}, torch fp32 err {et / s:.2e} of max {s:.3e}")
 
 
-@pytest.mark.parametrize("via", ["tables", "features"])
+@pytest.mark.parametrize("accumulate", [0, 1])
+def test_zfeature_grad_points_vs_fp64(accumulate):
+    """avr_zfeature_grad_points (ABI 16): the points' gradient through z_feature (rotation, positional encoding
+    with include_input; models.py:753-794, :41-87) given d loss / d z_feature's encoded columns, against float64
+    autograd of the module's z_features; two scenes with different poses, points far outside the unit cube (large
+    f_k z), rows with a leading dimension past 3 + 6F; accumulate=1 adds to what grad_xyz holds."""
+    from avr import _lib
+    from avr._lib import ViewDesc
+    net = _net(64, 2, 64, (8, 8), sb=2)
+    M = 600
+    xyz, vd, _ = _points(2, M, seed=29)
+    xyz = xyz * torch.where(torch.arange(M, device=DEV) % 4 == 0, 5.0, 1.0).reshape(1, M, 1)
+    F = net.code.num_freqs
+    n_pe = 3 + 6 * F
+    g = torch.Generator().manual_seed(8)
+    ld = net.d_in + 5
+    gbuf = torch.randn(2 * M, ld, generator=g).to(DEV)
+    gzf = gbuf[:, :net.d_in]                                     # the viewdir columns carry no position gradient
+    base = torch.randn(2 * M, 3, generator=g).to(DEV)
+    got = base.clone()
+    fused = net.fused()
+    views = (ViewDesc * 2)(*[fused.view(sb) for sb in range(2)])
+    _lib.call("avr_zfeature_grad_points", views, 2, _lib.ptr(xyz.contiguous()), M, _lib.ptr(gbuf), ld, F,
+              fused.dims(net.mlp_coarse).freq_factor, accumulate, _lib.ptr(got), _lib.stream_of(got))
+    if accumulate:
+        got = got - base
+
+    def autograd(dtype):
+        x = xyz.to(dtype).clone().requires_grad_(True)
+        zf = net.z_features(x, vd.to(dtype))
+        return torch.autograd.grad(zf, x, gzf.to(dtype))[0].reshape(-1, 3)
+
+    ref32 = autograd(torch.float32)
+    with torch.no_grad():
+        net.double()
+    try:
+        ref64 = autograd(torch.float64)
+    finally:
+        net.float()
+    s = float(ref64.abs().max())
+    eh = float((got.double() - ref64).abs().max())
+    et = float((ref32.double() - ref64).abs().max())
+    assert n_pe + 3 == net.d_in and eh <= 2.0 * et + 1e-6 * s, (eh, et, s)
+    print(f"z_feature grad points: HIP err {eh / s:.2e}, torch fp32 err {et / s:.2e} of max {s:.3e}")
+
+
+@pytest.mark.parametrize("via", ["tables", "features", "zf_autograd"])
 def test_field_train_point_gradient_paths(via, monkeypatch):
     """The band points' lookup gradient on the fused training path both ways (ABI 15's tables path, the default,
-    and the feature-gradient path it replaced, AVR_POINT_GRAD_VIA_FEATURES=1) against float64 autograd."""
+    and the feature-gradient path it replaced, AVR_POINT_GRAD_VIA_FEATURES=1), and z_feature's part both ways (ABI
+    16's avr_zfeature_grad_points, the default, and torch autograd, AVR_POINT_ZF_VIA_AUTOGRAD=1), against float64
+    autograd."""
     monkeypatch.setenv("AVR_POINT_GRAD_VIA_FEATURES", "1" if via == "features" else "0")
+    monkeypatch.setenv("AVR_POINT_ZF_VIA_AUTOGRAD", "1" if via == "zf_autograd" else "0")
     net = _net(512, 5, 512, (16, 16), 3)
     xyz0, vd, w = _points(1, 700, seed=19)
     res = {}
