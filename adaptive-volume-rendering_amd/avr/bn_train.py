@@ -22,7 +22,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import BnLayer, ViewDesc, call, ptr, stream_of
+from ._lib import BnLayer, call, ptr, stream_of
 
 F32 = torch.float32
 
@@ -158,7 +158,7 @@ class _FieldTrainBN(torch.autograd.Function):
             zfp[:, :d_in] = zf
             # lin_z[b](latent features) rows: gathered from the per-texel tables in the layer epilogues
             tables = fused.tables_batch(coarse, SB, fast=True, bn_fold=False)
-            views = (ViewDesc * SB)(*[fused.view(s) for s in range(SB)])
+            views = fused.views(range(SB))
             p = xyz.detach().to(F32).contiguous()
 
             def lin_z(b):

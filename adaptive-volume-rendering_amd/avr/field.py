@@ -240,6 +240,7 @@ class FusedField:
         self.net = net
         self._packed = {}     # coarse(bool) -> (key, _Packed)
         self._view_cache = {}
+        self._views_cache = {}    # (range, ns) -> ViewDesc arrays (views())
         self._latent_cache = {}   # per latent version: channels-last copies, max |latent| (both MLPs share them)
         # mlp (weakly) -> ([(name, owner dict, key)] params, [...] float buffers, generation, ids of its modules)
         self._slots = weakref.WeakKeyDictionary()
@@ -252,6 +253,7 @@ class FusedField:
         self._packed.clear()
         if views:
             self._view_cache.clear()
+            self._views_cache.clear()
         self._latent_cache.clear()
 
     def cache_tensors(self):
@@ -355,7 +357,8 @@ class FusedField:
         keep = []
 
         def P(t):
-            t = t.detach().to(F32).contiguous()
+            if not (t.dtype == F32 and t.is_contiguous()):   # (fp32 contiguous parameters: read in place)
+                t = t.detach().to(F32).contiguous()
             keep.append(t)
             return t.data_ptr()
 
@@ -473,6 +476,20 @@ class FusedField:
         self._view_cache[(sb, ns)] = (key, v, srcs)  # holding the sources keeps (ptr, version) keys sound
         return v
 
+    def views(self, idx, ns=1):
+        """The ViewDesc array of view(i, ns) for i in the range idx (the multi-scene launches' argument), cached
+        under one source-version key (per-view keys for every scene of every launch were host time)."""
+        net = self.net
+        srcs = [net.poses, net.focal, net.c, net.image_shape, net.encoder.latent_scaling]
+        slot = (idx.start, idx.stop, idx.step, ns)
+        key = (_version_key(srcs, gen=False), tuple(net.encoder.latent.shape))
+        hit = self._views_cache.get(slot)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        arr = (ViewDesc * len(idx))(*[self.view(i, ns) for i in idx])
+        self._views_cache[slot] = (key, arr, srcs)   # holding the sources keeps (ptr, version) keys sound
+        return arr
+
     # ----------------------------------------------------------- evaluation
     def forward_rays(self, ro, rd, z, coarse, sb=0):
         """sigma/RGB at ro[r] + rd[r]*z[r,s] with viewdir rd[r]: (R*N, 4)."""
@@ -508,7 +525,7 @@ class FusedField:
         entry.dims.precision = _lib.FIELD_X3
         for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
             n = min(_lib.AVR_MAX_SCENES, SB - g0)
-            views = (ViewDesc * n)(*[self.view(sb) for sb in range(g0, g0 + n)])
+            views = self.views(range(g0, g0 + n))
             call("avr_field_fwd_rays_batch", ctypes.byref(entry.dims), views, n, ptr(entry.packed), ptr(tables[g0]),
                  ptr(ro[g0]), ptr(rd[g0]), ptr(z[g0 * R]), R, N, ptr(out[g0 * R * N]), stream_of(z))
         return out
@@ -538,13 +555,13 @@ class FusedField:
         with _precision(dims, _lib.FIELD_X3):
             for g0 in range(0, K, _lib.AVR_MAX_SCENES):
                 n = min(_lib.AVR_MAX_SCENES, K - g0)
-                views = (ViewDesc * n)(*[self.view(k, NS) for k in range(g0, g0 + n)])
+                views = self.views(range(g0, g0 + n), NS)
                 call("avr_field_fwd_points_split", ctypes.byref(entry.dims), views, n, ptr(entry.packed),
                      ptr(tables[g0]), ptr(p[g0]), ptr(v[g0]), B, 0, cl, None, ptr(h[g0 * B]), None, stream_of(p))
             hc = combine_interleaved(h, (NS, B), mlp.combine_type).reshape(SB * B, H).contiguous()
             for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
                 n = min(_lib.AVR_MAX_SCENES, SB - g0)
-                views = (ViewDesc * n)(*[self.view(s * NS, NS) for s in range(g0, g0 + n)])
+                views = self.views(range(g0 * NS, (g0 + n) * NS, NS), NS)
                 call("avr_field_fwd_points_split", ctypes.byref(entry.dims), views, n, ptr(entry.packed),
                      ptr(tables[0]), None, None, B, cl, nb, ptr(hc[g0 * B]), None, ptr(out[g0]), stream_of(p))
         return out
@@ -569,7 +586,7 @@ class FusedField:
             entry.dims.precision = _lib.FIELD_X3
             for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
                 n = min(_lib.AVR_MAX_SCENES, SB - g0)
-                views = (ViewDesc * n)(*[self.view(sb) for sb in range(g0, g0 + n)])
+                views = self.views(range(g0, g0 + n))
                 call("avr_field_fwd_points_batch", ctypes.byref(entry.dims), views, n, ptr(entry.packed),
                      ptr(tables[g0]), ptr(p[g0]), ptr(v[g0]), B, ptr(out[g0]), stream_of(p))
             return out
@@ -674,7 +691,7 @@ class _FieldTrain(torch.autograd.Function):
             act_n, mask_n = ctypes.c_int64(0), ctypes.c_int64(0)
             _lib.check(_lib.load().avr_field_train_sizes(ctypes.byref(dims), n, B, ctypes.byref(act_n),
                                                          ctypes.byref(mask_n)), "avr_field_train_sizes")
-            views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+            views = fused.views(range(g0, g0 + n))
             mask = torch.empty(max(mask_n.value, 1), device=dev, dtype=torch.int32)
             call("avr_field_fwd_points_train", ctypes.byref(dims), views, n, ptr(entry.packed), ptr(tables[g0]),
                  ptr(p[g0]), ptr(v[g0]), B, ptr(out[g0]), ctypes.c_void_p(act.data_ptr() + g0 * B * H * 4), Mt,
@@ -729,7 +746,7 @@ class _FieldTrain(torch.autograd.Function):
                 p = xyz.detach().to(F32).contiguous()
                 for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
                     n = min(_lib.AVR_MAX_SCENES, SB - g0)
-                    views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+                    views = fused.views(range(g0, g0 + n))
                     call("avr_latent_features_batch", views, n, ptr(hwc[g0]), net.d_latent, ptr(p[g0]), B,
                          ptr(lat_feat[g0 * B]), stream_of(lat_feat))
             else:
@@ -788,7 +805,7 @@ class _FieldTrain(torch.autograd.Function):
                         gptr = [g.data_ptr() for g in Gz]
                         for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
                             n = min(_lib.AVR_MAX_SCENES, SB - g0)
-                            views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+                            views = fused.views(range(g0, g0 + n))
                             gr = (ctypes.c_void_p * nz)(*[g + g0 * B * ld * 4 for g in gptr])
                             call("avr_latent_tables_grad_points", views, n, ptr(tabs[g0]), tabs.stride(0),
                                  tabs.stride(1), nz, H, ptr(p[g0]), B, gr, ld, ptr(d_look[g0 * B]),
@@ -798,7 +815,7 @@ class _FieldTrain(torch.autograd.Function):
                         hwc = fused.latent_hwc_all(latent)
                         for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
                             n = min(_lib.AVR_MAX_SCENES, SB - g0)
-                            views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+                            views = fused.views(range(g0, g0 + n))
                             call("avr_latent_features_grad_points", views, n, ptr(hwc[g0]), net.d_latent,
                                  ptr(p[g0]), B, ptr(g_feat[g0 * B]), ptr(d_look[g0 * B]), stream_of(d_look))
             # z_feature's part (ABI 16): d loss / d z_feature = G_in W_in (its positional-encoded columns only), then
@@ -819,7 +836,7 @@ class _FieldTrain(torch.autograd.Function):
                         p = xyz.detach().to(F32).contiguous()
                     for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
                         n = min(_lib.AVR_MAX_SCENES, SB - g0)
-                        views = (ViewDesc * n)(*[fused.view(sb) for sb in range(g0, g0 + n)])
+                        views = fused.views(range(g0, g0 + n))
                         call("avr_zfeature_grad_points", views, n, ptr(p[g0]), B, ptr(d_zf[g0 * B]), d_zf.stride(0),
                              dims.num_freqs, dims.freq_factor, int(not net.stop_encoder_grad), ptr(d_look[g0 * B]),
                              stream_of(d_look))

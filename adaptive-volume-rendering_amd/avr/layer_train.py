@@ -26,7 +26,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import ViewDesc, call, ptr, stream_of
+from ._lib import call, ptr, stream_of
 
 F32 = torch.float32
 
@@ -74,7 +74,7 @@ def _gather(fused, tab, K, NS, p, B, C):
     out = torch.empty(K * B, C, device=p.device, dtype=F32)
     for g0 in range(0, K, _lib.AVR_MAX_SCENES):
         n = min(_lib.AVR_MAX_SCENES, K - g0)
-        views = (ViewDesc * n)(*[fused.view(k, NS) for k in range(g0, g0 + n)])
+        views = fused.views(range(g0, g0 + n), NS)
         call("avr_latent_features_batch", views, n, ptr(tab[g0]), C, ptr(p[g0]), B, ptr(out[g0 * B]),
              stream_of(out))
     return out
@@ -123,7 +123,7 @@ class _FieldTrainLayers(torch.autograd.Function):
             # (avr_bn_layer's lin_z_table, as avr.bn_train; nz <= combine_layer, so X[b] is X'[b] and no T row is
             # stored); use_spade's product, or more scenes than one launch takes, gathers them here
             zk = not spade and 0 < nz and K <= _lib.AVR_MAX_SCENES
-            views = (ViewDesc * K)(*[fused.view(k, NS) for k in range(K)]) if zk else None
+            views = fused.views(range(K), NS) if zk else None
 
             def lin_z(b):
                 if not zk or b >= nz:

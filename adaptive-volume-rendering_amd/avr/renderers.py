@@ -411,7 +411,7 @@ class _MarchTrain(torch.autograd.Function):
             world = torch.empty(n, 3, device=dev, dtype=torch.float32)
             trace = torch.empty(steps + 1, n, 3, device=dev, dtype=torch.float32)
             state = torch.empty(max(steps, 1), n, 96, device=dev, dtype=torch.float32)
-            views = (_lib.ViewDesc * SB)(*[fused.view(s) for s in range(SB)])
+            views = fused.views(range(SB))
             P = [t.detach().float().contiguous() for t in (w_hh, b_ih, b_hh, w_out, b_out)]
             ro = ros.detach().float().reshape(n, 3).contiguous()
             rd = rds.detach().float().reshape(n, 3).contiguous()
