@@ -475,6 +475,9 @@ def weight_grads(layers, n_rows, n_split=None):
         sizes = [n_split * l[0].shape[1] * (l[1].shape[1] + (1 if l[4] else 0)) for l in chunk]
         flat = torch.empty(sum(sizes), device=dev, dtype=torch.float32)
         dw_ptrs, db_ptrs = (ctypes.c_void_p * len(chunk))(), (ctypes.c_void_p * len(chunk))()
+        # every dW / db of the chunk as views of one allocation (two allocations per layer were host time)
+        osz = [l[0].shape[1] * l[1].shape[1] + (l[0].shape[1] if l[4] else 0) for l in chunk]
+        outs = torch.empty(sum(osz), device=dev, dtype=torch.float32).split(osz)
         res, off = [], 0
         for k, (g, x, gmax, xmax, want_bias, *bn) in enumerate(chunk):
             O, I = g.shape[1], x.shape[1]
@@ -495,8 +498,8 @@ def weight_grads(layers, n_rows, n_split=None):
             arr[k] = _lib.WGradLayer(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), O, I, gmax.data_ptr(),
                                      xmax.data_ptr(), part.data_ptr(), 0 if bpart is None else bpart.data_ptr(),
                                      *([t.data_ptr() for t in bn] if bn is not None else [None] * 3), int(relu))
-            dw = torch.empty(O, I, device=dev, dtype=torch.float32)
-            db = torch.empty(O, device=dev, dtype=torch.float32) if want_bias else None
+            dw = outs[k][:O * I].view(O, I)
+            db = outs[k][O * I:] if want_bias else None
             dw_ptrs[k], db_ptrs[k] = dw.data_ptr(), (db.data_ptr() if want_bias else None)
             res.append((dw, db))
         call("avr_weight_grads", arr, len(chunk), n_rows, n_split, stream)
