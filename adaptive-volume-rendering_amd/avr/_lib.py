@@ -104,6 +104,8 @@ _SIGS = {
     "avr_raymarch_bwd_scratch_bytes": [i64, c_int, i64, ctypes.POINTER(i64)],
     "avr_latent_tables_grad_points": [ctypes.POINTER(ViewDesc), c_int, c_void_p, i64, i64, c_int, c_int, c_void_p, i64,
                                       c_void_p, i64, c_void_p, c_void_p],
+    "avr_band_fwd": [i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, c_void_p, c_void_p, c_void_p],
+    "avr_band_bwd": [i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "avr_zfeature_grad_points": [ctypes.POINTER(ViewDesc), c_int, c_void_p, i64, c_void_p, i64, c_int, ctypes.c_float,
                                  c_int, c_void_p, c_void_p],
     "avr_raymarch_bwd": [ctypes.POINTER(ViewDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

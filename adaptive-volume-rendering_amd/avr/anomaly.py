@@ -75,7 +75,8 @@ OPS = ("world_rays", "rays_sample_coarse", "composite_depth", "depth_from_world_
        "weight_grads", "latent_features")
 FIELD_METHODS = ("forward_rays", "forward_rays_batch", "forward_points_multiview", "forward_points", "forward_train")
 FUNCTIONS = (("ops", "_Depth"), ("ops", "_Composite"), ("ops", "_DepthOfPoints"), ("field", "_FieldTrain"),
-             ("bn_train", "_FieldTrainBN"), ("renderers", "_MarchTrain"))
+             ("bn_train", "_FieldTrainBN"), ("renderers", "_MarchTrain"),
+             ("renderers", "_Band"))
 
 
 def install():

@@ -388,6 +388,43 @@ class _LSTMMarch(nn.Module):
         return world_coords[-1]
 
 
+class _Band(torch.autograd.Function):
+    """AdaptiveVolumeRenderer's band in training on HIP (renderers.py:490-508): from the marched points, z =
+    sample_coarse(d - eps, d + eps) per ray (d = (world - ro)_x / rd_x, quirk kept) sorted, and the band points ro +
+    rd z, in one launch (avr_band_fwd, bit-identical to the torch operations it replaces); backward avr_band_bwd
+    (dz / dd = 1 per sample: d loss / d world_x = sum (gz + gpts . rd) / rd_x). ros / rds must not need gradients."""
+
+    @staticmethod
+    def forward(ctx, world, ros, rds, noise, eps, n):
+        SB, R, _ = world.shape
+        with torch.no_grad():
+            w, ro, rd = (t.detach().float().reshape(SB * R, 3).contiguous() for t in (world, ros, rds))
+            u = noise.detach().float().reshape(SB * R, n).contiguous()
+            z = torch.empty(SB, R, n, device=w.device, dtype=torch.float32)
+            pts = torch.empty(SB * R * n, 3, device=w.device, dtype=torch.float32)
+            _lib.call("avr_band_fwd", SB * R, n, _lib.ptr(w), _lib.ptr(ro), _lib.ptr(rd), _lib.ptr(u), float(eps),
+                      _lib.ptr(z), _lib.ptr(pts), _lib.stream_of(w))
+        ctx.n, ctx.shape, ctx.rd = n, (SB, R), rd
+        return z, pts
+
+    @staticmethod
+    def backward(ctx, grad_z, grad_pts):
+        SB, R = ctx.shape
+        rd, ctx.rd = ctx.rd, None
+        gz = None if grad_z is None else grad_z.float().contiguous()
+        gp = None if grad_pts is None else grad_pts.float().contiguous()
+        gw = torch.empty(SB, R, 3, device=rd.device, dtype=torch.float32)
+        _lib.call("avr_band_bwd", SB * R, ctx.n, _lib.ptr(rd), _lib.ptr(gz), _lib.ptr(gp), _lib.ptr(gw),
+                  _lib.stream_of(rd))
+        return gw, None, None, None, None, None
+
+
+def _band_on_hip(phi, world, ros, rds, n):
+    """The training band on HIP: with the net's HIP backward on (its torch reference keeps the torch ops)."""
+    return (getattr(phi, "hip_backward", False) and torch.is_grad_enabled() and world.requires_grad and world.is_cuda
+            and world.dtype == torch.float32 and not ros.requires_grad and not rds.requires_grad and 1 <= n <= 64)
+
+
 class _MarchTrain(torch.autograd.Function):
     """Autograd of the LSTM march (renderers.py:413-432 / :320-343) on HIP: forward avr_raymarch_train on the
     per-texel gate tables (latent^T W_ih^T, one library GEMM per scene), backward avr_raymarch_bwd (reverse
@@ -524,14 +561,25 @@ class AdaptiveVolumeRenderer(_LSTMMarch):
             main = torch.cuda.current_stream(dev)
             marched = torch.cuda.Event()
             marched.record(main)
-        # band around the marched distance (renderers.py:490-496); the sort is a no-op on stratified z
-        final_distance = (world[..., 0] - ros[..., 0]) / rds[..., 0]
+        # band around the marched distance (renderers.py:490-496); the sort rarely changes stratified z (only
+        # rounding can swap neighbours)
         u = None if noise is None else noise.get("band")
-        z_vals = sample_coarse(final_distance - self.epsilon, final_distance + self.epsilon, self.n_coarse, dev,
-                               noise=u)
-        z_vals_sorted, _ = torch.sort(z_vals, dim=-1)
+        band = None
+        if _band_on_hip(phi, world, ros, rds, self.n_coarse):   # training: sampling, sort and band points in one launch
+            if u is None:
+                u = _noise((SB, num_rays, self.n_coarse), world, "rand")   # sample_coarse's draw
+            z_vals_sorted, band = _Band.apply(world, ros, rds, u, self.epsilon, self.n_coarse)
+        else:
+            final_distance = (world[..., 0] - ros[..., 0]) / rds[..., 0]
+            z_vals = sample_coarse(final_distance - self.epsilon, final_distance + self.epsilon, self.n_coarse, dev,
+                                   noise=u)
+            z_vals_sorted, _ = torch.sort(z_vals, dim=-1)
         fuse = (SB == 1 and not torch.is_grad_enabled() and hasattr(phi, "can_fuse") and phi.can_fuse(xy_pix))
-        if fuse:
+        if band is not None:
+            vd = rds.reshape(SB * num_rays, 1, 3).expand(SB * num_rays, self.n_coarse, 3)
+            field = phi(band.reshape(SB, -1, 3), coarse=False, viewdirs=vd.reshape(SB, -1, 3),
+                        return_features=False).reshape(SB, num_rays, self.n_coarse, 4)
+        elif fuse:
             field = phi.fused().forward_rays(ros[0], rds[0], z_vals_sorted[0], False).reshape(SB, num_rays,
                                                                                                self.n_coarse, 4)
         else:

@@ -607,6 +607,62 @@ __global__ void __launch_bounds__(256) sample_fine_kernel(
   for (int k = lane; k < Ntot; k += 64) out[k] = sbuf[k];
 }
 
+// AdaptiveVolumeRenderer's band in training (renderers.py:490-496 and the band points, :497-508): per ray the
+// marched distance d = (world_x - ro_x) / rd_x, z_i = (near + span * (i / n)) + (noise_i * span) / n with near =
+// d - eps, far = d + eps, span = far - near (sample_coarse's fp32 operations, renderers.py:10-14, in torch's
+// order), z sorted ascending (torch.sort: rounding can swap neighbours), pts = ro + rd * z. One thread per ray.
+constexpr int kBandMax = 64;
+
+__global__ void __launch_bounds__(256) band_fwd_kernel(int64_t R, int n, const float* __restrict__ world,
+                                                       const float* __restrict__ ro, const float* __restrict__ rd,
+                                                       const float* __restrict__ noise, float eps,
+                                                       float* __restrict__ z, float* __restrict__ pts) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= R) return;
+  const float o0 = ro[3 * r], o1 = ro[3 * r + 1], o2 = ro[3 * r + 2];
+  const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
+  const float d = fdiv(fsub(world[3 * r], o0), d0);
+  const float near_ = fsub(d, eps), far_ = fadd(d, eps), span = fsub(far_, near_);
+  const float fn = (float)n;
+  float zz[kBandMax];
+  for (int i = 0; i < n; ++i) {
+    const float v = fadd(fadd(near_, fmul(span, fdiv((float)i, fn))), fdiv(fmul(noise[r * n + i], span), fn));
+    int k = i;
+    for (; k > 0 && v < zz[k - 1]; --k) zz[k] = zz[k - 1];   // insertion: ascending, ties keep their order
+    zz[k] = v;
+  }
+  for (int i = 0; i < n; ++i) {
+    const float v = zz[i];
+    z[r * n + i] = v;
+    float* p = pts + 3 * (r * n + i);
+    p[0] = fadd(o0, fmul(d0, v));
+    p[1] = fadd(o1, fmul(d1, v));
+    p[2] = fadd(o2, fmul(d2, v));
+  }
+}
+
+// Its adjoint: every z_i moves with d (dz_i / dd = 1: near and far both do, span does not), pts with z along rd, so
+// d loss / d world_x = sum_i (gz_i + gpts_i . rd) / rd_x; world_y, world_z and ro / rd get nothing.
+__global__ void __launch_bounds__(256) band_bwd_kernel(int64_t R, int n, const float* __restrict__ rd,
+                                                       const float* __restrict__ gz, const float* __restrict__ gpts,
+                                                       float* __restrict__ gworld) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= R) return;
+  const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) {
+    float g = gz ? gz[r * n + i] : 0.f;
+    if (gpts) {
+      const float* q = gpts + 3 * (r * n + i);
+      g = fadd(g, fadd(fadd(fmul(q[0], d0), fmul(q[1], d1)), fmul(q[2], d2)));
+    }
+    s = fadd(s, g);
+  }
+  gworld[3 * r] = fdiv(s, d0);
+  gworld[3 * r + 1] = 0.f;
+  gworld[3 * r + 2] = 0.f;
+}
+
 }  // namespace avr
 
 using namespace avr;
@@ -682,4 +738,26 @@ extern "C" int avr_sample_fine(const float* weights, const float* z_coarse, floa
       weights, z_coarse, near_, far_, n_rays, n_coarse, n_importance, n_depth, depth_std, u, u2, noise_depth, seed,
       offset, ray_ids, sort_n, z_sorted, idx, z_fine);
   return check_launch("sample_fine_kernel");
+}
+
+extern "C" int avr_band_fwd(int64_t n_rays, int n_samples, const float* world, const float* ro, const float* rd,
+                            const float* noise, float eps, float* z, float* pts, void* stream) {
+  AVR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples <= kBandMax, "avr_band_fwd: bad sizes (1..%d samples)",
+              kBandMax);
+  if (n_rays == 0) return AVR_OK;
+  AVR_REQUIRE(world && ro && rd && noise && z && pts, "avr_band_fwd: null pointer");
+  band_fwd_kernel<<<(unsigned)((n_rays + 255) / 256), 256, 0, as_stream(stream)>>>(n_rays, n_samples, world, ro, rd,
+                                                                                   noise, eps, z, pts);
+  return check_launch("band_fwd_kernel");
+}
+
+extern "C" int avr_band_bwd(int64_t n_rays, int n_samples, const float* rd, const float* grad_z,
+                            const float* grad_pts, float* grad_world, void* stream) {
+  AVR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples <= kBandMax, "avr_band_bwd: bad sizes (1..%d samples)",
+              kBandMax);
+  if (n_rays == 0) return AVR_OK;
+  AVR_REQUIRE(rd && grad_world, "avr_band_bwd: null pointer");
+  band_bwd_kernel<<<(unsigned)((n_rays + 255) / 256), 256, 0, as_stream(stream)>>>(n_rays, n_samples, rd, grad_z,
+                                                                                   grad_pts, grad_world);
+  return check_launch("band_bwd_kernel");
 }

@@ -90,6 +90,16 @@ int avr_rays_sample_coarse(const float* x_pix, const float* K, const float* c2w,
  * around the raymarched distance (renderers.py:492-493).                        */
 int avr_sample_coarse_rays(const float* near_, const float* far_, int64_t n_rays, int n_samples,
                            const float* noise, uint64_t seed, uint64_t offset, float* z, void* stream);
+/* ABI 16: AdaptiveVolumeRenderer's band for training (renderers.py:490-508): per ray d = (world_x - ro_x) / rd_x,
+ * z = sample_coarse(d - eps, d + eps, n_samples) with the given noise (renderers.py:10-14's fp32 operations in
+ * torch's order), sorted ascending per ray (torch.sort), and the band points pts = ro + rd * z. world / ro / rd
+ * (n_rays, 3), noise / z (n_rays, n_samples), pts (n_rays * n_samples, 3); n_samples <= 64. avr_band_bwd: its
+ * adjoint, grad_world (n_rays, 3) = ((sum_i grad_z_i + grad_pts_i . rd) / rd_x, 0, 0); grad_z or grad_pts may be
+ * NULL (no gradient).                                                                                            */
+int avr_band_fwd(int64_t n_rays, int n_samples, const float* world, const float* ro, const float* rd,
+                 const float* noise, float eps, float* z, float* pts, void* stream);
+int avr_band_bwd(int64_t n_rays, int n_samples, const float* rd, const float* grad_z, const float* grad_pts,
+                 float* grad_world, void* stream);
 
 /* sample_fine + sample_depth + clamp + sort(cat(...)) — renderers.py:27-54,
  * :56-66, :252-258.

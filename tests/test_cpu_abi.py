@@ -75,7 +75,7 @@ def test_lin_out_rows_argument_checks():
 
 
 def test_round6_point_gradient_entry_points_argument_checks():
-    """avr_lin_out_act_bwd_rows and avr_zfeature_grad_points (ABI 16): zero rows is a no-op; null pointers, a scene
+    """avr_lin_out_act_bwd_rows, avr_zfeature_grad_points and avr_band_fwd / _bwd (ABI 16): zero rows is a no-op; null pointers, a scene
     count outside 1..AVR_MAX_SCENES and gradient rows shorter than 3 + 6 num_freqs are refused before any HIP call."""
     import ctypes
     from avr import _lib
@@ -91,6 +91,13 @@ def test_round6_point_gradient_entry_points_argument_checks():
     assert b"bad sizes" in lib.avr_last_error_string()
     assert z(v, 1, None, 3, None, 39, 6, ctypes.c_float(3.14159), 0, None, None) == 1001
     assert b"null" in lib.avr_last_error_string()
+    # the training band (avr_band_fwd / avr_band_bwd): 1..64 samples, null pointers refused, no rays a no-op
+    assert lib.avr_band_fwd(0, 20, None, None, None, None, ctypes.c_float(0.05), None, None, None) == 0
+    assert lib.avr_band_fwd(4, 65, None, None, None, None, ctypes.c_float(0.05), None, None, None) == 1001
+    assert lib.avr_band_fwd(4, 20, None, None, None, None, ctypes.c_float(0.05), None, None, None) == 1001
+    assert lib.avr_band_bwd(0, 20, None, None, None, None, None) == 0
+    assert lib.avr_band_bwd(4, 0, None, None, None, None, None) == 1001
+    assert lib.avr_band_bwd(4, 20, None, None, None, None, None) == 1001
 
 
 def test_spade_bwd_rows_argument_checks():
