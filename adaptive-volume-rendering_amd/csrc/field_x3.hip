@@ -791,8 +791,10 @@ __global__ void __launch_bounds__(64 * NW, 1) field_x3_kernel(FieldArgs a) {
 // latent_table_split_kernel's exact products): table[t][texel][f] = sum_c W_t[f][c] latent[c][texel]
 // (+ the table's bias with use_spade), for the 64 texels of a workgroup. The latent columns (CHW: one
 // coalesced 256-B row per channel) are split into X under one power-of-two scale per workgroup, then
-// KCL = d_latent / 32 K-chunks of the hidden layers' GEMM; blockIdx.y = table.
-template <int FT, int NW>
+// KCL = d_latent / 32 K-chunks of the hidden layers' GEMM; blockIdx.y = table. ALL: one workgroup makes every
+// table of its texels from the one staged operand (the latent read once instead of once per table, and each
+// table's stores drain under the next table's GEMM), for grids that fill the chip without the table dimension.
+template <int FT, int NW, bool ALL = false>
 __global__ void __launch_bounds__(64 * NW, 1) table_x3_kernel(const float* __restrict__ packed, Layout L,
                                                               const float* __restrict__ latent, int HW, int d_latent,
                                                               float* __restrict__ table, int64_t lat_stride,
@@ -808,11 +810,13 @@ __global__ void __launch_bounds__(64 * NW, 1) table_x3_kernel(const float* __res
   float* red = lds + KCL * 2048;                   // after X (8 KiB per chunk)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, j = lane & 15;
-  const int t = blockIdx.y;
+  const int t_first = ALL ? 0 : blockIdx.y, t_end = ALL ? L.n_tables : t_first + 1;
   const int64_t t0 = (int64_t)blockIdx.x * kX3Samples;
-  const uint4* W = reinterpret_cast<const uint4*>(packed) + L.x3_tab[t] / 4 + 2 * 64 * FT * wid;
+  const auto wtab = [&](int t) {
+    return reinterpret_cast<const uint4*>(packed) + L.x3_tab[t] / 4 + 2 * 64 * FT * wid;
+  };
   FragX3 A0[FT];
-  prefetch_a<FT, TWO ? FT : kPrefetch>(A0, W, lane);
+  prefetch_a<FT, TWO ? FT : kPrefetch>(A0, wtab(t_first), lane);
   // lane = texel; wave w loads channel groups w, w + NW, ...
   const int64_t tx = t0 + lane < HW ? t0 + lane : HW - 1;
   floatx4 xv[MAXQ];
@@ -844,38 +848,59 @@ __global__ void __launch_bounds__(64 * NW, 1) table_x3_kernel(const float* __res
     }
   }
   lds_barrier();
-  floatx4 acc[FT][4];
-  gemm<FT, true, TWO>(acc, A0, W, KCL, 64 * NTT, X16, lane);
-  const float inv = 1.0f / (layer_scale(packed, L, kX3TabHdr + t) * s_x);
-  float* dst = table + (int64_t)t * HW * HID;
+  for (int t = t_first; t < t_end; ++t) {
+    floatx4 acc[FT][4];
+    gemm<FT, true, TWO>(acc, A0, wtab(t), KCL, 64 * NTT, X16, lane);
+    if (t + 1 < t_end) prefetch_a<FT, TWO ? FT : kPrefetch>(A0, wtab(t + 1), lane);   // under this epilogue
+    const float inv = 1.0f / (layer_scale(packed, L, kX3TabHdr + t) * s_x);
+    float* dst = table + (int64_t)t * HW * HID;
 #pragma unroll
-  for (int ft = 0; ft < FT; ++ft) {
-    const int f0 = 16 * (FT * wid + ft) + 4 * g;
-    const floatx4 b = L.spade ? *reinterpret_cast<const floatx4*>(packed + L.b_tab[t] + f0) : floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int ft = 0; ft < FT; ++ft) {
+      const int f0 = 16 * (FT * wid + ft) + 4 * g;
+      const floatx4 b =
+          L.spade ? *reinterpret_cast<const floatx4*>(packed + L.b_tab[t] + f0) : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int sg = 0; sg < 4; ++sg) {
-      const int64_t texel = t0 + 16 * sg + j;
-      if (texel < HW) *reinterpret_cast<floatx4*>(dst + texel * HID + f0) = acc[ft][sg] * inv + b;
+      for (int sg = 0; sg < 4; ++sg) {
+        const int64_t texel = t0 + 16 * sg + j;
+        if (texel < HW) *reinterpret_cast<floatx4*>(dst + texel * HID + f0) = acc[ft][sg] * inv + b;
+      }
     }
   }
+}
+
+template <int FT, int NW, bool ALL>
+static int launch_table_x3_k(const float* packed, const Layout& L, const float* latent, int HW, int d_latent,
+                             float* table, int n_scenes, hipStream_t s) {
+  const size_t shm = (size_t)(d_latent / 32) * 8192 + 64;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&table_x3_kernel<FT, NW, ALL>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 8192 * 4 + 64) != hipSuccess)
+      return fail(AVR_E_HIP, "table_x3_kernel: cannot set dynamic LDS");
+    attr = true;
+  }
+  const dim3 grid((unsigned)((HW + kX3Samples - 1) / kX3Samples), ALL ? 1u : (unsigned)L.n_tables, (unsigned)n_scenes);
+  const int64_t tab_stride = (int64_t)(L.n_tables > 0 ? L.n_tables : 1) * HW * (16 * FT * NW);
+  table_x3_kernel<FT, NW, ALL><<<grid, 64 * NW, shm, s>>>(packed, L, latent, HW, d_latent, table,
+                                                          (int64_t)d_latent * HW, tab_stride);
+  return check_launch("table_x3_kernel");
+}
+
+// every table per workgroup once the texel blocks alone give a workgroup to each CU (AVR_TABLE_ALL=0|1 forces
+// the choice, for A/B)
+static bool table_all(int64_t blocks, int n_tables) {
+  const char* e = getenv("AVR_TABLE_ALL");
+  if (e) return e[0] == '1' && n_tables > 1;
+  return n_tables > 1 && blocks >= 256;
 }
 
 template <int FT, int NW>
 static int launch_table_x3(const float* packed, const Layout& L, const float* latent, int HW, int d_latent,
                            float* table, int n_scenes, hipStream_t s) {
-  const size_t shm = (size_t)(d_latent / 32) * 8192 + 64;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&table_x3_kernel<FT, NW>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 8192 * 4 + 64) != hipSuccess)
-      return fail(AVR_E_HIP, "table_x3_kernel: cannot set dynamic LDS");
-    attr = true;
-  }
-  const dim3 grid((unsigned)((HW + kX3Samples - 1) / kX3Samples), (unsigned)L.n_tables, (unsigned)n_scenes);
-  const int64_t tab_stride = (int64_t)(L.n_tables > 0 ? L.n_tables : 1) * HW * (16 * FT * NW);
-  table_x3_kernel<FT, NW><<<grid, 64 * NW, shm, s>>>(packed, L, latent, HW, d_latent, table, (int64_t)d_latent * HW,
-                                                     tab_stride);
-  return check_launch("table_x3_kernel");
+  const int64_t blocks = (int64_t)((HW + kX3Samples - 1) / kX3Samples) * n_scenes;
+  if (table_all(blocks, L.n_tables))
+    return launch_table_x3_k<FT, NW, true>(packed, L, latent, HW, d_latent, table, n_scenes, s);
+  return launch_table_x3_k<FT, NW, false>(packed, L, latent, HW, d_latent, table, n_scenes, s);
 }
 
 int dispatch_table_x3(const float* packed, const Layout& L, const float* latent, int HW, int d_latent, int d_hidden,
