@@ -426,13 +426,13 @@ class FusedField:
         entry.tables[sb] = (key, table, lat, _stamp(table))  # holding `lat` keeps its address from being reused
         return table
 
-    def tables_batch(self, coarse, n_scenes, fast=False, bn_fold=True):
+    def tables_batch(self, coarse, n_scenes, fast=False, bn_fold=True, entry=None):
         """The lin_z tables of scenes 0 .. n_scenes-1 back to back, (n_scenes,
         max(n_tables, 1), H*W, d_hidden): one buffer for the multi-scene launches.
         fast (the training path, which recomputes them every step): on the split-fp16
         GEMM (table_x3_kernel); otherwise exact fp32 products. bn_fold: which blob's
-        cache holds them (packed())."""
-        entry = self.packed(coarse, bn_fold)
+        cache holds them (packed()); entry: that packed() result when the caller has it."""
+        entry = entry or self.packed(coarse, bn_fold)
         lat = self.net.encoder.latent
         key = (n_scenes, bool(fast), _PARAM_GEN[0], lat.data_ptr(), lat._version, tuple(lat.shape))
         cache = entry.__dict__.setdefault("batch_tables", {})
@@ -684,7 +684,7 @@ class _FieldTrain(torch.autograd.Function):
         p = xyz.detach().to(F32).contiguous()
         v = viewdirs.reshape(SB, B, 3).detach().to(F32).contiguous()
         require_device(p, v)
-        tables = fused.tables_batch(coarse, SB, fast=True)
+        tables = fused.tables_batch(coarse, SB, fast=True, entry=entry)
         masks = []
         for g0 in range(0, SB, _lib.AVR_MAX_SCENES):     # one launch per group of scenes
             n = min(_lib.AVR_MAX_SCENES, SB - g0)
@@ -739,11 +739,11 @@ class _FieldTrain(torch.autograd.Function):
         # features (avr_latent_features, row-major) and z_feature (the training forward
         # stored it, padded to 16 B, with its max in act_max[n_l])
         d_in = dims.d_in
+        p = xyz.detach().to(F32).contiguous()
         with torch.no_grad():
             lat_feat = torch.empty(Mt, net.d_latent, device=dev, dtype=F32)
             if SB <= latent.shape[0]:   # every scene its own map: one launch per AVR_MAX_SCENES scenes
                 hwc = fused.latent_hwc_all(latent)
-                p = xyz.detach().to(F32).contiguous()
                 for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
                     n = min(_lib.AVR_MAX_SCENES, SB - g0)
                     views = fused.views(range(g0, g0 + n))
@@ -792,7 +792,6 @@ class _FieldTrain(torch.autograd.Function):
             if not net.stop_encoder_grad:
                 with torch.no_grad():
                     d_look = torch.empty(Mt, 3, device=dev, dtype=F32)
-                    p = xyz.detach().to(F32).contiguous()
                     tabs = ctx.tables
                     via_tables = (not dims.spade and nz <= _lib.AVR_LOOKUP_GRAD_TERMS and tabs.shape[0] == SB
                                   and os.environ.get("AVR_POINT_GRAD_VIA_FEATURES") != "1")
@@ -833,7 +832,6 @@ class _FieldTrain(torch.autograd.Function):
                     d_zf = G[2 * nb] @ P["lin_in.weight"].detach()[:, :n_pe]
                     if d_look is None:
                         d_look = torch.empty(Mt, 3, device=dev, dtype=F32)
-                        p = xyz.detach().to(F32).contiguous()
                     for g0 in range(0, SB, _lib.AVR_MAX_SCENES):
                         n = min(_lib.AVR_MAX_SCENES, SB - g0)
                         views = fused.views(range(g0, g0 + n))
