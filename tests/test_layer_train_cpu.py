@@ -254,3 +254,31 @@ def test_fused_field_parameter_slots_follow_replacements():
     del tmp
     gc.collect()
     assert len(fused._slots) == n - 1
+
+
+def test_fused_field_view_arrays_follow_the_sources():
+    """FusedField.views (the cached ViewDesc array of a multi-scene launch, round 6): one array object while the
+    source-view tensors are unchanged, holding view(i, ns) of each index; a new one after an in-place pose update, a
+    replaced focal tensor or invalidate(); invalidate(views=False) (GraphedTrainStep before a capture) keeps it."""
+    net = _net(16, 3, 64, 2, 1, 1, False, "average")
+    net.poses = net.poses.repeat(3, 1, 1).clone()
+    net.poses[:, 0, 3] += torch.tensor([0.0, 0.1, 0.2])
+    net.focal, net.c = net.focal.repeat(3, 1).clone(), net.c.repeat(3, 1).clone()
+    fused = net.fused()
+    a = fused.views(range(3))
+    assert fused.views(range(3)) is a and len(a) == 3
+    assert [round(a[i].poses[3], 5) for i in range(3)] == [round(float(net.poses[i, 0, 3]), 5) for i in range(3)]
+    b = fused.views(range(0, 3, 2))
+    assert b is not a and [round(b[i].poses[3], 5) for i in range(2)] == [round(a[0].poses[3], 5),
+                                                                          round(a[2].poses[3], 5)]
+    with torch.no_grad():
+        net.poses[1, 0, 3] += 1.0
+    a2 = fused.views(range(3))
+    assert a2 is not a and abs(a2[1].poses[3] - float(net.poses[1, 0, 3])) < 1e-6
+    net.focal = net.focal * 2.0
+    a3 = fused.views(range(3))
+    assert a3 is not a2 and abs(a3[0].focal[0] - float(net.focal[0, 0])) < 1e-4
+    fused.invalidate(views=False)
+    assert fused.views(range(3)) is a3
+    fused.invalidate()
+    assert fused.views(range(3)) is not a3
