@@ -160,6 +160,7 @@ torch.nn.modules.module.register_module_module_registration_hook(_module_registe
 # keys of the caches below would not see it (the blob would keep the old weights). The count is part of every key;
 # GraphedTrainStep advances it after each replay (a captured optimizer step runs no host hook).
 _PARAM_GEN = [0]
+_EXPLICIT_GEN = [0]   # bump_param_generation() calls alone: the key of latent maps no optimizer can hold
 
 
 def _optimizer_stepped(optimizer, args, kwargs):
@@ -173,6 +174,7 @@ def bump_param_generation():
     """Invalidate every FusedField cache entry derived from parameters or the latent map (after an update the
     version counters do not record: a replayed optimizer step, a write through .data)."""
     _PARAM_GEN[0] += 1
+    _EXPLICIT_GEN[0] += 1
 
 
 def param_generation():
@@ -239,6 +241,7 @@ class FusedField:
         self.precision = precision
         self.net = net
         self._packed = {}     # coarse(bool) -> (key, _Packed)
+        self._pack_args = {}  # coarse(bool) -> (pointer key, blob floats, ResnetFCWeights, kept tensors)
         self._view_cache = {}
         self._views_cache = {}    # (range, ns) -> ViewDesc arrays (views())
         self._latent_cache = {}   # per latent version: channels-last copies, max |latent| (both MLPs share them)
@@ -251,6 +254,7 @@ class FusedField:
         the host-side view descriptors (avr.graphs.GraphedTrainStep before a capture: building one reads the poses
         back to the host, which a capture cannot do)."""
         self._packed.clear()
+        self._pack_args.clear()
         if views:
             self._view_cache.clear()
             self._views_cache.clear()
@@ -272,7 +276,10 @@ class FusedField:
         return out
 
     def _latent_cached(self, what, latent, make):
-        key = (_PARAM_GEN[0], latent.data_ptr(), latent._version, tuple(latent.shape))
+        # the optimizer-step count matters only for a latent an optimizer can hold (a leaf that requires grad): a
+        # fixed or encoder-produced map keeps its copies across steps (its version counter sees in-place writes)
+        gen = _PARAM_GEN[0] if (latent.is_leaf and latent.requires_grad) else (-1, _EXPLICIT_GEN[0])
+        key = (gen, latent.data_ptr(), latent._version, tuple(latent.shape))
         hit = self._latent_cache.get(what)
         if hit is not None and hit[0] == key:
             _join(hit[3], hit[1])
@@ -349,16 +356,29 @@ class FusedField:
         dims = self.dims(mlp)
         if not bn_fold:
             dims.bn, dims.precision = 0, _lib.FIELD_X3
+        # an optimizer step updates the parameters in place: the same tensors at the same addresses, so the last
+        # build's weight pointers, blob size and kept tensors serve again and only the pack launch reruns (when
+        # every pointer was a parameter or buffer read in place; derived tensors -- the eval-BN folds, dtype
+        # conversions -- are rebuilt every time)
+        args_key = (id(mlp), tuple(pv[0] for pv in key[2][1:]), bytes(dims))
+        args = self._pack_args.get(slot)
+        if args is not None and args[0] == args_key:
+            _, n, w, keep = args
+            packed = torch.empty(n, device=params[0].device, dtype=F32)
+            call("avr_field_pack", ctypes.byref(dims), ctypes.byref(w), ptr(packed), stream_of(packed))
+            return self._store_packed(slot, key, dims, packed, keep, w)
         n = ctypes.c_int64(0)
         _lib.check(_lib.load().avr_field_packed_floats(ctypes.byref(dims), ctypes.byref(n)), "avr_field_packed_floats")
         dev = params[0].device
         packed = torch.empty(n.value, device=dev, dtype=F32)
         w = ResnetFCWeights()
         keep = []
+        derived = [False]
 
         def P(t):
             if not (t.dtype == F32 and t.is_contiguous()):   # (fp32 contiguous parameters: read in place)
                 t = t.detach().to(F32).contiguous()
+                derived[0] = True
             keep.append(t)
             return t.data_ptr()
 
@@ -384,6 +404,13 @@ class FusedField:
                 w.scale_z_w[b], w.scale_z_b[b] = P(mlp.scale_z[b].weight), P(mlp.scale_z[b].bias)
         require_device(*keep)
         call("avr_field_pack", ctypes.byref(dims), ctypes.byref(w), ptr(packed), stream_of(packed))
+        if dims.bn or derived[0]:
+            self._pack_args.pop(slot, None)
+        else:
+            self._pack_args[slot] = (args_key, n.value, w, keep)
+        return self._store_packed(slot, key, dims, packed, keep, w)
+
+    def _store_packed(self, slot, key, dims, packed, keep, w):
         entry = _Packed(dims, packed, None)
         entry._keep = keep
         entry.weights = w

@@ -4,6 +4,7 @@ All tensors are device tensors owned by PyTorch; every launch is enqueued on
 torch's current HIP stream. No function here has a host/CPU implementation.
 """
 import ctypes
+import functools
 
 import torch
 
@@ -435,7 +436,11 @@ _DW_TILE = 256        # avr_weight_grads output tile (weight_grad.hip kDwTile), 
 def _wgrad_splits(tiles, n_rows, dev):
     """K-split of avr_weight_grads: the grid (tiles x splits workgroups, one per
     CU) should end in full rounds, with K-ranges of at least 2048 rows."""
-    slots = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _wgrad_splits_cu(tiles, n_rows, torch.cuda.get_device_properties(dev).multi_processor_count)
+
+
+@functools.lru_cache(maxsize=256)
+def _wgrad_splits_cu(tiles, n_rows, slots):
     best, best_eff = 1, 0.0
     for n in range(1, 65):
         if n > 1 and n_rows < 2048 * n:
@@ -475,10 +480,14 @@ def weight_grads(layers, n_rows, n_split=None):
         sizes = [n_split * l[0].shape[1] * (l[1].shape[1] + (1 if l[4] else 0)) for l in chunk]
         flat = torch.empty(sum(sizes), device=dev, dtype=torch.float32)
         dw_ptrs, db_ptrs = (ctypes.c_void_p * len(chunk))(), (ctypes.c_void_p * len(chunk))()
-        # every dW / db of the chunk as views of one allocation (two allocations per layer were host time)
-        osz = [l[0].shape[1] * l[1].shape[1] + (l[0].shape[1] if l[4] else 0) for l in chunk]
-        outs = torch.empty(sum(osz), device=dev, dtype=torch.float32).split(osz)
-        res, off = [], 0
+        # every dW / db of the chunk as views of one allocation, cut by one split (two allocations per layer, then
+        # two slices per layer, were host time); the partials are addressed by offset, no view of them is needed
+        pieces = []
+        for l in chunk:
+            pieces += [l[0].shape[1] * l[1].shape[1], l[0].shape[1]] if l[4] else [l[0].shape[1] * l[1].shape[1]]
+        outs = torch.empty(sum(pieces), device=dev, dtype=torch.float32).split(pieces)
+        flat_p = flat.data_ptr()
+        res, off, vi = [], 0, 0
         for k, (g, x, gmax, xmax, want_bias, *bn) in enumerate(chunk):
             O, I = g.shape[1], x.shape[1]
             bn = bn[0] if bn else None
@@ -492,14 +501,15 @@ def weight_grads(layers, n_rows, n_split=None):
             if bn is not None and any(t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != I
                                       or t.data_ptr() % 16 for t in bn):
                 raise _lib.AVRError("weight_grads: the BatchNorm transform takes (in,) fp32 mu / scale / shift")
-            part = flat[off:off + n_split * O * I]
-            bpart = flat[off + n_split * O * I:off + sizes[k]] if want_bias else None
+            part_p = flat_p + 4 * off
+            bpart_p = part_p + 4 * n_split * O * I if want_bias else 0
             off += sizes[k]
             arr[k] = _lib.WGradLayer(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), O, I, gmax.data_ptr(),
-                                     xmax.data_ptr(), part.data_ptr(), 0 if bpart is None else bpart.data_ptr(),
+                                     xmax.data_ptr(), part_p, bpart_p,
                                      *([t.data_ptr() for t in bn] if bn is not None else [None] * 3), int(relu))
-            dw = outs[k][:O * I].view(O, I)
-            db = outs[k][O * I:] if want_bias else None
+            dw = outs[vi].view(O, I)
+            db = outs[vi + 1] if want_bias else None
+            vi += 2 if want_bias else 1
             dw_ptrs[k], db_ptrs[k] = dw.data_ptr(), (db.data_ptr() if want_bias else None)
             res.append((dw, db))
         call("avr_weight_grads", arr, len(chunk), n_rows, n_split, stream)

@@ -101,6 +101,15 @@ def volume_integral(z_vals, sigmas, radiances, white_back=True, infinity=1.8) ->
     return rgb.reshape(SB, R, 3), dist.reshape(SB, R, 1), w.reshape(SB, R, N, 1)
 
 
+def volume_integral_packed(z_vals, field, white_back=True, infinity=1.8):
+    """volume_integral(z_vals, field[..., 3:], field[..., :3]) for a field output (SB,R,N,4) in its own [r, g, b,
+    sigma] layout -- the layout volume_integral's cat builds -- so the same composite on the same values, without
+    the cat in the forward and the two slices' zero-padded adjoints and their sum in the backward."""
+    SB, R, N = z_vals.shape
+    rgb, dist, w = ops.composite(z_vals.reshape(SB * R, N), field.reshape(SB * R, N, 4), white_back, infinity)
+    return rgb.reshape(SB, R, 3), dist.reshape(SB, R, 1), w.reshape(SB, R, N, 1)
+
+
 # ---------------------------------------------------------------- renderer
 class VolumeRenderer(nn.Module):
     """renderers.py:121-289: coarse stratified pass -> inverse-CDF fine pass
@@ -594,8 +603,8 @@ class AdaptiveVolumeRenderer(_LSTMMarch):
                 t.record_stream(side)
             with torch.cuda.stream(side):
                 output_coarse, depth_coarse = coarse_pass()
-        rgb, distance_map, _ = volume_integral(z_vals_sorted, field[..., 3:], field[..., :3],
-                                               white_back=self.white_back)
+        # renderers.py:503: volume_integral(z, sigma, rad) with sigma = field[..., 3:], rad = field[..., :3]
+        rgb, distance_map, _ = volume_integral_packed(z_vals_sorted, field, white_back=self.white_back)
         depth_map = ops.depth_from_world(ros, rds, distance_map.reshape(SB, num_rays), c2w_info)
         if side is not None:   # join: the coarse outputs are read on the caller's stream from here on
             main.wait_stream(side)
