@@ -72,7 +72,7 @@ def _checked(name, fn):
 
 OPS = ("world_rays", "rays_sample_coarse", "composite_depth", "depth_from_world_fwd", "sample_coarse", "sample_fine",
        "composite_fwd", "composite_bwd", "march_fine", "sample_coarse_rays", "depth_of_points_fwd", "raymarch",
-       "weight_grads", "latent_features")
+       "weight_grads", "weight_grads_specs", "latent_features")
 FIELD_METHODS = ("forward_rays", "forward_rays_batch", "forward_points_multiview", "forward_points", "forward_train")
 FUNCTIONS = (("ops", "_Depth"), ("ops", "_Composite"), ("ops", "_DepthOfPoints"), ("field", "_FieldTrain"),
              ("bn_train", "_FieldTrainBN"), ("renderers", "_MarchTrain"),

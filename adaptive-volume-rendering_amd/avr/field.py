@@ -734,7 +734,7 @@ class _FieldTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
-        from .ops import latent_features, lin_out_act_bwd, weight_grads
+        from .ops import latent_features, lin_out_act_bwd, weight_grads_specs
         xyz, viewdirs, latent, out, *params = ctx.saved_tensors
         fused, entry, names = ctx.fused, ctx.entry, ctx.names
         net = fused.net
@@ -783,17 +783,25 @@ class _FieldTrain(torch.autograd.Function):
                                     hwc=fused.latent_hwc(latent, s))
         lat_max = fused.latent_max_bits(latent)   # |interpolated latent| <= max |latent| (convex blend)
         zf_max = act_max[n_l:n_l + 1]
-        # every layer's views in one call each (a slice per layer and operand was ~0.1 ms of host time per call)
-        Gl, Al, gm, am = G.unbind(0), act.unbind(0), g_max.split(1), act_max.split(1)
-        Gz = [Gl[2 * b - 1] if b > 0 else Gl[2 * nb] for b in range(nz)]
-        layers = [(Gl[k], Al[k], gm[k], am[k], True) for k in range(2 * nb)]
-        for b in range(nz):
-            layers.append((Gz[b], lat_feat, gm[2 * b - 1 if b > 0 else 2 * nb], lat_max, False))
-        layers.append((Gl[2 * nb], zf, gm[2 * nb], zf_max, True))
+        Gz = [G[2 * b - 1] if b > 0 else G[2 * nb] for b in range(nz)]
         # lin_out (4 outputs): d out through sigmoid / relu (torch: g * (1 - y) * y, g * (y > 0)), with its max
         d4, d4_max = lin_out_act_bwd(grad_out, out)
-        layers.append((d4, Al[2 * nb], d4_max, am[2 * nb], True))
-        res = weight_grads(layers, Mt)
+        # the layers of the batched weight-gradient launch addressed by offset into the buffers this Function
+        # allocated (row strides H, d_latent, zs, 4; 16-B aligned by construction): the fc layers (G_k, act_k),
+        # lin_z[b] (the gradient at block b's input, the interpolated latent), lin_in (the gradient at the first
+        # block's input, z_feature), lin_out (d4, the last block's output) -- no per-layer views or checks
+        Gp, Ap, gmp, amp, lay = G.data_ptr(), act.data_ptr(), g_max.data_ptr(), act_max.data_ptr(), Mt * H * 4
+        specs = [(Gp + k * lay, H, Ap + k * lay, H, H, H, gmp + 4 * k, amp + 4 * k, True, None, None, None, 0)
+                 for k in range(2 * nb)]
+        for b in range(nz):
+            k = 2 * b - 1 if b > 0 else 2 * nb
+            specs.append((Gp + k * lay, H, lat_feat.data_ptr(), net.d_latent, H, net.d_latent, gmp + 4 * k,
+                          lat_max.data_ptr(), False, None, None, None, 0))
+        specs.append((Gp + 2 * nb * lay, H, zf.data_ptr(), zf.shape[1], H, zf.shape[1], gmp + 8 * nb,
+                      zf_max.data_ptr(), True, None, None, None, 0))
+        specs.append((d4.data_ptr(), 4, Ap + 2 * nb * lay, H, 4, H, d4_max.data_ptr(), amp + 8 * nb, True, None, None,
+                      None, 0))
+        res = weight_grads_specs(specs, Mt, dev, stream_of(G))
         grads = {"lin_out.weight": res[-1][0], "lin_out.bias": res[-1][1]}
         res = res[:-1]
         for b in range(nb):

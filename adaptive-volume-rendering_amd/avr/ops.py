@@ -468,45 +468,56 @@ def weight_grads(layers, n_rows, n_split=None):
     if n_rows == 0:
         return [(torch.zeros(l[0].shape[1], l[1].shape[1], device=dev), torch.zeros(l[0].shape[1], device=dev) if l[4] else None)
                 for l in layers]
-    tiles = sum(-(-l[0].shape[1] // _DW_TILE) * -(-l[1].shape[1] // _DW_TILE) for l in layers)
+    specs = []
+    for g, x, gmax, xmax, want_bias, *bn in layers:
+        O, I = g.shape[1], x.shape[1]
+        bn = bn[0] if bn else None
+        relu = isinstance(bn, str)
+        if relu and bn != "relu":
+            raise _lib.AVRError(f"weight_grads: unknown input transform {bn!r}")
+        bn = None if relu else bn
+        for t in (g, x):
+            if t.dtype != torch.float32 or t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+                raise _lib.AVRError("weight_grads: operands must be fp32 rows, 16-B aligned, unit column stride")
+        if bn is not None and any(t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != I
+                                  or t.data_ptr() % 16 for t in bn):
+            raise _lib.AVRError("weight_grads: the BatchNorm transform takes (in,) fp32 mu / scale / shift")
+        specs.append((g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), O, I, gmax.data_ptr(), xmax.data_ptr(),
+                      bool(want_bias), *([t.data_ptr() for t in bn] if bn is not None else [None] * 3), int(relu)))
+    return weight_grads_specs(specs, n_rows, dev, stream_of(layers[0][0]), n_split)
+
+
+def weight_grads_specs(specs, n_rows, dev, stream, n_split=None):
+    """weight_grads on layers given as plain integers -- (grad ptr, grad row stride, input ptr, input row stride,
+    out, in, grad_max ptr, input_max ptr, want_bias, mu ptr, scale ptr, shift ptr, input relu) -- for callers
+    that own the row buffers and address their layers by offset (the fused field's training backward: no
+    per-layer views, checks or tensor calls). Same launches and results as weight_grads."""
+    if n_rows == 0:
+        return [(torch.zeros(s[4], s[5], device=dev), torch.zeros(s[4], device=dev) if s[8] else None)
+                for s in specs]
     if n_split is None:
-        n_split = _wgrad_splits(tiles, n_rows, dev)
+        n_split = _wgrad_splits(sum(-(-s[4] // _DW_TILE) * -(-s[5] // _DW_TILE) for s in specs), n_rows, dev)
     out = []
-    stream = stream_of(layers[0][0])
-    for base in range(0, len(layers), _lib.AVR_WGRAD_MAX_LAYERS):
-        chunk = layers[base:base + _lib.AVR_WGRAD_MAX_LAYERS]
+    for base in range(0, len(specs), _lib.AVR_WGRAD_MAX_LAYERS):
+        chunk = specs[base:base + _lib.AVR_WGRAD_MAX_LAYERS]
         arr = (_lib.WGradLayer * len(chunk))()
         # the partials of the whole chunk in one buffer (every piece a multiple of 16 B: O, I multiples of 4)
-        sizes = [n_split * l[0].shape[1] * (l[1].shape[1] + (1 if l[4] else 0)) for l in chunk]
+        sizes = [n_split * s[4] * (s[5] + (1 if s[8] else 0)) for s in chunk]
         flat = torch.empty(sum(sizes), device=dev, dtype=torch.float32)
         dw_ptrs, db_ptrs = (ctypes.c_void_p * len(chunk))(), (ctypes.c_void_p * len(chunk))()
         # every dW / db of the chunk as views of one allocation, cut by one split (two allocations per layer, then
         # two slices per layer, were host time); the partials are addressed by offset, no view of them is needed
         pieces = []
-        for l in chunk:
-            pieces += [l[0].shape[1] * l[1].shape[1], l[0].shape[1]] if l[4] else [l[0].shape[1] * l[1].shape[1]]
+        for s in chunk:
+            pieces += [s[4] * s[5], s[4]] if s[8] else [s[4] * s[5]]
         outs = torch.empty(sum(pieces), device=dev, dtype=torch.float32).split(pieces)
         flat_p = flat.data_ptr()
         res, off, vi = [], 0, 0
-        for k, (g, x, gmax, xmax, want_bias, *bn) in enumerate(chunk):
-            O, I = g.shape[1], x.shape[1]
-            bn = bn[0] if bn else None
-            relu = isinstance(bn, str)
-            if relu and bn != "relu":
-                raise _lib.AVRError(f"weight_grads: unknown input transform {bn!r}")
-            bn = None if relu else bn
-            for t in (g, x):
-                if t.dtype != torch.float32 or t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
-                    raise _lib.AVRError("weight_grads: operands must be fp32 rows, 16-B aligned, unit column stride")
-            if bn is not None and any(t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != I
-                                      or t.data_ptr() % 16 for t in bn):
-                raise _lib.AVRError("weight_grads: the BatchNorm transform takes (in,) fp32 mu / scale / shift")
+        for k, (gp, ldg, xp, ldx, O, I, gmp, xmp, want_bias, mu, sc, sh, relu) in enumerate(chunk):
             part_p = flat_p + 4 * off
-            bpart_p = part_p + 4 * n_split * O * I if want_bias else 0
             off += sizes[k]
-            arr[k] = _lib.WGradLayer(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), O, I, gmax.data_ptr(),
-                                     xmax.data_ptr(), part_p, bpart_p,
-                                     *([t.data_ptr() for t in bn] if bn is not None else [None] * 3), int(relu))
+            arr[k] = _lib.WGradLayer(gp, ldg, xp, ldx, O, I, gmp, xmp, part_p,
+                                     part_p + 4 * n_split * O * I if want_bias else 0, mu, sc, sh, relu)
             dw = outs[vi].view(O, I)
             db = outs[vi + 1] if want_bias else None
             vi += 2 if want_bias else 1
