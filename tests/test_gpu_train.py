@@ -708,3 +708,56 @@ def test_fused_optimizer_step_reaches_the_field():
         a = net(xyz, coarse=True, viewdirs=vd)
         b = net.forward_torch(xyz, True, vd)
     np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), atol=1e-4)
+
+
+def test_weight_grads_specs_bit_equal_to_tensor_api():
+    """ops.weight_grads_specs (the layers as offsets into caller-owned buffers: _FieldTrain.backward's route) and
+    ops.weight_grads (tensor views, checked) are one launch sequence: bit-equal dW / db on layers cut from one
+    (layers, M, H) buffer, a narrow layer and one without bias."""
+    from avr import ops
+    M, H, nl = 777, 128, 3
+    g = torch.Generator(device="cpu").manual_seed(5)
+    G = (torch.randn(nl, M, H, generator=g) * 1e-3).to(DEV)
+    A = torch.relu(torch.randn(nl, M, H, generator=g)).to(DEV)
+    Z = torch.randn(M, 44, generator=g).to(DEV)
+    gm = torch.stack([ops._max_bits(G[k])[0] for k in range(nl)])
+    am = torch.stack([ops._max_bits(A[k])[0] for k in range(nl)] + [ops._max_bits(Z)[0]])
+    lay = [(G[k], A[k], gm[k:k + 1], am[k:k + 1], True) for k in range(nl)]
+    lay.append((G[0], Z, gm[0:1], am[nl:nl + 1], False))
+    ref = ops.weight_grads(lay, M)
+    sz, Gp, Ap = M * H * 4, G.data_ptr(), A.data_ptr()
+    specs = [(Gp + k * sz, H, Ap + k * sz, H, H, H, gm.data_ptr() + 4 * k, am.data_ptr() + 4 * k, True, None,
+              None, None, 0) for k in range(nl)]
+    specs.append((Gp, H, Z.data_ptr(), 44, H, 44, gm.data_ptr(), am.data_ptr() + 4 * nl, False, None, None, None,
+                  0))
+    got = ops.weight_grads_specs(specs, M, DEV, ops.stream_of(G))
+    for (dw0, db0), (dw1, db1) in zip(ref, got):
+        assert torch.equal(dw0, dw1)
+        assert (db0 is None) == (db1 is None) and (db0 is None or torch.equal(db0, db1))
+
+
+def test_repack_after_in_place_update_matches_fresh_pack():
+    """FusedField.packed() reuses the last build's weight pointers when an optimizer step updated the parameters in
+    place (only the pack launch reruns): the field it evaluates must equal, bit for bit, that of a FusedField
+    packing from scratch (the blobs' unwritten padding is not compared), and a replaced parameter tensor must be
+    seen."""
+    from avr.field import FusedField
+    net = _net(64, 3, 64, (8, 8))
+    fused = net.fused()
+    opt = torch.optim.Adam(net.mlp_coarse.parameters(), lr=1e-2)
+    xyz, vd, w = _points(1, 200, seed=31)
+    for _ in range(3):
+        opt.zero_grad()
+        (net(xyz, coarse=True, viewdirs=vd) * w).sum().backward()
+        opt.step()
+
+    def both():
+        with torch.no_grad():
+            return (fused.forward_points(xyz, vd, True),
+                    FusedField(net, fused.precision).forward_points(xyz, vd, True))
+    a, b = both()
+    assert torch.equal(a, b)
+    with torch.no_grad():   # a new tensor object for one parameter: new pointers, a full rebuild
+        net.mlp_coarse.lin_out.weight = torch.nn.Parameter(net.mlp_coarse.lin_out.weight * 2.0)
+    a2, b2 = both()
+    assert torch.equal(a2, b2) and not torch.equal(a2, a)
