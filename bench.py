@@ -868,6 +868,7 @@ def config5_leg(args, net, fused, K, device):
 
     def step():
         fused._packed.clear()
+        fused._pack_args.clear()
         with torch.no_grad():
             if sharded:
                 return render_sharded(render_fn, c2w, K, x_pix, timer=stimer)[1]
@@ -912,6 +913,7 @@ def config2_leg(args, net, fused, K, c2w, x_pix, device):
 
     def step():
         fused._packed.clear()
+        fused._pack_args.clear()
         with torch.no_grad():
             ro, rd, zc, _, _ = avr.ops.rays_sample_coarse(x_pix, K, c2w, 0.8, 1.8, args.n_coarse, seed=1234)
             rgb_c, _, _ = avr.ops.composite(zc, fused.forward_rays(ro[0], rd[0], zc, True), True, want_weights=False)
@@ -977,6 +979,7 @@ def fp32_leg(args, net, fused, timer, K, c2w, x_pix, device):
 
     def step():
         fused._packed.clear()
+        fused._pack_args.clear()
         with torch.no_grad():
             return rend(c2w, K, x_pix, net)[1]
 
@@ -1139,7 +1142,8 @@ def main():
         return rend(c, k, x, net, ray_ids=ray_ids, n_rays_total=n_rays_total)
 
     def step():
-        fused._packed.clear()       # per-scene prep inside the step: repack weights, rebuild lin_z tables
+        fused._packed.clear()       # per-scene prep inside the step: repack weights (from scratch), rebuild lin_z tables
+        fused._pack_args.clear()
         with torch.no_grad():
             if config == 5:
                 if use_dist:
